@@ -1,0 +1,118 @@
+"""CPU oracle (test infra): functional fp32 restatement of the reference
+relative-position Transformer (models/transformer/model_transformer.py:8-165).
+
+Parameters are a dict keyed by the reference's state_dict names; autograd
+provides the backward. Dropout is 0 (the parity fixtures are recorded with
+``cc.config.values.dropout = params.dropout = 0``).
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+META = 6  # metadata prefix length, hard-coded in generate_matrix (model_transformer.py:14)
+
+
+def allowed_mask(S: int) -> torch.Tensor:
+    """generate_matrix(n, 1) (model_transformer.py:8-16): row i sees j<=i and j<6."""
+    i = torch.arange(S)[:, None]
+    j = torch.arange(S)[None, :]
+    return (j <= i) | (j < META)
+
+
+def skew_index(S: int):
+    """Index form of HeadRelPos._rel_shift (model_transformer.py:84-90).
+
+    The reference pads a zero column in front of QR[S,S], re-views the
+    [S, S+1] buffer as [S+1, S] and drops the first row. Element (i, j) of the
+    result is therefore flat element f = (i+1)*S + j of the padded buffer:
+    row f // (S+1), padded column f % (S+1) (column 0 is the zero pad).
+    Returns (row, col, is_pad) index tensors into QR.
+    """
+    i = torch.arange(S)[:, None]
+    j = torch.arange(S)[None, :]
+    f = (i + 1) * S + j
+    row = f // (S + 1)
+    pc = f % (S + 1)
+    return row, (pc - 1).clamp(min=0), pc == 0
+
+
+def rel_head(x, wq, wk, wv, R, scale):
+    """One HeadRelPos (model_transformer.py:64-82): scores (q.k + skew(q.R)) * scale."""
+    B, S, _ = x.shape
+    q, k, v = x @ wq.t(), x @ wk.t(), x @ wv.t()
+    ac = q @ k.transpose(1, 2)
+    qr = q @ R[:S].t()                       # qr[b, i, r] = q_i . R[r]
+    row, col, pad = skew_index(S)
+    bd = qr[:, row, col].masked_fill(pad, 0.0)
+    s = (ac + bd) * scale
+    s = s.masked_fill(~allowed_mask(S), float("-inf"))
+    return torch.softmax(s, dim=-1) @ v
+
+
+def forward(p: dict, idx: torch.Tensor, meta: torch.Tensor, n_layer: int, n_heads: int) -> torch.Tensor:
+    """Transformer.forward (model_transformer.py:149-165): meta rows first,
+    pre-LN blocks, LN_f, lm_head, keep the last T rows."""
+    B, T = idx.shape
+    x = torch.cat([p["metadata_embedding_table.weight"][meta], p["token_embedding_table.weight"][idx]], dim=1)
+    C = x.shape[-1]
+    scale = C ** -0.5                         # n_embd^-1/2, not head_size (model_transformer.py:65,77)
+    for l in range(n_layer):
+        pre = f"blocks.{l}."
+        h = F.layer_norm(x, (C,), p[pre + "ln1.weight"], p[pre + "ln1.bias"], 1e-5)
+        heads = []
+        for hh in range(n_heads):
+            hp = f"{pre}sa.heads.{hh}."
+            heads.append(rel_head(h, p[hp + "query.weight"], p[hp + "key.weight"], p[hp + "value.weight"],
+                                  p[hp + "rel_pos_emb"], scale))
+        att = torch.cat(heads, dim=-1)
+        x = x + F.linear(att, p[pre + "sa.proj.weight"], p[pre + "sa.proj.bias"])
+        h = F.layer_norm(x, (C,), p[pre + "ln2.weight"], p[pre + "ln2.bias"], 1e-5)
+        h = torch.relu(F.linear(h, p[pre + "ffwd.net.0.weight"], p[pre + "ffwd.net.0.bias"]))
+        x = x + F.linear(h, p[pre + "ffwd.net.2.weight"], p[pre + "ffwd.net.2.bias"])
+    x = F.layer_norm(x, (C,), p["ln_f.weight"], p["ln_f.bias"], 1e-5)
+    return F.linear(x, p["lm_head.weight"], p["lm_head.bias"])[:, -T:, :]
+
+
+def param_shapes(n_embd, n_heads, n_layer, block_len, vocab, meta_vocab):
+    """Reference state_dict keys (minus the ``tril`` buffers) and shapes."""
+    hs = n_embd // n_heads
+    S_max = block_len + META
+    shapes = {"token_embedding_table.weight": (vocab, n_embd),
+              "metadata_embedding_table.weight": (meta_vocab, n_embd)}
+    for l in range(n_layer):
+        pre = f"blocks.{l}."
+        for h in range(n_heads):
+            hp = f"{pre}sa.heads.{h}."
+            shapes[hp + "rel_pos_emb"] = (S_max, hs)
+            shapes[hp + "key.weight"] = (hs, n_embd)
+            shapes[hp + "query.weight"] = (hs, n_embd)
+            shapes[hp + "value.weight"] = (hs, n_embd)
+        shapes[pre + "sa.proj.weight"] = (n_embd, n_embd)
+        shapes[pre + "sa.proj.bias"] = (n_embd,)
+        shapes[pre + "ffwd.net.0.weight"] = (4 * n_embd, n_embd)
+        shapes[pre + "ffwd.net.0.bias"] = (4 * n_embd,)
+        shapes[pre + "ffwd.net.2.weight"] = (n_embd, 4 * n_embd)
+        shapes[pre + "ffwd.net.2.bias"] = (n_embd,)
+        for ln in ("ln1", "ln2"):
+            shapes[f"{pre}{ln}.weight"] = (n_embd,)
+            shapes[f"{pre}{ln}.bias"] = (n_embd,)
+    shapes["ln_f.weight"] = (n_embd,)
+    shapes["ln_f.bias"] = (n_embd,)
+    shapes["lm_head.weight"] = (vocab, n_embd)
+    shapes["lm_head.bias"] = (vocab,)
+    return shapes
+
+
+def filled_params(shapes: dict) -> dict:
+    from .fill import fill_param
+    return {k: torch.from_numpy(fill_param(k, s)) for k, s in shapes.items()}
+
+
+def n_flops_fwd_per_seq(n_embd, n_layer, S, V):
+    """Algorithmic forward FLOPs per sequence (SURVEY.md §8(d) cfg 2)."""
+    d = n_embd
+    return n_layer * (24 * S * d * d + 3 * d * S * (S + 1)) + 2 * (S - META) * d * V
+
+
+__all__ = ["forward", "param_shapes", "filled_params", "allowed_mask", "skew_index", "math"]
