@@ -1,0 +1,81 @@
+"""ctypes binding of libmidiseq.so (include/midiseq.h).
+
+The product path has NO CPU fallback: if the library is missing or a call
+fails, a RuntimeError is raised. torch must be imported first so that the
+process-wide libamdhip64.so.7 is torch's (same SONAME, one HIP runtime).
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime before libmidiseq)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmidiseq.so")
+
+F32, BF16 = 0, 1
+EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_RESID, EPI_RELU_MASK, EPI_ACCUM = range(6)
+
+_p, _i, _i64, _f, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
+
+# symbol -> (restype, argtypes); must mirror include/midiseq.h exactly
+SIGNATURES = {
+    "msq_last_error": (ctypes.c_char_p, []),
+    "msq_version": (_i, []),
+    "msq_embed_fwd": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "msq_embed_bwd": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "msq_layernorm_fwd": (_i, [_p, _i, _p, _p, _p, _p, _p, _i64, _i64, _f, _p]),
+    "msq_layernorm_bwd_workspace": (_sz, [_i64, _i64]),
+    "msq_layernorm_bwd": (_i, [_p, _p, _i, _p, _p, _p, _i, _p, _p, _p, _p, _i64, _i64, _p, _p]),
+    "msq_gemm": (_i, [_i, _i, _i, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _p, _i, _i64, _i64, _i64, _i,
+                      _p, _p, _i, _i64, _i64, _p]),
+    "msq_colsum_workspace": (_sz, [_i64, _i64]),
+    "msq_colsum": (_i, [_p, _i, _p, _i, _i64, _i64, _i64, _p, _p]),
+    "msq_cast": (_i, [_p, _i, _p, _i, _i64, _p]),
+    "msq_adam_step": (_i, [_p, _p, _p, _p, _p, _i64, _f, _f, _f, _f, _i64, _p]),
+    "msq_relattn_fwd": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64, _p]),
+    "msq_relattn_bwd_workspace": (_sz, [_i, _i64, _i64, _i64]),
+    "msq_relattn_bwd": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64,
+                             _p, _p]),
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libmidiseq.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed ({rc}): {lib().msq_last_error().decode()}")
+    return rc
+
+
+def ptr(t):
+    """device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dt(t):
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"unsupported dtype {t.dtype}")

@@ -1,0 +1,23 @@
+// Internal interface between the attention translation units.
+#pragma once
+#include "common.h"
+
+struct AttnArgs {
+    int64_t B, S, H, hs, S_max, n_meta;
+    float scale;
+    const void* qkv; int64_t ldq;  // [B*S, ldq]: q | k | v, head h at col h*hs
+    const void* R;                 // [H, S_max, hs]
+};
+
+// exact fp32 path (attn_exact.hip)
+size_t exact_bwd_workspace(int64_t B, int64_t S, int64_t H);
+int exact_fwd(const AttnArgs& a, float* out, int64_t ldo, float* lse, hipStream_t s);
+int exact_bwd(const AttnArgs& a, const float* lse, const float* dout, int64_t ldo, float* dqkv, int64_t ldd, float* dR,
+              void* ws, hipStream_t s);
+
+// bf16 flash path (attn_flash.hip), hs == 128
+int64_t flash_dqr_ld(int64_t S);
+size_t flash_bwd_workspace(int64_t B, int64_t S, int64_t H);
+int flash_fwd(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s);
+int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo, const bf16* out, bf16* dqkv,
+              int64_t ldd, float* dR, void* ws, hipStream_t s);

@@ -1,0 +1,381 @@
+// GEMM for every nn.Linear of the hot path (fwd + both backward products).
+//
+// bf16 fast path: 128x128x64 block tile, 4 waves (2x2), each wave 64x64 built
+// from v_mfma_f32_16x16x32_bf16 with fp32 accumulation. Operand tiles are
+// staged global->registers->LDS (double buffered, one barrier per K tile):
+//   * a K-contiguous operand ([rows][k], 128-B LDS rows, 16-B chunks XOR
+//     swizzled by (row>>1)&7) is read with ds_read_b128;
+//   * an M/N-contiguous operand ([k][rows], 256-B LDS rows, chunk XOR 2*g(k))
+//     is read with ds_read_b64_tr_b16 (hardware transpose, T10) so the
+//     backward products (dX = dY.W, dW = dY^T.X) need no transpose kernel.
+// The MFMA is issued with the B fragment first, so each lane ends up holding 4
+// consecutive output COLUMNS of one row: the epilogue (bias, ReLU, residual,
+// ReLU-mask, accumulate) works on float4 and stores 8/16 B per lane.
+//
+// fp32 exact path: plain LDS-tiled FMA kernel, fp32 end to end (parity mode).
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+
+struct GemmArgs {
+    int64_t M, N, K;
+    const void* A; int64_t lda, sA;
+    const void* B; int64_t ldb, sB;
+    void* C; int64_t ldc, sC;
+    const float* bias;
+    const void* aux; int64_t ldx, sX;
+    int tiles_m, tiles_n, batch;
+    int vec;  // C / aux / bias rows allow 16-B vector access
+};
+
+__device__ __forceinline__ int swz_k(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+__device__ __forceinline__ int swz_mn(int k, int chunk) { return chunk ^ ((((k & 3) | ((k >> 1) & 4))) << 1); }
+
+// load 8 bf16 starting at p; `valid` elements are in bounds (<=0: zero)
+__device__ __forceinline__ u32x4 load_chunk(const bf16* p, int valid) {
+    if (valid >= 8) return *(const u32x4*)p;
+    union { u32x4 v; bf16 e[8]; } u;
+    u.v = (u32x4){0u, 0u, 0u, 0u};
+    for (int i = 0; i < valid; ++i) u.e[i] = p[i];
+    return u.v;
+}
+
+template <int TA, int TB>
+struct Stager {
+    // Each thread moves 4 16-B chunks of A and 4 of B per K tile.
+    u32x4 ra[4], rb[4];
+
+    __device__ __forceinline__ void load(const GemmArgs& g, const bf16* A, const bf16* B, int m0, int n0, int k0,
+                                         int tid) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = tid + NT * i;
+            if (TA == 0) {  // A [M][K]: 128 rows x 8 chunks
+                const int row = c >> 3, ch = c & 7;
+                const int64_t gm = m0 + row, gk = k0 + ch * 8;
+                const int valid = (gm < g.M) ? (int)min<int64_t>(8, g.K - gk) : 0;
+                ra[i] = load_chunk(A + gm * g.lda + gk, valid);
+            } else {  // A [K][M]: 64 rows x 16 chunks
+                const int kr = c >> 4, ch = c & 15;
+                const int64_t gk = k0 + kr, gm = m0 + ch * 8;
+                const int valid = (gk < g.K) ? (int)min<int64_t>(8, g.M - gm) : 0;
+                ra[i] = load_chunk(A + gk * g.lda + gm, valid);
+            }
+            if (TB == 0) {  // B [N][K]
+                const int row = c >> 3, ch = c & 7;
+                const int64_t gn = n0 + row, gk = k0 + ch * 8;
+                const int valid = (gn < g.N) ? (int)min<int64_t>(8, g.K - gk) : 0;
+                rb[i] = load_chunk(B + gn * g.ldb + gk, valid);
+            } else {  // B [K][N]
+                const int kr = c >> 4, ch = c & 15;
+                const int64_t gk = k0 + kr, gn = n0 + ch * 8;
+                const int valid = (gk < g.K) ? (int)min<int64_t>(8, g.N - gn) : 0;
+                rb[i] = load_chunk(B + gk * g.ldb + gn, valid);
+            }
+        }
+    }
+
+    __device__ __forceinline__ void store(char* sa, char* sb, int tid) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = tid + NT * i;
+            if (TA == 0) {
+                const int row = c >> 3, ch = c & 7;
+                *(u32x4*)(sa + row * 128 + swz_k(row, ch) * 16) = ra[i];
+            } else {
+                const int kr = c >> 4, ch = c & 15;
+                *(u32x4*)(sa + kr * 256 + swz_mn(kr, ch) * 16) = ra[i];
+            }
+            if (TB == 0) {
+                const int row = c >> 3, ch = c & 7;
+                *(u32x4*)(sb + row * 128 + swz_k(row, ch) * 16) = rb[i];
+            } else {
+                const int kr = c >> 4, ch = c & 15;
+                *(u32x4*)(sb + kr * 256 + swz_mn(kr, ch) * 16) = rb[i];
+            }
+        }
+    }
+};
+
+// fragment of 16 rows (rb..rb+15) x 8 k (k-step ks, lane group l>>4)
+template <int KCONTIG>
+__device__ __forceinline__ bf16x8 read_frag(const char* s, int rb, int ks, int lane) {
+    if (KCONTIG) {
+        const int row = rb + (lane & 15);
+        const int ch = ks * 4 + (lane >> 4);
+        return *(const bf16x8*)(s + row * 128 + swz_k(row, ch) * 16);
+    } else {
+        const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
+        const int kA = ks * 32 + 8 * g + q, kB = kA + 4;
+        const int ch = (rb >> 3) + (p >> 1);
+        const int offA = kA * 256 + swz_mn(kA, ch) * 16 + (p & 1) * 8;
+        const int offB = kB * 256 + swz_mn(kB, ch) * 16 + (p & 1) * 8;
+        i16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((i16x4 __attribute__((address_space(3)))*)(
+            (__attribute__((address_space(3))) char*)s + offA));
+        i16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((i16x4 __attribute__((address_space(3)))*)(
+            (__attribute__((address_space(3))) char*)s + offB));
+        union { i16x4 h[2]; bf16x8 v; } u;
+        u.h[0] = a;
+        u.h[1] = b;
+        return u.v;
+    }
+}
+
+template <typename TC>
+__device__ __forceinline__ void epi_store(TC* p, f32x4 v, int nv) {
+    if (nv == 4) {
+        store4(p, v);
+    } else {
+        const int n = nv < 0 ? -nv : nv;
+        for (int i = 0; i < n; ++i) p[i] = (TC)v[i];
+    }
+}
+// load up to 4 elements (nv as in epi_store)
+template <typename T>
+__device__ __forceinline__ f32x4 epi_load(const T* p, int nv) {
+    if (nv == 4) return load4(p);
+    const int n = nv < 0 ? -nv : nv;
+    f32x4 x = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < n; ++i) x[i] = (float)p[i];
+    return x;
+}
+
+template <int TA, int TB, int EPI, typename TC, typename TX>
+__global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * (BM * BK + BN * BK) * 2];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tiles = g.tiles_m * g.tiles_n;
+    int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bz = bid / tiles;
+    bid -= bz * tiles;
+    // grouped ordering: 8 M-tiles share each sweep over N (L2 reuse of B)
+    const int GROUP = 8;
+    const int per_group = GROUP * g.tiles_n;
+    const int grp = bid / per_group, first_m = grp * GROUP;
+    const int gsz = min(g.tiles_m - first_m, GROUP);
+    const int tm = first_m + (bid % per_group) % gsz;
+    const int tn = (bid % per_group) / gsz;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    const bf16* A = (const bf16*)g.A + bz * g.sA;
+    const bf16* B = (const bf16*)g.B + bz * g.sB;
+
+    constexpr int STAGE = (BM * BK + BN * BK) * 2;  // bytes per pipeline stage
+
+    const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    Stager<TA, TB> st;
+    const int nk = (int)((g.K + BK - 1) / BK);
+    st.load(g, A, B, m0, n0, 0, tid);
+    st.store(smem, smem + BM * BK * 2, tid);
+    __syncthreads();
+
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        char* sa = smem + cur * STAGE;
+        char* sb = sa + BM * BK * 2;
+        if (kt + 1 < nk) st.load(g, A, B, m0, n0, (kt + 1) * BK, tid);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 af[4], bfr[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[i] = read_frag<TA == 0>(sa, wm + i * 16, ks, lane);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bfr[j] = read_frag<TB == 0>(sb, wn + j * 16, ks, lane);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) st.store(smem + (cur ^ 1) * STAGE, smem + (cur ^ 1) * STAGE + BM * BK * 2, tid);
+        __syncthreads();
+    }
+
+    // epilogue: lane holds C[m][n..n+3]
+    TC* C = (TC*)g.C + bz * g.sC;
+    const TX* X = (const TX*)g.aux + (g.aux ? bz * g.sX : 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t m = m0 + wm + i * 16 + (lane & 15);
+        if (m >= g.M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t n = n0 + wn + j * 16 + 4 * (lane >> 4);
+            if (n >= g.N) continue;
+            const int nv = g.vec ? (int)min<int64_t>(4, g.N - n) : -(int)min<int64_t>(4, g.N - n);
+            f32x4 v = acc[i][j];
+            if ((EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID) && g.bias)
+                v += epi_load(g.bias + n, nv);
+            if (EPI == MSQ_EPI_BIAS_RELU) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);
+            }
+            if (EPI == MSQ_EPI_BIAS_RESID) {
+                v += epi_load(X + m * g.ldx + n, nv);
+            }
+            if (EPI == MSQ_EPI_RELU_MASK) {
+                const f32x4 x = epi_load(X + m * g.ldx + n, nv);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) v[t] = x[t] > 0.f ? v[t] : 0.f;
+            }
+            TC* cp = C + m * g.ldc + n;
+            if (EPI == MSQ_EPI_ACCUM) v += epi_load(cp, nv);
+            epi_store(cp, v, nv);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- fp32 exact
+constexpr int EB = 64, EK = 16;
+
+template <int EPI, typename TC, typename TX>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g, int ta, int tb) {
+    __shared__ float sa[EK][EB + 1];
+    __shared__ float sb[EK][EB + 1];
+    const int tid = threadIdx.x;
+    const int bz = blockIdx.z;
+    const int64_t m0 = (int64_t)blockIdx.y * EB, n0 = (int64_t)blockIdx.x * EB;
+    const float* A = (const float*)g.A + bz * g.sA;
+    const float* B = (const float*)g.B + bz * g.sB;
+    const int tx = tid & 15, ty = tid >> 4;
+    float acc[4][4] = {};
+    for (int64_t k0 = 0; k0 < g.K; k0 += EK) {
+        for (int e = tid; e < EB * EK; e += 256) {
+            const int r = e / EK, kk = e % EK;  // r in tile rows, kk in k
+            const int64_t gm = m0 + r, gn = n0 + r, gk = k0 + kk;
+            float av = 0.f, bv = 0.f;
+            if (gm < g.M && gk < g.K) av = ta ? A[gk * g.lda + gm] : A[gm * g.lda + gk];
+            if (gn < g.N && gk < g.K) bv = tb ? B[gk * g.ldb + gn] : B[gn * g.ldb + gk];
+            sa[kk][r] = av;
+            sb[kk][r] = bv;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < EK; ++kk) {
+            float a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = sa[kk][ty * 4 + i];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = sb[kk][tx * 4 + j];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+        }
+        __syncthreads();
+    }
+    TC* C = (TC*)g.C + bz * g.sC;
+    const TX* X = (const TX*)g.aux + (g.aux ? bz * g.sX : 0);
+    for (int i = 0; i < 4; ++i) {
+        const int64_t m = m0 + ty * 4 + i;
+        if (m >= g.M) continue;
+        for (int j = 0; j < 4; ++j) {
+            const int64_t n = n0 + tx * 4 + j;
+            if (n >= g.N) continue;
+            float v = acc[i][j];
+            if ((EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID) && g.bias) v += g.bias[n];
+            if (EPI == MSQ_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+            if (EPI == MSQ_EPI_BIAS_RESID) v += (float)X[m * g.ldx + n];
+            if (EPI == MSQ_EPI_RELU_MASK) v = ((float)X[m * g.ldx + n] > 0.f) ? v : 0.f;
+            TC* cp = C + m * g.ldc + n;
+            if (EPI == MSQ_EPI_ACCUM) v += (float)*cp;
+            *cp = (TC)v;
+        }
+    }
+}
+
+template <int TA, int TB, int EPI, typename TC, typename TX>
+void launch_bf16(const GemmArgs& g, hipStream_t s) {
+    const int nblk = g.tiles_m * g.tiles_n * g.batch;
+    hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, EPI, TC, TX>), dim3(nblk), dim3(NT), 0, s, g);
+}
+
+template <int EPI, typename TC, typename TX>
+int dispatch_bf16_t(const GemmArgs& g, int ta, int tb, hipStream_t s) {
+    if (ta == 0 && tb == 0) launch_bf16<0, 0, EPI, TC, TX>(g, s);
+    else if (ta == 0 && tb == 1) launch_bf16<0, 1, EPI, TC, TX>(g, s);
+    else if (ta == 1 && tb == 1) launch_bf16<1, 1, EPI, TC, TX>(g, s);
+    else launch_bf16<1, 0, EPI, TC, TX>(g, s);
+    return 0;
+}
+
+template <int EPI, typename TC, typename TX>
+int dispatch_f32_t(const GemmArgs& g, int ta, int tb, hipStream_t s) {
+    dim3 grid((unsigned)((g.N + EB - 1) / EB), (unsigned)((g.M + EB - 1) / EB), (unsigned)g.batch);
+    hipLaunchKernelGGL((gemm_f32_kernel<EPI, TC, TX>), grid, dim3(256), 0, s, g, ta, tb);
+    return 0;
+}
+
+template <bool BF, typename TC>
+int dispatch_epi(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hipStream_t s) {
+#define D(E, TX) (BF ? dispatch_bf16_t<E, TC, TX>(g, ta, tb, s) : dispatch_f32_t<E, TC, TX>(g, ta, tb, s))
+    switch (epi) {
+        case MSQ_EPI_NONE: return D(MSQ_EPI_NONE, float);
+        case MSQ_EPI_BIAS: return D(MSQ_EPI_BIAS, float);
+        case MSQ_EPI_BIAS_RELU: return D(MSQ_EPI_BIAS_RELU, float);
+        case MSQ_EPI_BIAS_RESID: return D(MSQ_EPI_BIAS_RESID, float);
+        case MSQ_EPI_RELU_MASK:
+            return aux_dtype == MSQ_BF16 ? D(MSQ_EPI_RELU_MASK, bf16) : D(MSQ_EPI_RELU_MASK, float);
+        case MSQ_EPI_ACCUM: return D(MSQ_EPI_ACCUM, float);
+    }
+#undef D
+    return -1;
+}
+
+}  // namespace
+
+extern "C" int msq_gemm(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                        int64_t strideA, const void* B, int64_t ldb, int64_t strideB, void* C, int c_dtype,
+                        int64_t ldc, int64_t strideC, int64_t batch, int epilogue, const float* bias,
+                        const void* aux, int aux_dtype, int64_t ld_aux, int64_t stride_aux, void* stream) {
+    MSQ_CHECK_ARG(dtype == MSQ_BF16 || dtype == MSQ_F32, "msq_gemm: bad dtype %d", dtype);
+    MSQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && batch > 0, "msq_gemm: empty problem");
+    MSQ_CHECK_ARG(epilogue >= MSQ_EPI_NONE && epilogue <= MSQ_EPI_ACCUM, "msq_gemm: bad epilogue");
+    MSQ_CHECK_ARG(!(epilogue == MSQ_EPI_ACCUM && c_dtype != MSQ_F32), "msq_gemm: ACCUM needs fp32 C");
+    MSQ_CHECK_ARG(bias || (epilogue != MSQ_EPI_BIAS && epilogue != MSQ_EPI_BIAS_RELU),
+                  "msq_gemm: epilogue needs bias (BIAS_RESID accepts NULL)");
+    MSQ_CHECK_ARG(aux || (epilogue != MSQ_EPI_BIAS_RESID && epilogue != MSQ_EPI_RELU_MASK),
+                  "msq_gemm: epilogue needs aux");
+    MSQ_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? N : K) && ldc >= N, "msq_gemm: leading dim too small");
+    if (dtype == MSQ_BF16) {
+        MSQ_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && (strideA % 8) == 0 && (strideB % 8) == 0,
+                      "msq_gemm: bf16 path needs lda/ldb (and batch strides) %% 8 == 0");
+        MSQ_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "msq_gemm: A/B must be 16-B aligned");
+    }
+    GemmArgs g;
+    g.M = M; g.N = N; g.K = K;
+    g.A = A; g.lda = lda; g.sA = strideA;
+    g.B = B; g.ldb = ldb; g.sB = strideB;
+    g.C = C; g.ldc = ldc; g.sC = strideC;
+    g.bias = bias; g.aux = aux; g.ldx = ld_aux; g.sX = stride_aux;
+    g.tiles_m = (int)((M + BM - 1) / BM);
+    g.tiles_n = (int)((N + BN - 1) / BN);
+    g.batch = (int)batch;
+    {
+        const int esz = c_dtype == MSQ_BF16 ? 2 : 4;
+        const int xsz = aux_dtype == MSQ_BF16 ? 2 : 4;
+        bool vec = (ldc % 4 == 0) && (strideC % 4 == 0) && ((uintptr_t)C % (4 * esz) == 0);
+        if (bias) vec = vec && ((uintptr_t)bias % 16 == 0);
+        if (aux) vec = vec && (ld_aux % 4 == 0) && (stride_aux % 4 == 0) && ((uintptr_t)aux % (4 * xsz) == 0);
+        g.vec = vec ? 1 : 0;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    int rc;
+    if (dtype == MSQ_BF16)
+        rc = c_dtype == MSQ_BF16 ? dispatch_epi<true, bf16>(g, ta, tb, epilogue, aux_dtype, s)
+                                 : dispatch_epi<true, float>(g, ta, tb, epilogue, aux_dtype, s);
+    else
+        rc = c_dtype == MSQ_BF16 ? dispatch_epi<false, bf16>(g, ta, tb, epilogue, aux_dtype, s)
+                                 : dispatch_epi<false, float>(g, ta, tb, epilogue, aux_dtype, s);
+    if (rc) return msq_set_error(MSQ_ERR_ARG, "msq_gemm: unsupported combination");
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}

@@ -1,0 +1,346 @@
+// Memory-bound row/element kernels: embedding gather/scatter, LayerNorm
+// fwd/bwd, column sums (bias grads), casts and Adam. All HBM-bound; loads are
+// 16-B (fp32x4) or 8-B (bf16x4) per lane (guide §6 G13).
+#include "common.h"
+
+// ------------------------------------------------------------------ embedding
+// model_transformer.py:152-155 / mamba.py:29-30: meta rows first, then tokens.
+__global__ void embed_fwd_kernel(float* __restrict__ x, const float* __restrict__ tok, const float* __restrict__ met,
+                                 const int64_t* __restrict__ idx, const int64_t* __restrict__ meta, int64_t B,
+                                 int64_t T, int64_t nm, int64_t d) {
+    const int64_t S = T + nm;
+    const int64_t d4 = d / 4;
+    const int64_t total = B * S * d4;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t c = e % d4, row = e / d4;
+        const int64_t b = row / S, s = row % S;
+        const float* src = s < nm ? met + meta[b * nm + s] * d : tok + idx[b * T + (s - nm)] * d;
+        *(f32x4*)(x + row * d + c * 4) = *(const f32x4*)(src + c * 4);
+    }
+}
+
+__global__ void embed_bwd_kernel(float* __restrict__ gt, float* __restrict__ gm, const float* __restrict__ dx,
+                                 const int64_t* __restrict__ idx, const int64_t* __restrict__ meta, int64_t B,
+                                 int64_t T, int64_t nm, int64_t d) {
+    const int64_t S = T + nm;
+    const int64_t total = B * S * d;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t c = e % d, row = e / d;
+        const int64_t b = row / S, s = row % S;
+        float* dst = s < nm ? gm + meta[b * nm + s] * d : gt + idx[b * T + (s - nm)] * d;
+        atomicAdd(dst + c, dx[e]);
+    }
+}
+
+extern "C" int msq_embed_fwd(float* x, const float* tok_table, const float* meta_table, const int64_t* idx,
+                             const int64_t* meta, int64_t B, int64_t T, int64_t n_meta, int64_t d, void* stream) {
+    MSQ_CHECK_ARG(d % 4 == 0 && B > 0 && T >= 0 && n_meta >= 0, "msq_embed_fwd: d %% 4 != 0 or bad sizes");
+    const int64_t total = B * (T + n_meta) * (d / 4);
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, tok_table, meta_table,
+                       idx, meta, B, T, n_meta, d);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
+extern "C" int msq_embed_bwd(float* g_tok, float* g_meta, const float* dx, const int64_t* idx, const int64_t* meta,
+                             int64_t B, int64_t T, int64_t n_meta, int64_t d, void* stream) {
+    MSQ_CHECK_ARG(B > 0 && d > 0, "msq_embed_bwd: bad sizes");
+    const int64_t total = B * (T + n_meta) * d;
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
+    hipLaunchKernelGGL(embed_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, g_tok, g_meta, dx, idx,
+                       meta, B, T, n_meta, d);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
+// ------------------------------------------------------------------ LayerNorm
+// one wave per row; the row (d <= 64*4*MAXC) is held in registers.
+template <typename TY, int MAXC>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(TY* __restrict__ y, float* __restrict__ mean,
+                                                     float* __restrict__ rstd, const float* __restrict__ x,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     int64_t rows, int d, float eps) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = blockIdx.x * 4LL + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float* xr = x + row * d;
+    f32x4 v[MAXC];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        const int col = (c * 64 + lane) * 4;
+        v[c] = col < d ? *(const f32x4*)(xr + col) : (f32x4){0.f, 0.f, 0.f, 0.f};
+        s += v[c][0] + v[c][1] + v[c][2] + v[c][3];
+    }
+    const float mu = wave_sum(s) / d;
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        const int col = (c * 64 + lane) * 4;
+        if (col < d) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) { const float z = v[c][t] - mu; q += z * z; }
+        }
+    }
+    const float rs = rsqrtf(wave_sum(q) / d + eps);
+    if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+    TY* yr = y + row * d;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        const int col = (c * 64 + lane) * 4;
+        if (col < d) {
+            const f32x4 g = *(const f32x4*)(gamma + col), b = *(const f32x4*)(beta + col);
+            f32x4 o;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) o[t] = (v[c][t] - mu) * rs * g[t] + b[t];
+            store4(yr + col, o);
+        }
+    }
+}
+
+constexpr int LN_BWD_BLOCKS = 512;
+
+// dx_acc += rstd*(dyg - mean(dyg) - xhat*mean(dyg*xhat)); per-block dgamma/dbeta partials
+template <typename TD, typename TO, int MAXC>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO* __restrict__ dcopy,
+                                                     float* __restrict__ part, const TD* __restrict__ dy,
+                                                     const float* __restrict__ x, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                                     int64_t rows, int d) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    f32x4 pg[MAXC], pb[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) pg[c] = pb[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int64_t row = blockIdx.x * 4LL + wid; row < rows; row += (int64_t)gridDim.x * 4) {
+        const float mu = mean[row], rs = rstd[row];
+        f32x4 xh[MAXC], g[MAXC];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+            const int col = (c * 64 + lane) * 4;
+            if (col < d) {
+                const f32x4 xv = *(const f32x4*)(x + row * d + col);
+                const f32x4 dv = load4(dy + row * d + col);
+                const f32x4 gm = *(const f32x4*)(gamma + col);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    xh[c][t] = (xv[t] - mu) * rs;
+                    g[c][t] = dv[t] * gm[t];
+                    s1 += g[c][t];
+                    s2 += g[c][t] * xh[c][t];
+                    pg[c][t] += dv[t] * xh[c][t];
+                    pb[c][t] += dv[t];
+                }
+            } else {
+                xh[c] = g[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            }
+        }
+        const float m1 = wave_sum(s1) / d, m2 = wave_sum(s2) / d;
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+            const int col = (c * 64 + lane) * 4;
+            if (col < d) {
+                float* dp = dxa + row * d + col;
+                f32x4 o = *(f32x4*)dp;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) o[t] += rs * (g[c][t] - m1 - xh[c][t] * m2);
+                *(f32x4*)dp = o;
+                if (dcopy) store4(dcopy + row * d + col, o);
+            }
+        }
+    }
+    // block reduce of the partials through LDS, then one row per block
+    __shared__ f32x4 red[4][64 * MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) red[wid][c * 64 + lane] = pg[c];
+    __syncthreads();
+    if (wid == 0) {
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+            const int col = (c * 64 + lane) * 4;
+            f32x4 t = red[0][c * 64 + lane] + red[1][c * 64 + lane] + red[2][c * 64 + lane] + red[3][c * 64 + lane];
+            if (col < d) *(f32x4*)(part + (int64_t)blockIdx.x * 2 * d + col) = t;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) red[wid][c * 64 + lane] = pb[c];
+    __syncthreads();
+    if (wid == 0) {
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+            const int col = (c * 64 + lane) * 4;
+            f32x4 t = red[0][c * 64 + lane] + red[1][c * 64 + lane] + red[2][c * 64 + lane] + red[3][c * 64 + lane];
+            if (col < d) *(f32x4*)(part + (int64_t)blockIdx.x * 2 * d + d + col) = t;
+        }
+    }
+}
+
+// out[c] += sum_p part[p, c] for c < 2d (dgamma | dbeta)
+__global__ void ln_reduce_kernel(float* __restrict__ dg, float* __restrict__ db, const float* __restrict__ part,
+                                 int nparts, int d) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= 2 * d) return;
+    float s = 0.f;
+    for (int p = 0; p < nparts; ++p) s += part[(int64_t)p * 2 * d + c];
+    if (c < d) dg[c] += s;
+    else db[c - d] += s;
+}
+
+extern "C" size_t msq_layernorm_bwd_workspace(int64_t rows, int64_t d) {
+    (void)rows;
+    return (size_t)LN_BWD_BLOCKS * 2 * d * sizeof(float);
+}
+
+template <typename TY>
+static void ln_fwd_launch(TY* y, float* mean, float* rstd, const float* x, const float* g, const float* b,
+                          int64_t rows, int d, float eps, hipStream_t s) {
+    const dim3 grid((unsigned)((rows + 3) / 4));
+    if (d <= 256) hipLaunchKernelGGL((ln_fwd_kernel<TY, 1>), grid, dim3(256), 0, s, y, mean, rstd, x, g, b, rows, d, eps);
+    else if (d <= 1024) hipLaunchKernelGGL((ln_fwd_kernel<TY, 4>), grid, dim3(256), 0, s, y, mean, rstd, x, g, b, rows, d, eps);
+    else hipLaunchKernelGGL((ln_fwd_kernel<TY, 8>), grid, dim3(256), 0, s, y, mean, rstd, x, g, b, rows, d, eps);
+}
+
+extern "C" int msq_layernorm_fwd(void* y, int y_dtype, float* mean, float* rstd, const float* x, const float* gamma,
+                                 const float* beta, int64_t rows, int64_t d, float eps, void* stream) {
+    MSQ_CHECK_ARG(d % 4 == 0 && d <= 2048 && rows > 0, "msq_layernorm_fwd: need d %% 4 == 0, d <= 2048");
+    hipStream_t s = (hipStream_t)stream;
+    if (y_dtype == MSQ_BF16) ln_fwd_launch((bf16*)y, mean, rstd, x, gamma, beta, rows, (int)d, eps, s);
+    else ln_fwd_launch((float*)y, mean, rstd, x, gamma, beta, rows, (int)d, eps, s);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
+template <typename TD, typename TO>
+static void ln_bwd_launch(float* dxa, TO* dcopy, float* part, const TD* dy, const float* x, const float* mean,
+                          const float* rstd, const float* gamma, int64_t rows, int d, hipStream_t s) {
+    const dim3 grid(LN_BWD_BLOCKS);
+    if (d <= 256) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 1>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d);
+    else if (d <= 1024) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d);
+    else hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 8>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d);
+}
+
+extern "C" int msq_layernorm_bwd(float* dx_acc, void* dx_copy, int copy_dtype, float* dgamma, float* dbeta,
+                                 const void* dy, int dy_dtype, const float* x, const float* mean, const float* rstd,
+                                 const float* gamma, int64_t rows, int64_t d, void* workspace, void* stream) {
+    MSQ_CHECK_ARG(d % 4 == 0 && d <= 2048 && rows > 0 && workspace, "msq_layernorm_bwd: bad args");
+    hipStream_t s = (hipStream_t)stream;
+    float* part = (float*)workspace;
+    const int di = (int)d;
+    if (dy_dtype == MSQ_BF16) {
+        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, s);
+        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, s);
+    } else {
+        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, s);
+        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, s);
+    }
+    hipLaunchKernelGGL(ln_reduce_kernel, dim3((unsigned)((2 * d + 255) / 256)), dim3(256), 0, s, dgamma, dbeta, part,
+                       LN_BWD_BLOCKS, di);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
+// ------------------------------------------------------------------ colsum
+constexpr int CS_SPLIT = 128;
+
+template <typename T>
+__global__ void colsum_part_kernel(float* __restrict__ part, const T* __restrict__ x, int64_t rows, int64_t cols,
+                                   int64_t ld) {
+    // block (col chunk of 1024, row split); each thread 4 columns
+    const int64_t c = (blockIdx.x * 256LL + threadIdx.x) * 4;
+    const int64_t per = (rows + gridDim.y - 1) / gridDim.y;
+    const int64_t r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+    if (c >= cols) return;
+    f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (c + 4 <= cols) {
+        for (int64_t r = r0; r < r1; ++r) s += load4(x + r * ld + c);
+    } else {
+        for (int64_t r = r0; r < r1; ++r)
+            for (int t = 0; c + t < cols; ++t) s[t] += (float)x[r * ld + c + t];
+    }
+    for (int t = 0; t < 4 && c + t < cols; ++t) part[blockIdx.y * cols + c + t] = s[t];
+}
+
+__global__ void colsum_reduce_kernel(float* __restrict__ out, const float* __restrict__ part, int nparts,
+                                     int64_t cols, int accumulate) {
+    const int64_t c = blockIdx.x * 256LL + threadIdx.x;
+    if (c >= cols) return;
+    float s = 0.f;
+    for (int p = 0; p < nparts; ++p) s += part[p * cols + c];
+    out[c] = accumulate ? out[c] + s : s;
+}
+
+extern "C" size_t msq_colsum_workspace(int64_t rows, int64_t cols) {
+    (void)rows;
+    return (size_t)CS_SPLIT * cols * sizeof(float);
+}
+
+extern "C" int msq_colsum(float* out, int accumulate, const void* x, int dtype, int64_t rows, int64_t cols,
+                          int64_t ld, void* workspace, void* stream) {
+    MSQ_CHECK_ARG(rows > 0 && cols > 0 && workspace && ld % 4 == 0, "msq_colsum: bad args (ld %% 4 == 0)");
+    hipStream_t s = (hipStream_t)stream;
+    const int split = (int)std::min<int64_t>(CS_SPLIT, rows);
+    dim3 grid((unsigned)((cols + 1023) / 1024), (unsigned)split);
+    if (dtype == MSQ_BF16) hipLaunchKernelGGL(colsum_part_kernel<bf16>, grid, dim3(256), 0, s, (float*)workspace, (const bf16*)x, rows, cols, ld);
+    else hipLaunchKernelGGL(colsum_part_kernel<float>, grid, dim3(256), 0, s, (float*)workspace, (const float*)x, rows, cols, ld);
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, s, out,
+                       (const float*)workspace, split, cols, accumulate);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
+// ------------------------------------------------------------------ cast
+template <typename TD, typename TS>
+__global__ void cast_kernel(TD* __restrict__ d, const TS* __restrict__ s, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        d[i] = (TD)(float)s[i];
+}
+
+extern "C" int msq_cast(void* dst, int dst_dtype, const void* src, int src_dtype, int64_t n, void* stream) {
+    MSQ_CHECK_ARG(n >= 0, "msq_cast: n < 0");
+    if (n == 0) return MSQ_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, 16384);
+    if (dst_dtype == MSQ_BF16 && src_dtype == MSQ_F32) hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(grid), dim3(256), 0, s, (bf16*)dst, (const float*)src, n);
+    else if (dst_dtype == MSQ_F32 && src_dtype == MSQ_BF16) hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(grid), dim3(256), 0, s, (float*)dst, (const bf16*)src, n);
+    else if (dst_dtype == MSQ_F32 && src_dtype == MSQ_F32) hipLaunchKernelGGL((cast_kernel<float, float>), dim3(grid), dim3(256), 0, s, (float*)dst, (const float*)src, n);
+    else hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(grid), dim3(256), 0, s, (bf16*)dst, (const bf16*)src, n);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
+// ------------------------------------------------------------------ Adam
+// torch.optim.Adam (foreach, weight_decay=0, amsgrad=False):
+//   m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2
+//   p -= (lr / (1-b1^t)) * m / (sqrt(v) / sqrt(1-b2^t) + eps)
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, bf16* __restrict__ shadow, int64_t n, float b1, float b2, float eps,
+                            float step_size, float bc2_sqrt) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float gi = g[i];
+        const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1-b1)
+        const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        const float den = sqrtf(vi) / bc2_sqrt + eps;
+        const float pi = p[i] - step_size * (mi / den);
+        p[i] = pi;
+        if (shadow) shadow[i] = (bf16)pi;
+    }
+}
+
+extern "C" int msq_adam_step(float* p, const float* g, float* m, float* v, void* p_shadow, int64_t n, float lr,
+                             float beta1, float beta2, float eps, int64_t step, void* stream) {
+    MSQ_CHECK_ARG(n >= 0 && step >= 1, "msq_adam_step: bad args");
+    if (n == 0) return MSQ_OK;
+    const double bc1 = 1.0 - pow((double)beta1, (double)step);
+    const double bc2 = 1.0 - pow((double)beta2, (double)step);
+    const float step_size = (float)(lr / bc1);
+    const float bc2s = (float)sqrt(bc2);
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, 16384);
+    hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (bf16*)p_shadow, n,
+                       beta1, beta2, eps, step_size, bc2s);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}

@@ -1,0 +1,104 @@
+"""Thin tensor-level wrappers over the libmidiseq C ABI (no autograd here).
+
+Every function launches on torch's current stream and raises on failure;
+there is no fallback path.
+"""
+import torch
+
+from . import _lib as L
+from ._lib import ptr, call, stream, dt
+
+
+def _mat(t, trans):
+    """(rows, cols, ld, batch_stride, batch) of a 2-D/3-D row-major tensor."""
+    assert t.stride(-1) == 1, "innermost dim must be contiguous"
+    r, c = t.shape[-2], t.shape[-1]
+    ld = t.stride(-2)
+    if t.dim() == 3:
+        return r, c, ld, t.stride(0), t.shape[0]
+    return r, c, ld, 0, 1
+
+
+def gemm(A, B, *, ta=False, tb=False, out=None, out_dtype=None, epilogue=L.EPI_NONE, bias=None, aux=None):
+    """C = op(A) . op(B).  ta: A stored [K,M]; tb: B stored [K,N] (else [N,K])."""
+    ar, ac, lda, sA, ba = _mat(A, ta)
+    br, bc, ldb, sB, bb = _mat(B, tb)
+    M, K = (ac, ar) if ta else (ar, ac)
+    N, K2 = (bc, br) if tb else (br, bc)
+    assert K == K2, f"K mismatch {K} vs {K2}"
+    assert A.dtype == B.dtype
+    batch = max(ba, bb)
+    if out is None:
+        odt = out_dtype or A.dtype
+        out = torch.empty((batch, M, N) if batch > 1 or A.dim() == 3 else (M, N), device=A.device, dtype=odt)
+    cr, cc, ldc, sC, bcnt = _mat(out, False)
+    assert (cr, cc) == (M, N), f"out shape {(cr, cc)} != {(M, N)}"
+    ldx = sX = 0
+    axd = L.F32
+    if aux is not None:
+        _, _, ldx, sX, _ = _mat(aux, False)
+        axd = dt(aux)
+    call("msq_gemm", dt(A), int(ta), int(tb), M, N, K, ptr(A), lda, sA, ptr(B), ldb, sB, ptr(out), dt(out), ldc,
+         sC, batch, epilogue, ptr(bias), ptr(aux), axd, ldx, sX, stream())
+    return out
+
+
+def layernorm_fwd(x, gamma, beta, eps=1e-5, out_dtype=torch.float32, out=None):
+    rows, d = x.numel() // x.shape[-1], x.shape[-1]
+    y = out if out is not None else torch.empty(x.shape, device=x.device, dtype=out_dtype)
+    mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+    call("msq_layernorm_fwd", ptr(y), dt(y), ptr(mean), ptr(rstd), ptr(x), ptr(gamma), ptr(beta), rows, d,
+         float(eps), stream())
+    return y, mean, rstd
+
+
+_ws_cache = {}
+
+
+def workspace(nbytes, device, tag="ws"):
+    key = (tag, device)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1), device=device, dtype=torch.uint8)
+        _ws_cache[key] = buf
+    return buf
+
+
+def layernorm_bwd(dx_acc, dy, x, mean, rstd, gamma, dgamma, dbeta, dx_copy=None):
+    """dx_acc += LN'(dy); dgamma/dbeta += ...; optional copy of dx_acc."""
+    rows, d = x.numel() // x.shape[-1], x.shape[-1]
+    ws = workspace(L.lib().msq_layernorm_bwd_workspace(rows, d), x.device, "ln")
+    call("msq_layernorm_bwd", ptr(dx_acc), ptr(dx_copy), dt(dx_copy) if dx_copy is not None else L.F32,
+         ptr(dgamma), ptr(dbeta), ptr(dy), dt(dy), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), rows, d, ptr(ws),
+         stream())
+
+
+def colsum(x2d, out, accumulate=False):
+    rows, cols = x2d.shape
+    ws = workspace(L.lib().msq_colsum_workspace(rows, cols), x2d.device, "colsum")
+    call("msq_colsum", ptr(out), int(accumulate), ptr(x2d), dt(x2d), rows, cols, x2d.stride(0), ptr(ws), stream())
+    return out
+
+
+def embed_fwd(x, tok_table, meta_table, idx, meta):
+    B, T = idx.shape
+    call("msq_embed_fwd", ptr(x), ptr(tok_table), ptr(meta_table), ptr(idx), ptr(meta), B, T, meta.shape[1],
+         tok_table.shape[1], stream())
+    return x
+
+
+def embed_bwd(g_tok, g_meta, dx, idx, meta):
+    B, T = idx.shape
+    call("msq_embed_bwd", ptr(g_tok), ptr(g_meta), ptr(dx), ptr(idx), ptr(meta), B, T, meta.shape[1],
+         g_tok.shape[1], stream())
+
+
+def cast(dst, src):
+    call("msq_cast", ptr(dst), dt(dst), ptr(src), dt(src), src.numel(), stream())
+    return dst
+
+
+def adam_step(p, g, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, shadow=None):
+    call("msq_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow), p.numel(), float(lr), float(beta1),
+         float(beta2), float(eps), int(step), stream())

@@ -1,0 +1,117 @@
+/* libmidiseq — C ABI of the MI355X (gfx950) symbolic-music sequence-model path.
+ *
+ * Drop-in boundary for the hot path of thorGabe123/Deep-Learning-Based-Sequence-
+ * Models-for-Music-Generation (reference @ 2025-08-24). Every entry point names
+ * the reference interface it replaces (file:line). The reference is pure
+ * Python/PyTorch, so its "FFI" for these ops is PyTorch's ATen dispatch; the
+ * Python host layer of this repo binds these symbols with ctypes
+ * (INTEGRATION.md shows the binding).
+ *
+ * Conventions:
+ *   - raw device pointers, int64 sizes/strides (in ELEMENTS), a dtype enum and
+ *     a hipStream_t passed as void*;
+ *   - the caller owns every buffer; scratch comes from *_workspace() queries;
+ *   - launches are asynchronous on the given stream; nothing here allocates,
+ *     synchronises or copies to the host (graph-capture safe);
+ *   - return 0 on success, a negative MSQ_ERR_* code on failure;
+ *     msq_last_error() returns a thread-local message.
+ */
+#ifndef MIDISEQ_H
+#define MIDISEQ_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSQ_OK 0
+#define MSQ_ERR_ARG (-1)
+#define MSQ_ERR_HIP (-2)
+#define MSQ_ERR_UNSUPPORTED (-3)
+
+/* element types */
+#define MSQ_F32 0
+#define MSQ_BF16 1
+
+/* GEMM epilogues */
+#define MSQ_EPI_NONE 0       /* C = acc                                   */
+#define MSQ_EPI_BIAS 1       /* C = acc + bias[n]                          */
+#define MSQ_EPI_BIAS_RELU 2  /* C = relu(acc + bias[n])                    */
+#define MSQ_EPI_BIAS_RESID 3 /* C = acc + bias[n] + aux[m,n]  (aux fp32)   */
+#define MSQ_EPI_RELU_MASK 4  /* C = acc * (aux[m,n] > 0)                   */
+#define MSQ_EPI_ACCUM 5      /* C += acc                     (C fp32)      */
+
+const char* msq_last_error(void);
+int msq_version(void);
+
+/* ---- token + metadata embedding -------------------------------------------
+ * Replaces nn.Embedding x2 + torch.cat (model_transformer.py:152-155,
+ * mamba.py:29-30). x[b, 0:n_meta] = meta_table[meta[b]], x[b, n_meta+t] =
+ * tok_table[idx[b,t]]; x is fp32 [B, n_meta+T, d].                           */
+int msq_embed_fwd(float* x, const float* tok_table, const float* meta_table, const int64_t* idx,
+                  const int64_t* meta, int64_t B, int64_t T, int64_t n_meta, int64_t d, void* stream);
+/* backward: g_tok[idx[b,t]] += dx[b, n_meta+t], g_meta[meta[b,i]] += dx[b,i]
+ * (fp32 atomics; caller zeroes or accumulates).                               */
+int msq_embed_bwd(float* g_tok, float* g_meta, const float* dx, const int64_t* idx, const int64_t* meta,
+                  int64_t B, int64_t T, int64_t n_meta, int64_t d, void* stream);
+
+/* ---- LayerNorm (nn.LayerNorm, model_transformer.py:115-116,146; mamba.py:25)
+ * y = (x - mean) * rstd * gamma + beta; x fp32 [rows, d]; y in y_dtype.      */
+int msq_layernorm_fwd(void* y, int y_dtype, float* mean, float* rstd, const float* x, const float* gamma,
+                      const float* beta, int64_t rows, int64_t d, float eps, void* stream);
+size_t msq_layernorm_bwd_workspace(int64_t rows, int64_t d);
+/* dx_acc[r,:] += LN'(dy) (fp32, in place); if dx_copy != NULL also writes the
+ * updated dx_acc in copy_dtype; dgamma/dbeta accumulate (+=).                 */
+int msq_layernorm_bwd(float* dx_acc, void* dx_copy, int copy_dtype, float* dgamma, float* dbeta, const void* dy,
+                      int dy_dtype, const float* x, const float* mean, const float* rstd, const float* gamma,
+                      int64_t rows, int64_t d, void* workspace, void* stream);
+
+/* ---- GEMM (nn.Linear fwd/bwd: model_transformer.py:46,57-59,97-100,147;
+ * Mamba2 in_proj/out_proj). C[b] = op(A[b]) . op(B[b]) with
+ *   ta = 0: A stored [M,K] (K contiguous)     ta = 1: A stored [K,M]
+ *   tb = 0: B stored [N,K] (K contiguous)     tb = 1: B stored [K,N]
+ * dtype = MSQ_BF16: bf16 operands, fp32 accumulation on MFMA (fast path);
+ * dtype = MSQ_F32 : fp32 operands and accumulation (exact/parity path).
+ * c_dtype: output type (ACCUM requires fp32). aux is fp32 for BIAS_RESID,
+ * aux_dtype-typed for RELU_MASK. Leading dims must be multiples of 8.        */
+int msq_gemm(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+             int64_t strideA, const void* B, int64_t ldb, int64_t strideB, void* C, int c_dtype, int64_t ldc,
+             int64_t strideC, int64_t batch, int epilogue, const float* bias, const void* aux, int aux_dtype,
+             int64_t ld_aux, int64_t stride_aux, void* stream);
+
+/* column sums (bias gradients): out[c] (+)= sum_r x[r, c]                      */
+size_t msq_colsum_workspace(int64_t rows, int64_t cols);
+int msq_colsum(float* out, int accumulate, const void* x, int dtype, int64_t rows, int64_t cols, int64_t ld,
+               void* workspace, void* stream);
+
+/* elementwise cast (weights fp32 -> bf16 shadow etc.)                        */
+int msq_cast(void* dst, int dst_dtype, const void* src, int src_dtype, int64_t n, void* stream);
+
+/* ---- Adam (torch.optim.Adam, train_parallel.py:157,183; foreach formula)
+ * Optional p_shadow receives the updated parameters in bf16.                 */
+int msq_adam_step(float* p, const float* g, float* m, float* v, void* p_shadow, int64_t n, float lr, float beta1,
+                  float beta2, float eps, int64_t step, void* stream);
+
+
+/* ---- relative-position causal attention (HeadRelPos x n_heads +
+ * torch.cat, model_transformer.py:41-90). Per head h and batch b:
+ *   s(i,j) = (q_i.k_j + BD(i,j)) * scale, allowed iff j <= i or j < n_meta,
+ *   BD(i,j) = q_i.R[S-1-i+j] (j <= i) | 0 (j == i+1) | q_{i+1}.R[j-i-2] (j >= i+2)
+ * qkv: [B*S, ld_qkv] with q | k | v blocks of H*hs columns (head h at h*hs);
+ * R: [H, S_max, hs]; out: [B*S, ld_out]; lse: fp32 [B, H, S] (natural log).
+ * dtype MSQ_BF16 (flash MFMA kernels, hs == 128) or MSQ_F32 (exact path).   */
+int msq_relattn_fwd(int dtype, void* out, int64_t ld_out, float* lse, const void* qkv, int64_t ld_qkv,
+                    const void* R, int64_t B, int64_t S, int64_t H, int64_t hs, int64_t S_max, float scale,
+                    int64_t n_meta, void* stream);
+size_t msq_relattn_bwd_workspace(int dtype, int64_t B, int64_t S, int64_t H);
+/* dqkv (same layout as qkv) is overwritten; dR (fp32 [H, S_max, hs]) accumulates. */
+int msq_relattn_bwd(int dtype, void* dqkv, int64_t ld_dqkv, float* dR, const void* dout, int64_t ld_dout,
+                    const void* out, const float* lse, const void* qkv, int64_t ld_qkv, const void* R, int64_t B,
+                    int64_t S, int64_t H, int64_t hs, int64_t S_max, float scale, int64_t n_meta, void* workspace,
+                    void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -39,8 +39,12 @@ def skew_index(S: int):
 
 def rel_head(x, wq, wk, wv, R, scale):
     """One HeadRelPos (model_transformer.py:64-82): scores (q.k + skew(q.R)) * scale."""
-    B, S, _ = x.shape
-    q, k, v = x @ wq.t(), x @ wk.t(), x @ wv.t()
+    return rel_attention(x @ wq.t(), x @ wk.t(), x @ wv.t(), R, scale)
+
+
+def rel_attention(q, k, v, R, scale):
+    """Attention core of HeadRelPos given q, k, v [B,S,hs] and R [>=S, hs]."""
+    S = q.shape[1]
     ac = q @ k.transpose(1, 2)
     qr = q @ R[:S].t()                       # qr[b, i, r] = q_i . R[r]
     row, col, pad = skew_index(S)

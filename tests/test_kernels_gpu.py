@@ -1,0 +1,148 @@
+"""GPU parity of the building-block kernels against torch fp32 CPU references.
+
+Tolerances: fp32 path (exact mode) 1e-5 relative; bf16 path uses bf16-rounded
+inputs and fp32 accumulation, compared against an fp32 product of the SAME
+rounded inputs at 2e-3 relative (accumulation order only)."""
+import pytest
+import torch
+
+from midiseq import ops
+from midiseq import _lib as L
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-30)).item()
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 1), (1, 0)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 128), (130, 70, 72), (64, 17914 // 32 * 8 + 2, 64)])
+def test_gemm_layouts(ta, tb, dtype, M, N, K):
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    a = torch.randn(M, K, generator=g).to(dtype)
+    b = torch.randn(N, K, generator=g).to(dtype)
+    ref = a.float() @ b.float().t()
+    A = (a.t().contiguous() if ta else a).to(dev)
+    Bm = (b.t().contiguous() if tb else b).to(dev)
+    if (ta and M % 8) or (tb and N % 8):
+        pytest.skip("bf16/ld alignment needs ld % 8 == 0")
+    out = ops.gemm(A, Bm, ta=bool(ta), tb=bool(tb), out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    tol = 1e-5 if dtype == torch.float32 else 2e-3
+    assert _rel(out, ref) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogues(dtype):
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 200, 256, 192
+    a = torch.randn(M, K, generator=g).to(dtype)
+    w = torch.randn(N, K, generator=g).to(dtype)
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g)
+    base = a.float() @ w.float().t()
+    A, W, bi, R = a.to(dev), w.to(dev), bias.to(dev), res.to(dev)
+    tol = 1e-5 if dtype == torch.float32 else 2e-3
+    o = ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_BIAS, bias=bi)
+    assert _rel(o, base + bias) < tol
+    o = ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_BIAS_RELU, bias=bi)
+    assert _rel(o, torch.relu(base + bias)) < tol
+    o = ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_BIAS_RESID, bias=bi, aux=R)
+    assert _rel(o, base + bias + res) < tol
+    o = ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_RELU_MASK, aux=R)
+    assert _rel(o, base * (res > 0)) < tol
+    acc = R.clone()
+    ops.gemm(A, W, out=acc, epilogue=L.EPI_ACCUM)
+    assert _rel(acc, base + res) < tol
+    ob = ops.gemm(A, W, out_dtype=torch.bfloat16, epilogue=L.EPI_BIAS, bias=bi)
+    assert _rel(ob.float(), base + bias) < 1e-2
+
+
+def test_gemm_batched_strided():
+    g = torch.Generator().manual_seed(5)
+    Bt, S, T, d, V = 3, 70, 64, 128, 200
+    x = torch.randn(Bt, S, d, generator=g).bfloat16()
+    w = torch.randn(V, d, generator=g).bfloat16()
+    ref = (x[:, S - T:].float() @ w.float().t())
+    X = x.to(dev)
+    out = torch.empty(Bt, T, V + 8, device=dev)[:, :, :V]
+    ops.gemm(X[:, S - T:], w.to(dev), out=out)
+    assert _rel(out, ref) < 2e-3
+
+
+@pytest.mark.parametrize("d", [32, 128, 1024])
+@pytest.mark.parametrize("ydt", [torch.float32, torch.bfloat16])
+def test_layernorm(d, ydt):
+    g = torch.Generator().manual_seed(d)
+    rows = 333
+    x = torch.randn(rows, d, generator=g) * 3 + 1
+    gamma = torch.randn(d, generator=g)
+    beta = torch.randn(d, generator=g)
+    dy = torch.randn(rows, d, generator=g)
+    xr = x.clone().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    yref = torch.nn.functional.layer_norm(xr, (d,), gr, br, 1e-5)
+    yref.backward(dy)
+    y, mean, rstd = ops.layernorm_fwd(x.to(dev), gamma.to(dev), beta.to(dev), out_dtype=ydt)
+    assert _rel(y.float(), yref.detach()) < (1e-5 if ydt == torch.float32 else 1e-2)
+    acc = torch.ones(rows, d, device=dev)
+    dg = torch.zeros(d, device=dev)
+    db = torch.zeros(d, device=dev)
+    cp = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
+    ops.layernorm_bwd(acc, dy.to(dev), x.to(dev), mean, rstd, gamma.to(dev), dg, db, dx_copy=cp)
+    assert _rel(acc - 1, xr.grad) < 1e-5
+    assert _rel(dg, gr.grad) < 1e-5 and _rel(db, br.grad) < 1e-5
+    assert _rel(cp.float(), acc) < 1e-2
+
+
+def test_embedding():
+    g = torch.Generator().manual_seed(1)
+    V, MV, d, B, T = 50, 9, 64, 3, 17
+    tok = torch.randn(V, d, generator=g)
+    met = torch.randn(MV, d, generator=g)
+    idx = torch.randint(0, V, (B, T), generator=g)
+    meta = torch.randint(0, MV, (B, 6), generator=g)
+    ref = torch.cat([met[meta], tok[idx]], dim=1)
+    x = torch.empty(B, T + 6, d, device=dev)
+    ops.embed_fwd(x, tok.to(dev), met.to(dev), idx.to(dev), meta.to(dev))
+    assert torch.equal(x.cpu(), ref)
+    dx = torch.randn(B, T + 6, d, generator=g)
+    gt = torch.zeros(V, d, device=dev)
+    gm = torch.zeros(MV, d, device=dev)
+    ops.embed_bwd(gt, gm, dx.to(dev), idx.to(dev), meta.to(dev))
+    rt = torch.zeros(V, d).index_add_(0, idx.reshape(-1), dx[:, 6:].reshape(-1, d))
+    rm = torch.zeros(MV, d).index_add_(0, meta.reshape(-1), dx[:, :6].reshape(-1, d))
+    assert _rel(gt, rt) < 1e-5 and _rel(gm, rm) < 1e-5
+
+
+def test_colsum_and_cast():
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(1000, 300, generator=g)
+    out = torch.zeros(300, device=dev)
+    ops.colsum(x.to(dev), out)
+    assert _rel(out, x.sum(0)) < 1e-5
+    xb = torch.empty(1000, 300, device=dev, dtype=torch.bfloat16)
+    ops.cast(xb, x.to(dev))
+    assert torch.equal(xb.cpu(), x.bfloat16())
+
+
+def test_adam_matches_torch():
+    g = torch.Generator().manual_seed(4)
+    n = 10007
+    p0 = torch.randn(n, generator=g)
+    p = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.Adam([p], lr=5e-5)
+    P, M, Vv = p0.clone().to(dev), torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    sh = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    for step in range(1, 4):
+        gr = torch.randn(n, generator=g)
+        p.grad = gr.clone()
+        opt.step()
+        ops.adam_step(P, gr.to(dev), M, Vv, step, 5e-5, shadow=sh)
+    assert _rel(P, p.detach()) < 1e-6
+    assert torch.equal(sh.cpu(), P.cpu().bfloat16())
