@@ -23,9 +23,9 @@ SIGNATURES = {
     "msq_version": (_i, []),
     "msq_embed_fwd": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "msq_embed_bwd": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
-    "msq_layernorm_fwd": (_i, [_p, _i, _p, _p, _p, _p, _p, _i64, _i64, _f, _p]),
+    "msq_layernorm_fwd": (_i, [_p, _i, _p, _p, _p, _p, _p, _i64, _i64, _f, _i64, _i64, _p]),
     "msq_layernorm_bwd_workspace": (_sz, [_i64, _i64]),
-    "msq_layernorm_bwd": (_i, [_p, _p, _i, _p, _p, _p, _i, _p, _p, _p, _p, _i64, _i64, _p, _p]),
+    "msq_layernorm_bwd": (_i, [_p, _p, _i, _p, _p, _p, _i, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _p]),
     "msq_gemm": (_i, [_i, _i, _i, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _p, _i, _i64, _i64, _i64, _i,
                       _p, _p, _i, _i64, _i64, _p]),
     "msq_colsum_workspace": (_sz, [_i64, _i64]),
@@ -33,6 +33,14 @@ SIGNATURES = {
     "msq_cast": (_i, [_p, _i, _p, _i, _i64, _p]),
     "msq_adam_step": (_i, [_p, _p, _p, _p, _p, _i64, _f, _f, _f, _f, _i64, _p]),
     "msq_relattn_fwd": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64, _p]),
+    "msq_filtered_workspace": (_sz, [_i64, _i64, _i64]),
+    "msq_filtered_colstats": (_i, [_p, _p, _i, _i64, _i64, _i64, _i64, _p, _p]),
+    "msq_filtered_ce": (_i, [_p, _p, _i64, _p, _i, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _f,
+                             _p, _p, _p]),
+    "msq_filtered_logit": (_i, [_p, _i64, _p, _i, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p,
+                                _p, _p]),
+    "msq_filtered_logit_bwd": (_i, [_p, _i64, _p, _i64, _p, _i, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64,
+                                    _i64, _p, _p, _p]),
     "msq_relattn_bwd_workspace": (_sz, [_i, _i64, _i64, _i64]),
     "msq_relattn_bwd": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64,
                              _p, _p]),

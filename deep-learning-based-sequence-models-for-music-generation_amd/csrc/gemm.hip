@@ -27,7 +27,9 @@ struct GemmArgs {
     const float* bias;
     const void* aux; int64_t ldx, sX;
     int tiles_m, tiles_n, batch;
-    int vec;  // C / aux / bias rows allow 16-B vector access
+    int vec;     // C / aux / bias rows allow 16-B vector access
+    int ksplit;  // >1: K range split over blocks, ACCUM epilogue via fp32 atomics
+    int64_t kper;
 };
 
 __device__ __forceinline__ int swz_k(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -148,6 +150,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int tiles = g.tiles_m * g.tiles_n;
     int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int kslice = bid % g.ksplit;  // slices of one tile are adjacent (same XCD group)
+    bid /= g.ksplit;
     const int bz = bid / tiles;
     bid -= bz * tiles;
     // grouped ordering: 8 M-tiles share each sweep over N (L2 reuse of B)
@@ -172,8 +176,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
         for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     Stager<TA, TB> st;
-    const int nk = (int)((g.K + BK - 1) / BK);
-    st.load(g, A, B, m0, n0, 0, tid);
+    const int64_t kbeg = (int64_t)kslice * g.kper;
+    const int64_t kend = min<int64_t>(g.K, kbeg + g.kper);
+    const int nk = (int)((kend - kbeg + BK - 1) / BK);
+    st.load(g, A, B, m0, n0, (int)kbeg, tid);
     st.store(smem, smem + BM * BK * 2, tid);
     __syncthreads();
 
@@ -181,7 +187,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
         const int cur = kt & 1;
         char* sa = smem + cur * STAGE;
         char* sb = sa + BM * BK * 2;
-        if (kt + 1 < nk) st.load(g, A, B, m0, n0, (kt + 1) * BK, tid);
+        if (kt + 1 < nk) st.load(g, A, B, m0, n0, (int)(kbeg + (kt + 1) * BK), tid);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             bf16x8 af[4], bfr[4];
@@ -227,6 +233,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
                 for (int t = 0; t < 4; ++t) v[t] = x[t] > 0.f ? v[t] : 0.f;
             }
             TC* cp = C + m * g.ldc + n;
+            if (EPI == MSQ_EPI_ACCUM && g.ksplit > 1) {
+                const int na = nv < 0 ? -nv : nv;
+                for (int t = 0; t < na; ++t) atomicAdd((float*)cp + t, v[t]);
+                continue;
+            }
             if (EPI == MSQ_EPI_ACCUM) v += epi_load(cp, nv);
             epi_store(cp, v, nv);
         }
@@ -294,7 +305,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g, int ta, int t
 
 template <int TA, int TB, int EPI, typename TC, typename TX>
 void launch_bf16(const GemmArgs& g, hipStream_t s) {
-    const int nblk = g.tiles_m * g.tiles_n * g.batch;
+    const int nblk = g.tiles_m * g.tiles_n * g.batch * g.ksplit;
     hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, EPI, TC, TX>), dim3(nblk), dim3(NT), 0, s, g);
 }
 
@@ -366,6 +377,18 @@ extern "C" int msq_gemm(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t
         if (bias) vec = vec && ((uintptr_t)bias % 16 == 0);
         if (aux) vec = vec && (ld_aux % 4 == 0) && (stride_aux % 4 == 0) && ((uintptr_t)aux % (4 * xsz) == 0);
         g.vec = vec ? 1 : 0;
+    }
+    // split-K for skinny-output weight-gradient products (C += acc only)
+    g.ksplit = 1;
+    g.kper = ((K + BK - 1) / BK) * BK;
+    if (dtype == MSQ_BF16 && epilogue == MSQ_EPI_ACCUM) {
+        const int64_t nb = (int64_t)g.tiles_m * g.tiles_n * batch;
+        int64_t ks = (1024 + nb - 1) / nb;
+        ks = std::min<int64_t>(ks, std::max<int64_t>(1, K / 1024));
+        if (ks > 1) {
+            g.kper = ((K + ks - 1) / ks + BK - 1) / BK * BK;
+            g.ksplit = (int)((K + g.kper - 1) / g.kper);
+        }
     }
     hipStream_t s = (hipStream_t)stream;
     int rc;

@@ -1,0 +1,351 @@
+// Grammar-weighted "filtered" loss (train.py:79-138, train_parallel.py:83-141,
+// CrossEntropyLoss at :156,179) without materialising any [B,T,V] weights:
+//   W[b,t,:]  = wtab[bucket(src[b,t])]          (5 x V table, L2 resident)
+//   lse_t     = logsumexp over the TIME axis of logits[b,:,v]   (colstats)
+//   Z[b,t,v]  = -(o[b,t,v] - lse_t[b,v]) * W[b,t,v]             (filtered_logit)
+//   loss      = mean_{b,t} ( logsumexp_v Z[b,t,:] - Z[b,t,y] )
+// Backward for an upstream dZ (CE: dZ = (softmax_v Z - onehot y) * gs):
+//   dO = -W*dZ + softmax_t(o) * colsum_t(W*dZ)
+// Kernels: colstats (online max/sum over t, split over t), a row kernel (one
+// workgroup per 32 rows of one sequence; a row of V values stays in
+// registers; the column sums of W*dZ are accumulated in registers over the 32
+// rows and flushed with one atomic per column), and an elementwise finisher.
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int VPT = 4;             // values per thread per chunk (vector width)
+constexpr int CHUNK = NT * VPT;    // 1024 columns per chunk
+constexpr int MAXCH = 18;          // V <= 18432
+constexpr int ROWS = 32;           // rows per workgroup in the row kernel
+constexpr int TSPLIT = 16;         // time splits in colstats
+
+struct LossArgs {
+    const void* o; int64_t ld;
+    const int64_t* src; const int64_t* trg;
+    const float* wtab;
+    int64_t b0, b1, b2, b3;  // bucket boundaries (dyn-1, length-1, time-1, tempo-1)
+    int64_t B, T, V;
+};
+
+__device__ __forceinline__ int bucket_of(const LossArgs& a, int64_t tok) {
+    return (tok > a.b0) + (tok > a.b1) + (tok > a.b2) + (tok > a.b3);
+}
+
+template <typename T>
+__device__ __forceinline__ f32x4 ld4(const T* p, int64_t v, int64_t V) {
+    if (v + 4 <= V) return load4(p + v);
+    f32x4 x = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4 && v + i < V; ++i) x[i] = (float)p[v + i];
+    return x;
+}
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+    v = wave_max(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+__device__ __forceinline__ float block_sum(float v, float* red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// ---- colstats: partial (max, sumexp) over a time split, then merge
+template <typename T>
+__global__ __launch_bounds__(NT) void colstats_part_kernel(LossArgs a, float* __restrict__ part) {
+    const int64_t v = ((int64_t)blockIdx.x * NT + threadIdx.x) * VPT;
+    const int64_t b = blockIdx.y, ts = blockIdx.z;
+    const int64_t per = (a.T + TSPLIT - 1) / TSPLIT;
+    const int64_t t0 = ts * per, t1 = min(a.T, t0 + per);
+    if (v >= a.V) return;
+    const T* o = (const T*)a.o + b * a.T * a.ld;
+    f32x4 m = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY}, s = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int64_t t = t0; t < t1; ++t) {
+        const f32x4 x = ld4(o + t * a.ld, v, a.V);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float mn = fmaxf(m[i], x[i]);
+            s[i] = s[i] * expf(m[i] - mn) + expf(x[i] - mn);
+            m[i] = mn;
+        }
+    }
+    float* pm = part + ((b * TSPLIT + ts) * 2) * a.V;
+    for (int i = 0; i < 4 && v + i < a.V; ++i) {
+        pm[v + i] = m[i];
+        pm[a.V + v + i] = s[i];
+    }
+}
+
+__global__ void colstats_merge_kernel(LossArgs a, const float* __restrict__ part, float* __restrict__ col_lse) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= a.B * a.V) return;
+    const int64_t b = e / a.V, v = e % a.V;
+    float m = -INFINITY;
+    for (int ts = 0; ts < TSPLIT; ++ts) m = fmaxf(m, part[((b * TSPLIT + ts) * 2) * a.V + v]);
+    float s = 0.f;
+    for (int ts = 0; ts < TSPLIT; ++ts) {
+        const float pm = part[((b * TSPLIT + ts) * 2) * a.V + v];
+        if (pm != -INFINITY) s += part[((b * TSPLIT + ts) * 2 + 1) * a.V + v] * expf(pm - m);
+    }
+    col_lse[e] = m + logf(s);
+}
+
+// ---- row kernel. MODE 0: loss only; 1: CE train (loss + dO partial);
+// 2: given dZ (autograd of filtered_logit); 3: write Z (filtered_logit fwd)
+template <int MODE, typename T, typename TD>
+__global__ __launch_bounds__(NT) void row_kernel(LossArgs a, const float* __restrict__ col_lse,
+                                                 float* __restrict__ loss_rows, TD* __restrict__ dout, int64_t ldd,
+                                                 const float* __restrict__ dz, int64_t ldz,
+                                                 float* __restrict__ colsum, float gs, int64_t t_begin) {
+    __shared__ float red[4];
+    const int64_t nrows = a.T - t_begin;
+    const int64_t blocks_per_b = (nrows + ROWS - 1) / ROWS;
+    const int64_t b = blockIdx.x / blocks_per_b;
+    const int64_t r0 = t_begin + (blockIdx.x % blocks_per_b) * ROWS;
+    const int64_t r1 = min(a.T, r0 + ROWS);
+    const int tid = threadIdx.x;
+    const int nch = (int)((a.V + CHUNK - 1) / CHUNK);
+    const float* cl = col_lse + b * a.V;
+    f32x4 csum[MAXCH];
+#pragma unroll
+    for (int c = 0; c < MAXCH; ++c) csum[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    for (int64_t t = r0; t < r1; ++t) {
+        const int64_t row = b * a.T + t;
+        const T* o = (const T*)a.o + row * a.ld;
+        const float* w = a.wtab + bucket_of(a, a.src[row]) * a.V;
+        f32x4 z[MAXCH];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < MAXCH; ++c) {
+            const int64_t v = (int64_t)c * CHUNK + tid * VPT;
+            z[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (c < nch && v < a.V) {
+                const f32x4 ov = ld4(o, v, a.V), cv = ld4(cl, v, a.V), wv = ld4(w, v, a.V);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    z[c][i] = -(ov[i] - cv[i]) * wv[i];
+                    if (v + i < a.V) mx = fmaxf(mx, z[c][i]);
+                }
+            }
+        }
+        if (MODE == 3) {  // Z output
+            TD* zp = dout + (b * nrows + (t - t_begin)) * ldd;  // z rows [B, T - t_begin, V]
+#pragma unroll
+            for (int c = 0; c < MAXCH; ++c) {
+                const int64_t v = (int64_t)c * CHUNK + tid * VPT;
+                if (c < nch && v < a.V) {
+                    if (v + 4 <= a.V) store4(zp + v, z[c]);
+                    else for (int i = 0; v + i < a.V; ++i) zp[v + i] = (TD)z[c][i];
+                }
+            }
+            continue;
+        }
+        float lse = 0.f;
+        if (MODE == 0 || MODE == 1) {
+            mx = block_max(mx, red);
+            float se = 0.f;
+#pragma unroll
+            for (int c = 0; c < MAXCH; ++c) {
+                const int64_t v = (int64_t)c * CHUNK + tid * VPT;
+                if (c < nch && v < a.V) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (v + i < a.V) se += expf(z[c][i] - mx);
+                }
+            }
+            lse = mx + logf(block_sum(se, red));
+            if (tid == 0) {
+                const int64_t y = a.trg[row];
+                const float zy = -((float)((const T*)a.o)[row * a.ld + y] - cl[y]) * w[y];
+                loss_rows[row] = lse - zy;
+            }
+        }
+        if (MODE == 0) continue;
+        // dZ -> wg = W*dZ ; dO = -wg ; colsum += wg
+        const int64_t y = MODE == 1 ? a.trg[row] : -1;
+        TD* dp = dout + row * ldd;
+#pragma unroll
+        for (int c = 0; c < MAXCH; ++c) {
+            const int64_t v = (int64_t)c * CHUNK + tid * VPT;
+            if (c < nch && v < a.V) {
+                const f32x4 wv = ld4(w, v, a.V);
+                f32x4 g;
+                if (MODE == 1) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) g[i] = (expf(z[c][i] - lse) - (v + i == y ? 1.f : 0.f)) * gs;
+                } else {
+                    g = ld4(dz + (b * a.T + t) * ldz, v, a.V);
+                    g *= gs;
+                }
+                const f32x4 wg = wv * g;
+                csum[c] += wg;
+                if (v + 4 <= a.V) store4(dp + v, -wg);
+                else for (int i = 0; v + i < a.V; ++i) dp[v + i] = (TD)(-wg[i]);
+            }
+        }
+    }
+    if (MODE == 1 || MODE == 2) {
+#pragma unroll
+        for (int c = 0; c < MAXCH; ++c) {
+            const int64_t v = (int64_t)c * CHUNK + tid * VPT;
+            if (c < nch && v < a.V) {
+                for (int i = 0; i < 4 && v + i < a.V; ++i) atomicAdd(colsum + b * a.V + v + i, csum[c][i]);
+            }
+        }
+    }
+}
+
+// dO[b,t,v] += exp(o[b,t,v] - lse_t[b,v]) * colsum[b,v]
+template <typename T, typename TD>
+__global__ void finish_kernel(LossArgs a, const float* __restrict__ col_lse, const float* __restrict__ colsum,
+                              TD* __restrict__ dout, int64_t ldd) {
+    const int64_t V4 = (a.V + 3) / 4;
+    const int64_t total = a.B * a.T * V4;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = e / V4, v = (e % V4) * 4;
+        const int64_t b = row / a.T;
+        const f32x4 ov = ld4((const T*)a.o + row * a.ld, v, a.V);
+        const f32x4 cl = ld4(col_lse + b * a.V, v, a.V);
+        const f32x4 cs = ld4(colsum + b * a.V, v, a.V);
+        TD* dp = dout + row * ldd;
+        f32x4 d = ld4(dp, v, a.V);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d[i] += expf(ov[i] - cl[i]) * cs[i];
+        if (v + 4 <= a.V) store4(dp + v, d);
+        else for (int i = 0; v + i < a.V; ++i) dp[v + i] = (TD)d[i];
+    }
+}
+
+__global__ void mean_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+    __shared__ float red[4];
+    float s = 0.f;
+    for (int64_t i = threadIdx.x; i < n; i += NT) s += x[i];
+    s = block_sum(s, red);
+    if (threadIdx.x == 0) *out = s / (float)n;
+}
+
+LossArgs mk(const void* o, int64_t ld, const int64_t* src, const int64_t* trg, const float* wtab, int64_t b0,
+            int64_t b1, int64_t b2, int64_t b3, int64_t B, int64_t T, int64_t V) {
+    LossArgs a;
+    a.o = o; a.ld = ld; a.src = src; a.trg = trg; a.wtab = wtab;
+    a.b0 = b0; a.b1 = b1; a.b2 = b2; a.b3 = b3;
+    a.B = B; a.T = T; a.V = V;
+    return a;
+}
+
+template <typename T>
+void colstats_launch(const LossArgs& a, float* col_lse, float* part, hipStream_t s) {
+    dim3 grid((unsigned)((a.V + CHUNK - 1) / CHUNK), (unsigned)a.B, TSPLIT);
+    hipLaunchKernelGGL(colstats_part_kernel<T>, grid, dim3(NT), 0, s, a, part);
+    hipLaunchKernelGGL(colstats_merge_kernel, dim3((unsigned)((a.B * a.V + 255) / 256)), dim3(256), 0, s, a, part,
+                       col_lse);
+}
+
+}  // namespace
+
+extern "C" size_t msq_filtered_workspace(int64_t B, int64_t T, int64_t V) {
+    // colstats partials | colsum [B,V] | loss rows [B*T]
+    (void)T;
+    return (size_t)B * TSPLIT * 2 * V * 4 + (size_t)B * V * 4 + (size_t)B * T * 4 + 256;
+}
+
+#define LOSS_CHECK()                                                                                  \
+    MSQ_CHECK_ARG(B > 0 && T > 0 && V > 0 && V <= (int64_t)MAXCH * CHUNK && ld >= V && ld % 4 == 0,    \
+                  "filtered loss: bad sizes (V <= %d, ld %% 4 == 0)", MAXCH * CHUNK)
+
+extern "C" int msq_filtered_colstats(float* col_lse, const void* logits, int dtype, int64_t ld, int64_t B, int64_t T,
+                                     int64_t V, void* workspace, void* stream) {
+    LOSS_CHECK();
+    const LossArgs a = mk(logits, ld, nullptr, nullptr, nullptr, 0, 0, 0, 0, B, T, V);
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == MSQ_BF16) colstats_launch<bf16>(a, col_lse, (float*)workspace, s);
+    else colstats_launch<float>(a, col_lse, (float*)workspace, s);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
+extern "C" int msq_filtered_ce(float* loss, void* dlogits, int64_t ldd, const void* logits, int dtype, int64_t ld,
+                               const int64_t* src, const int64_t* trg, const float* wtab, int64_t b0, int64_t b1,
+                               int64_t b2, int64_t b3, int64_t B, int64_t T, int64_t V, float grad_scale,
+                               float* col_lse, void* workspace, void* stream) {
+    LOSS_CHECK();
+    MSQ_CHECK_ARG(!dlogits || ldd % 4 == 0, "msq_filtered_ce: ldd %% 4 != 0");
+    const LossArgs a = mk(logits, ld, src, trg, wtab, b0, b1, b2, b3, B, T, V);
+    hipStream_t s = (hipStream_t)stream;
+    char* ws = (char*)workspace;
+    float* part = (float*)ws;
+    float* colsum = (float*)(ws + (size_t)B * TSPLIT * 2 * V * 4);
+    float* rows = colsum + B * V;
+    const bool bfl = dtype == MSQ_BF16;
+    if (bfl) colstats_launch<bf16>(a, col_lse, part, s);
+    else colstats_launch<float>(a, col_lse, part, s);
+    const unsigned nblk = (unsigned)(B * ((T + ROWS - 1) / ROWS));
+    if (!dlogits) {
+        if (bfl) hipLaunchKernelGGL((row_kernel<0, bf16, float>), dim3(nblk), dim3(NT), 0, s, a, col_lse, rows, (float*)nullptr, 0, nullptr, 0, nullptr, 0.f, 0);
+        else hipLaunchKernelGGL((row_kernel<0, float, float>), dim3(nblk), dim3(NT), 0, s, a, col_lse, rows, (float*)nullptr, 0, nullptr, 0, nullptr, 0.f, 0);
+    } else {
+        hipMemsetAsync(colsum, 0, (size_t)B * V * 4, s);
+        const unsigned gf = (unsigned)std::min<int64_t>(B * T * ((V + 3) / 4) / 256 + 1, 16384);
+        if (bfl) {
+            hipLaunchKernelGGL((row_kernel<1, bf16, bf16>), dim3(nblk), dim3(NT), 0, s, a, col_lse, rows, (bf16*)dlogits, ldd, nullptr, 0, colsum, grad_scale, 0);
+            hipLaunchKernelGGL((finish_kernel<bf16, bf16>), dim3(gf), dim3(256), 0, s, a, col_lse, colsum, (bf16*)dlogits, ldd);
+        } else {
+            hipLaunchKernelGGL((row_kernel<1, float, float>), dim3(nblk), dim3(NT), 0, s, a, col_lse, rows, (float*)dlogits, ldd, nullptr, 0, colsum, grad_scale, 0);
+            hipLaunchKernelGGL((finish_kernel<float, float>), dim3(gf), dim3(256), 0, s, a, col_lse, colsum, (float*)dlogits, ldd);
+        }
+    }
+    hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(NT), 0, s, rows, B * T, loss);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
+extern "C" int msq_filtered_logit(float* z, int64_t ldz, const void* logits, int dtype, int64_t ld,
+                                  const int64_t* src, const float* wtab, int64_t b0, int64_t b1, int64_t b2,
+                                  int64_t b3, int64_t B, int64_t T, int64_t V, int64_t t_begin, float* col_lse,
+                                  void* workspace, void* stream) {
+    LOSS_CHECK();
+    MSQ_CHECK_ARG(t_begin >= 0 && t_begin < T && ldz % 4 == 0, "msq_filtered_logit: bad t_begin / ldz");
+    const LossArgs a = mk(logits, ld, src, nullptr, wtab, b0, b1, b2, b3, B, T, V);
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned nblk = (unsigned)(B * ((T - t_begin + ROWS - 1) / ROWS));
+    if (dtype == MSQ_BF16) {
+        colstats_launch<bf16>(a, col_lse, (float*)workspace, s);
+        hipLaunchKernelGGL((row_kernel<3, bf16, float>), dim3(nblk), dim3(NT), 0, s, a, col_lse, nullptr, z, ldz, nullptr, 0, nullptr, 0.f, t_begin);
+    } else {
+        colstats_launch<float>(a, col_lse, (float*)workspace, s);
+        hipLaunchKernelGGL((row_kernel<3, float, float>), dim3(nblk), dim3(NT), 0, s, a, col_lse, nullptr, z, ldz, nullptr, 0, nullptr, 0.f, t_begin);
+    }
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
+extern "C" int msq_filtered_logit_bwd(void* dlogits, int64_t ldd, const float* dz, int64_t ldz, const void* logits,
+                                      int dtype, int64_t ld, const int64_t* src, const float* wtab, int64_t b0,
+                                      int64_t b1, int64_t b2, int64_t b3, int64_t B, int64_t T, int64_t V,
+                                      const float* col_lse, void* workspace, void* stream) {
+    LOSS_CHECK();
+    const LossArgs a = mk(logits, ld, src, nullptr, wtab, b0, b1, b2, b3, B, T, V);
+    hipStream_t s = (hipStream_t)stream;
+    float* colsum = (float*)((char*)workspace + (size_t)B * TSPLIT * 2 * V * 4);
+    hipMemsetAsync(colsum, 0, (size_t)B * V * 4, s);
+    const unsigned nblk = (unsigned)(B * ((T + ROWS - 1) / ROWS));
+    const unsigned gf = (unsigned)std::min<int64_t>(B * T * ((V + 3) / 4) / 256 + 1, 16384);
+    if (dtype == MSQ_BF16) {
+        hipLaunchKernelGGL((row_kernel<2, bf16, bf16>), dim3(nblk), dim3(NT), 0, s, a, col_lse, nullptr, (bf16*)dlogits, ldd, dz, ldz, colsum, 1.f, 0);
+        hipLaunchKernelGGL((finish_kernel<bf16, bf16>), dim3(gf), dim3(256), 0, s, a, col_lse, colsum, (bf16*)dlogits, ldd);
+    } else {
+        hipLaunchKernelGGL((row_kernel<2, float, float>), dim3(nblk), dim3(NT), 0, s, a, col_lse, nullptr, (float*)dlogits, ldd, dz, ldz, colsum, 1.f, 0);
+        hipLaunchKernelGGL((finish_kernel<float, float>), dim3(gf), dim3(256), 0, s, a, col_lse, colsum, (float*)dlogits, ldd);
+    }
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}

@@ -56,15 +56,21 @@ extern "C" int msq_embed_bwd(float* g_tok, float* g_meta, const float* dx, const
 
 // ------------------------------------------------------------------ LayerNorm
 // one wave per row; the row (d <= 64*4*MAXC) is held in registers.
+// Row r of the compact output maps to input row
+//   (r / seg) * (seg + skip) + skip + r % seg      (identity when skip == 0)
+// so LN_f can normalise only the T token rows of every [meta | tokens] segment.
+__device__ __forceinline__ int64_t map_row(int64_t r, int64_t seg, int64_t skip) {
+    return skip == 0 ? r : (r / seg) * (seg + skip) + skip + r % seg;
+}
 template <typename TY, int MAXC>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(TY* __restrict__ y, float* __restrict__ mean,
                                                      float* __restrict__ rstd, const float* __restrict__ x,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                     int64_t rows, int d, float eps) {
+                                                     int64_t rows, int d, float eps, int64_t seg, int64_t skip) {
     const int lane = threadIdx.x & 63;
     const int64_t row = blockIdx.x * 4LL + (threadIdx.x >> 6);
     if (row >= rows) return;
-    const float* xr = x + row * d;
+    const float* xr = x + map_row(row, seg, skip) * d;
     f32x4 v[MAXC];
     float s = 0.f;
 #pragma unroll
@@ -107,20 +113,21 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
                                                      float* __restrict__ part, const TD* __restrict__ dy,
                                                      const float* __restrict__ x, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const float* __restrict__ gamma,
-                                                     int64_t rows, int d) {
+                                                     int64_t rows, int d, int64_t seg, int64_t skip) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     f32x4 pg[MAXC], pb[MAXC];
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) pg[c] = pb[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
     for (int64_t row = blockIdx.x * 4LL + wid; row < rows; row += (int64_t)gridDim.x * 4) {
         const float mu = mean[row], rs = rstd[row];
+        const int64_t xrow = map_row(row, seg, skip);
         f32x4 xh[MAXC], g[MAXC];
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int c = 0; c < MAXC; ++c) {
             const int col = (c * 64 + lane) * 4;
             if (col < d) {
-                const f32x4 xv = *(const f32x4*)(x + row * d + col);
+                const f32x4 xv = *(const f32x4*)(x + xrow * d + col);
                 const f32x4 dv = load4(dy + row * d + col);
                 const f32x4 gm = *(const f32x4*)(gamma + col);
 #pragma unroll
@@ -141,12 +148,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
         for (int c = 0; c < MAXC; ++c) {
             const int col = (c * 64 + lane) * 4;
             if (col < d) {
-                float* dp = dxa + row * d + col;
+                float* dp = dxa + xrow * d + col;
                 f32x4 o = *(f32x4*)dp;
 #pragma unroll
                 for (int t = 0; t < 4; ++t) o[t] += rs * (g[c][t] - m1 - xh[c][t] * m2);
                 *(f32x4*)dp = o;
-                if (dcopy) store4(dcopy + row * d + col, o);
+                if (dcopy) store4(dcopy + xrow * d + col, o);
             }
         }
     }
@@ -195,45 +202,50 @@ extern "C" size_t msq_layernorm_bwd_workspace(int64_t rows, int64_t d) {
 
 template <typename TY>
 static void ln_fwd_launch(TY* y, float* mean, float* rstd, const float* x, const float* g, const float* b,
-                          int64_t rows, int d, float eps, hipStream_t s) {
+                          int64_t rows, int d, float eps, int64_t seg, int64_t skip, hipStream_t s) {
     const dim3 grid((unsigned)((rows + 3) / 4));
-    if (d <= 256) hipLaunchKernelGGL((ln_fwd_kernel<TY, 1>), grid, dim3(256), 0, s, y, mean, rstd, x, g, b, rows, d, eps);
-    else if (d <= 1024) hipLaunchKernelGGL((ln_fwd_kernel<TY, 4>), grid, dim3(256), 0, s, y, mean, rstd, x, g, b, rows, d, eps);
-    else hipLaunchKernelGGL((ln_fwd_kernel<TY, 8>), grid, dim3(256), 0, s, y, mean, rstd, x, g, b, rows, d, eps);
+    if (d <= 256) hipLaunchKernelGGL((ln_fwd_kernel<TY, 1>), grid, dim3(256), 0, s, y, mean, rstd, x, g, b, rows, d, eps, seg, skip);
+    else if (d <= 1024) hipLaunchKernelGGL((ln_fwd_kernel<TY, 4>), grid, dim3(256), 0, s, y, mean, rstd, x, g, b, rows, d, eps, seg, skip);
+    else hipLaunchKernelGGL((ln_fwd_kernel<TY, 8>), grid, dim3(256), 0, s, y, mean, rstd, x, g, b, rows, d, eps, seg, skip);
 }
 
 extern "C" int msq_layernorm_fwd(void* y, int y_dtype, float* mean, float* rstd, const float* x, const float* gamma,
-                                 const float* beta, int64_t rows, int64_t d, float eps, void* stream) {
+                                 const float* beta, int64_t rows, int64_t d, float eps, int64_t seg_len,
+                                 int64_t seg_skip, void* stream) {
     MSQ_CHECK_ARG(d % 4 == 0 && d <= 2048 && rows > 0, "msq_layernorm_fwd: need d %% 4 == 0, d <= 2048");
+    MSQ_CHECK_ARG(seg_skip == 0 || seg_len > 0, "msq_layernorm_fwd: seg_len must be > 0 with seg_skip");
     hipStream_t s = (hipStream_t)stream;
-    if (y_dtype == MSQ_BF16) ln_fwd_launch((bf16*)y, mean, rstd, x, gamma, beta, rows, (int)d, eps, s);
-    else ln_fwd_launch((float*)y, mean, rstd, x, gamma, beta, rows, (int)d, eps, s);
+    if (y_dtype == MSQ_BF16) ln_fwd_launch((bf16*)y, mean, rstd, x, gamma, beta, rows, (int)d, eps, seg_len, seg_skip, s);
+    else ln_fwd_launch((float*)y, mean, rstd, x, gamma, beta, rows, (int)d, eps, seg_len, seg_skip, s);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }
 
 template <typename TD, typename TO>
 static void ln_bwd_launch(float* dxa, TO* dcopy, float* part, const TD* dy, const float* x, const float* mean,
-                          const float* rstd, const float* gamma, int64_t rows, int d, hipStream_t s) {
+                          const float* rstd, const float* gamma, int64_t rows, int d, int64_t seg, int64_t skip,
+                          hipStream_t s) {
     const dim3 grid(LN_BWD_BLOCKS);
-    if (d <= 256) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 1>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d);
-    else if (d <= 1024) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d);
-    else hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 8>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d);
+    if (d <= 256) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 1>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip);
+    else if (d <= 1024) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip);
+    else hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 8>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip);
 }
 
 extern "C" int msq_layernorm_bwd(float* dx_acc, void* dx_copy, int copy_dtype, float* dgamma, float* dbeta,
                                  const void* dy, int dy_dtype, const float* x, const float* mean, const float* rstd,
-                                 const float* gamma, int64_t rows, int64_t d, void* workspace, void* stream) {
+                                 const float* gamma, int64_t rows, int64_t d, int64_t seg_len, int64_t seg_skip,
+                                 void* workspace, void* stream) {
     MSQ_CHECK_ARG(d % 4 == 0 && d <= 2048 && rows > 0 && workspace, "msq_layernorm_bwd: bad args");
+    MSQ_CHECK_ARG(seg_skip == 0 || seg_len > 0, "msq_layernorm_bwd: seg_len must be > 0 with seg_skip");
     hipStream_t s = (hipStream_t)stream;
     float* part = (float*)workspace;
     const int di = (int)d;
     if (dy_dtype == MSQ_BF16) {
-        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, s);
-        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, s);
+        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, s);
+        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, s);
     } else {
-        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, s);
-        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, s);
+        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, s);
+        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, s);
     }
     hipLaunchKernelGGL(ln_reduce_kernel, dim3((unsigned)((2 * d + 255) / 256)), dim3(256), 0, s, dgamma, dbeta, part,
                        LN_BWD_BLOCKS, di);

@@ -43,13 +43,18 @@ def gemm(A, B, *, ta=False, tb=False, out=None, out_dtype=None, epilogue=L.EPI_N
     return out
 
 
-def layernorm_fwd(x, gamma, beta, eps=1e-5, out_dtype=torch.float32, out=None):
-    rows, d = x.numel() // x.shape[-1], x.shape[-1]
-    y = out if out is not None else torch.empty(x.shape, device=x.device, dtype=out_dtype)
-    mean = torch.empty(rows, device=x.device, dtype=torch.float32)
-    rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+def layernorm_fwd(x, gamma, beta, eps=1e-5, out_dtype=torch.float32, out=None, mean=None, rstd=None, seg=(0, 0)):
+    """seg=(seg_len, seg_skip): normalise only rows skip..skip+seg_len-1 of every
+    (seg_len+seg_skip)-row segment of x into a compact output."""
+    d = x.shape[-1]
+    rows = x.numel() // d
+    if seg[1]:
+        rows = rows // (seg[0] + seg[1]) * seg[0]
+    y = out if out is not None else torch.empty((rows, d), device=x.device, dtype=out_dtype)
+    mean = mean if mean is not None else torch.empty(rows, device=x.device, dtype=torch.float32)
+    rstd = rstd if rstd is not None else torch.empty(rows, device=x.device, dtype=torch.float32)
     call("msq_layernorm_fwd", ptr(y), dt(y), ptr(mean), ptr(rstd), ptr(x), ptr(gamma), ptr(beta), rows, d,
-         float(eps), stream())
+         float(eps), seg[0], seg[1], stream())
     return y, mean, rstd
 
 
@@ -65,13 +70,14 @@ def workspace(nbytes, device, tag="ws"):
     return buf
 
 
-def layernorm_bwd(dx_acc, dy, x, mean, rstd, gamma, dgamma, dbeta, dx_copy=None):
-    """dx_acc += LN'(dy); dgamma/dbeta += ...; optional copy of dx_acc."""
-    rows, d = x.numel() // x.shape[-1], x.shape[-1]
+def layernorm_bwd(dx_acc, dy, x, mean, rstd, gamma, dgamma, dbeta, dx_copy=None, seg=(0, 0)):
+    """dx_acc[map(r)] += LN'(dy[r]); dgamma/dbeta += ...; optional copy of the updated rows."""
+    d = x.shape[-1]
+    rows = mean.numel()
     ws = workspace(L.lib().msq_layernorm_bwd_workspace(rows, d), x.device, "ln")
     call("msq_layernorm_bwd", ptr(dx_acc), ptr(dx_copy), dt(dx_copy) if dx_copy is not None else L.F32,
-         ptr(dgamma), ptr(dbeta), ptr(dy), dt(dy), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), rows, d, ptr(ws),
-         stream())
+         ptr(dgamma), ptr(dbeta), ptr(dy), dt(dy), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), rows, d, seg[0], seg[1],
+         ptr(ws), stream())
 
 
 def colsum(x2d, out, accumulate=False):

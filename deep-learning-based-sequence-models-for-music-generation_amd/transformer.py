@@ -1,0 +1,446 @@
+"""Drop-in for models/transformer/model_transformer.py:136-168 (``Transformer``)
+backed by an explicit forward/backward engine over the HIP kernels.
+
+Layout in HBM (one allocation per kind, everything resident):
+  * parameters: ONE flat fp32 buffer (the nn.Parameter the optimiser sees),
+    every tensor 256-B aligned; a bf16 shadow with the same offsets feeds the
+    MFMA kernels (refreshed by the fused Adam kernel or lazily on version bump);
+  * gradients: ONE flat fp32 buffer with the same offsets (DDP buckets are
+    contiguous slices of it, in reverse layer order);
+  * the residual stream is fp32 [B*S, d]; matmul operands/activations are bf16
+    (or fp32 in the exact parity mode); the per-head q/k/v projections of the
+    reference are packed into one [3d, d] matrix (q heads | k heads | v heads),
+    so state_dict keys map to row slices of it.
+Names in state_dict() are exactly the reference's (406 keys incl. the 64
+``tril`` buffers, which are emitted as views of ONE shared mask)."""
+import math
+from collections import OrderedDict
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from . import ops
+from .attention import relattn_fwd, relattn_bwd
+from .config import N_META, VOCAB_SIZE, METADATA_VOCAB_SIZE, BLOCK_LEN
+
+
+@dataclass
+class TransformerConfig:
+    n_embd: int = 1024
+    n_heads: int = 8
+    n_layer: int = 8
+    block_len: int = BLOCK_LEN
+    dropout: float = 0.0
+    vocab_size: int = VOCAB_SIZE
+    metadata_vocab_size: int = METADATA_VOCAB_SIZE
+    precision: str = "bf16"  # "bf16" (MFMA fast path) | "fp32" (exact parity path)
+
+    @property
+    def head_size(self):
+        return self.n_embd // self.n_heads
+
+    @property
+    def s_max(self):
+        return self.block_len + N_META
+
+    @property
+    def v_pad(self):
+        return (self.vocab_size + 7) // 8 * 8
+
+    @classmethod
+    def from_params(cls, params, **kw):
+        """Accepts the reference's SimpleNamespace (train_parallel.py:49-54)."""
+        return cls(n_embd=params.n_embd, n_heads=params.n_heads, n_layer=params.n_layer,
+                   block_len=params.block_len, dropout=getattr(params, "dropout", 0.0),
+                   vocab_size=params.vocab_size, metadata_vocab_size=params.metadata_vocab_size, **kw)
+
+
+def _align(n, a=64):
+    return (n + a - 1) // a * a
+
+
+class ParamLayout:
+    """Offsets of every tensor inside the flat buffer."""
+
+    def __init__(self, cfg: TransformerConfig):
+        d, H, hs = cfg.n_embd, cfg.n_heads, cfg.head_size
+        entries = [("tok_emb", (cfg.vocab_size, d)), ("meta_emb", (cfg.metadata_vocab_size, d))]
+        for l in range(cfg.n_layer):
+            entries += [(f"{l}.ln1_w", (d,)), (f"{l}.ln1_b", (d,)), (f"{l}.wqkv", (3 * d, d)),
+                        (f"{l}.R", (H, cfg.s_max, hs)), (f"{l}.wproj", (d, d)), (f"{l}.bproj", (d,)),
+                        (f"{l}.ln2_w", (d,)), (f"{l}.ln2_b", (d,)), (f"{l}.w1", (4 * d, d)), (f"{l}.b1", (4 * d,)),
+                        (f"{l}.w2", (d, 4 * d)), (f"{l}.b2", (d,))]
+        entries += [("lnf_w", (d,)), ("lnf_b", (d,)), ("lm_w", (cfg.v_pad, d)), ("lm_b", (cfg.v_pad,))]
+        self.entries, self.offsets = entries, {}
+        off = 0
+        for name, shape in entries:
+            self.offsets[name] = (off, shape)
+            off += _align(math.prod(shape))
+        self.numel = off
+
+    def layer_range(self, l):
+        """[start, end) of layer l's tensors (a contiguous DDP bucket)."""
+        s = self.offsets[f"{l}.ln1_w"][0]
+        e = self.offsets[f"{l}.b2"][0] + _align(self.offsets[f"{l}.b2"][1][0])
+        return s, e
+
+    def views(self, flat):
+        out = {}
+        for name, (off, shape) in self.offsets.items():
+            out[name] = flat[off:off + math.prod(shape)].view(shape)
+        return out
+
+
+def reference_keys(cfg: TransformerConfig):
+    """Reference state_dict key -> (internal name, row slice or head index)."""
+    d, hs = cfg.n_embd, cfg.head_size
+    m = OrderedDict()
+    m["token_embedding_table.weight"] = ("tok_emb", None)
+    m["metadata_embedding_table.weight"] = ("meta_emb", None)
+    for l in range(cfg.n_layer):
+        for h in range(cfg.n_heads):
+            p = f"blocks.{l}.sa.heads.{h}."
+            m[p + "rel_pos_emb"] = (f"{l}.R", ("head", h))
+            m[p + "tril"] = ("__tril__", None)
+            m[p + "key.weight"] = (f"{l}.wqkv", ("rows", d + h * hs, d + (h + 1) * hs))
+            m[p + "query.weight"] = (f"{l}.wqkv", ("rows", h * hs, (h + 1) * hs))
+            m[p + "value.weight"] = (f"{l}.wqkv", ("rows", 2 * d + h * hs, 2 * d + (h + 1) * hs))
+        p = f"blocks.{l}."
+        m[p + "sa.proj.weight"] = (f"{l}.wproj", None)
+        m[p + "sa.proj.bias"] = (f"{l}.bproj", None)
+        m[p + "ffwd.net.0.weight"] = (f"{l}.w1", None)
+        m[p + "ffwd.net.0.bias"] = (f"{l}.b1", None)
+        m[p + "ffwd.net.2.weight"] = (f"{l}.w2", None)
+        m[p + "ffwd.net.2.bias"] = (f"{l}.b2", None)
+        m[p + "ln1.weight"] = (f"{l}.ln1_w", None)
+        m[p + "ln1.bias"] = (f"{l}.ln1_b", None)
+        m[p + "ln2.weight"] = (f"{l}.ln2_w", None)
+        m[p + "ln2.bias"] = (f"{l}.ln2_b", None)
+    m["ln_f.weight"] = ("lnf_w", None)
+    m["ln_f.bias"] = ("lnf_b", None)
+    m["lm_head.weight"] = ("lm_w", ("rows", 0, cfg.vocab_size))
+    m["lm_head.bias"] = ("lm_b", ("rows", 0, cfg.vocab_size))
+    return m
+
+
+def _select(t, sel):
+    if sel is None:
+        return t
+    if sel[0] == "head":
+        return t[sel[1]]
+    return t[sel[1]:sel[2]]
+
+
+def tril_mask(n, device="cpu"):
+    """generate_matrix(n, 1) (model_transformer.py:8-16) without the python loop."""
+    i = torch.arange(n, device=device)[:, None]
+    j = torch.arange(n, device=device)[None, :]
+    return ((j <= i) | (j < N_META)).to(torch.float32)
+
+
+class _Acts:
+    """Activation + scratch buffers for one (B, T), reused across steps."""
+
+    def __init__(self, cfg, B, T, device, act):
+        d, H = cfg.n_embd, cfg.n_heads
+        S = T + N_META
+        M = B * S
+        Lc = cfg.n_layer
+        f32 = torch.float32
+        e = lambda *s, dt=act: torch.empty(*s, device=device, dtype=dt)  # noqa: E731
+        self.B, self.T, self.S, self.M = B, T, S, M
+        self.x = e(Lc + 1, M, d, dt=f32)
+        self.xm = e(Lc, M, d, dt=f32)
+        self.a, self.c = e(Lc, M, d), e(Lc, M, d)
+        self.st1, self.st2 = e(Lc, 2, M, dt=f32), e(Lc, 2, M, dt=f32)
+        self.qkv = e(Lc, M, 3 * d)
+        self.o = e(Lc, M, d)
+        self.lse = e(Lc, B, H, S, dt=f32)
+        self.h = e(Lc, M, 4 * d)
+        self.f = e(B * T, d)
+        self.stf = e(2, B * T, dt=f32)
+        self.logits = e(B * T, cfg.v_pad)
+        self.gen = 0
+        self._bwd = None
+
+    def bwd(self, cfg, device, act):
+        if self._bwd is None:
+            d = cfg.n_embd
+            M = self.M
+            f32 = torch.float32
+            e = lambda *s, dt=act: torch.empty(*s, device=device, dtype=dt)  # noqa: E731
+            self._bwd = dict(gres=e(M, d, dt=f32), gb=e(M, d) if act != f32 else None, dtmp=e(M, d),
+                             dh=e(M, 4 * d), dqkv=e(M, 3 * d), df=e(self.B * self.T, d),
+                             dlogits=e(self.B * self.T, cfg.v_pad))
+        return self._bwd
+
+
+class TransformerEngine:
+    """Explicit forward / backward over the libmidiseq kernels."""
+
+    def __init__(self, cfg: TransformerConfig, flat: torch.Tensor):
+        if cfg.dropout not in (0, 0.0):
+            raise NotImplementedError("dropout > 0 is not implemented in this engine yet (use dropout=0)")
+        self.cfg = cfg
+        self.layout = ParamLayout(cfg)
+        self.act = torch.bfloat16 if cfg.precision == "bf16" else torch.float32
+        self.bind(flat)
+        self._acts = {}
+
+    def bind(self, flat):
+        self.flat = flat
+        self.device = flat.device
+        self.P = self.layout.views(flat.data)
+        if self.act == torch.bfloat16:
+            self.shadow = torch.empty(self.layout.numel, device=flat.device, dtype=torch.bfloat16)
+            self.W = self.layout.views(self.shadow)
+        else:
+            self.shadow = None
+            self.W = self.P
+        self._shadow_version = None
+
+    def refresh_shadow(self, force=False):
+        if self.shadow is None:
+            return
+        v = self.flat._version
+        if force or v != self._shadow_version:
+            ops.cast(self.shadow, self.flat.data)
+            self._shadow_version = self.flat._version
+
+    def mark_shadow_fresh(self):
+        self._shadow_version = self.flat._version
+
+    def acts(self, B, T):
+        key = (B, T)
+        if key not in self._acts:
+            self._acts.clear()
+            self._acts[key] = _Acts(self.cfg, B, T, self.device, self.act)
+        return self._acts[key]
+
+    # ------------------------------------------------------------- forward
+    def forward(self, idx, meta):
+        cfg, P, W = self.cfg, self.P, self.W
+        if not idx.is_cuda:
+            raise RuntimeError("the MI355X engine runs on the GPU only (no CPU fallback)")
+        self.refresh_shadow()
+        B, T = idx.shape
+        if T + N_META > cfg.s_max:
+            raise ValueError(f"sequence of {T} tokens exceeds block_len {cfg.block_len}")
+        A = self.acts(B, T)
+        A.gen += 1
+        d, H, hs, S = cfg.n_embd, cfg.n_heads, cfg.head_size, T + N_META
+        scale = d ** -0.5  # C**-0.5 with C = n_embd (model_transformer.py:65,77)
+        idx = idx.contiguous()
+        meta = meta.contiguous()
+        self._idx, self._meta = idx, meta
+        ops.embed_fwd(A.x[0].view(B, S, d), P["tok_emb"], P["meta_emb"], idx, meta)
+        for l in range(cfg.n_layer):
+            x = A.x[l]
+            ops.layernorm_fwd(x, P[f"{l}.ln1_w"], P[f"{l}.ln1_b"], out=A.a[l], mean=A.st1[l, 0], rstd=A.st1[l, 1])
+            ops.gemm(A.a[l], W[f"{l}.wqkv"], out=A.qkv[l])
+            relattn_fwd(A.qkv[l], W[f"{l}.R"], B, S, H, hs, scale, out=A.o[l], lse=A.lse[l])
+            ops.gemm(A.o[l], W[f"{l}.wproj"], out=A.xm[l], epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.bproj"], aux=x)
+            ops.layernorm_fwd(A.xm[l], P[f"{l}.ln2_w"], P[f"{l}.ln2_b"], out=A.c[l], mean=A.st2[l, 0],
+                              rstd=A.st2[l, 1])
+            ops.gemm(A.c[l], W[f"{l}.w1"], out=A.h[l], epilogue=L.EPI_BIAS_RELU, bias=P[f"{l}.b1"])
+            ops.gemm(A.h[l], W[f"{l}.w2"], out=A.x[l + 1], epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.b2"], aux=A.xm[l])
+        ops.layernorm_fwd(A.x[cfg.n_layer], P["lnf_w"], P["lnf_b"], out=A.f, mean=A.stf[0], rstd=A.stf[1],
+                          seg=(T, N_META))
+        V = cfg.vocab_size
+        ops.gemm(A.f, W["lm_w"][:V], out=A.logits[:, :V], epilogue=L.EPI_BIAS, bias=P["lm_b"][:V])
+        return A.logits.view(B, T, cfg.v_pad)[:, :, :V]
+
+    # ------------------------------------------------------------ backward
+    def backward(self, dlogits, grads):
+        """dlogits: [B*T, ld] (act dtype) whose first V columns are dL/dlogits;
+        grads: flat fp32 buffer (accumulated)."""
+        cfg, P, W = self.cfg, self.P, self.W
+        G = self.layout.views(grads)
+        idx, meta = self._idx, self._meta
+        B, T = idx.shape
+        A = self.acts(B, T)
+        Bw = A.bwd(cfg, self.device, self.act)
+        d, H, hs, S, M, V = cfg.n_embd, cfg.n_heads, cfg.head_size, T + N_META, A.M, cfg.vocab_size
+        scale = d ** -0.5
+        dl = dlogits[:, :V]
+        # lm_head (model_transformer.py:147,161)
+        ops.gemm(dl, A.f, ta=True, tb=True, out=G["lm_w"][:V], epilogue=L.EPI_ACCUM)
+        ops.colsum(dl, G["lm_b"][:V], accumulate=True)
+        ops.gemm(dl, W["lm_w"][:V], tb=True, out=Bw["df"])
+        gres = Bw["gres"]
+        gres.zero_()
+        gb = Bw["gb"] if Bw["gb"] is not None else gres
+        if Bw["gb"] is not None:
+            gb.zero_()
+        ops.layernorm_bwd(gres, Bw["df"], A.x[cfg.n_layer], A.stf[0], A.stf[1], P["lnf_w"], G["lnf_w"], G["lnf_b"],
+                          dx_copy=Bw["gb"], seg=(T, N_META))
+        hook = getattr(self, "layer_grad_ready", None)
+        for l in reversed(range(cfg.n_layer)):
+            # FFN (model_transformer.py:92-105,120)
+            ops.gemm(gb, A.h[l], ta=True, tb=True, out=G[f"{l}.w2"], epilogue=L.EPI_ACCUM)
+            ops.colsum(gres, G[f"{l}.b2"], accumulate=True)
+            ops.gemm(gb, W[f"{l}.w2"], tb=True, out=Bw["dh"], epilogue=L.EPI_RELU_MASK, aux=A.h[l])
+            ops.gemm(Bw["dh"], A.c[l], ta=True, tb=True, out=G[f"{l}.w1"], epilogue=L.EPI_ACCUM)
+            ops.colsum(Bw["dh"], G[f"{l}.b1"], accumulate=True)
+            ops.gemm(Bw["dh"], W[f"{l}.w1"], tb=True, out=Bw["dtmp"])
+            ops.layernorm_bwd(gres, Bw["dtmp"], A.xm[l], A.st2[l, 0], A.st2[l, 1], P[f"{l}.ln2_w"], G[f"{l}.ln2_w"],
+                              G[f"{l}.ln2_b"], dx_copy=Bw["gb"])
+            # attention (model_transformer.py:41-90,119)
+            ops.gemm(gb, A.o[l], ta=True, tb=True, out=G[f"{l}.wproj"], epilogue=L.EPI_ACCUM)
+            ops.colsum(gres, G[f"{l}.bproj"], accumulate=True)
+            ops.gemm(gb, W[f"{l}.wproj"], tb=True, out=Bw["dtmp"])
+            relattn_bwd(Bw["dtmp"], A.o[l], A.lse[l], A.qkv[l], W[f"{l}.R"], B, S, H, hs, scale, dqkv=Bw["dqkv"],
+                        dR=G[f"{l}.R"])
+            ops.gemm(Bw["dqkv"], A.a[l], ta=True, tb=True, out=G[f"{l}.wqkv"], epilogue=L.EPI_ACCUM)
+            ops.gemm(Bw["dqkv"], W[f"{l}.wqkv"], tb=True, out=Bw["dtmp"])
+            ops.layernorm_bwd(gres, Bw["dtmp"], A.x[l], A.st1[l, 0], A.st1[l, 1], P[f"{l}.ln1_w"], G[f"{l}.ln1_w"],
+                              G[f"{l}.ln1_b"], dx_copy=Bw["gb"])
+            if hook is not None:
+                hook(l)
+        ops.embed_bwd(G["tok_emb"], G["meta_emb"], gres, idx, meta)
+        if hook is not None:
+            hook(-1)
+
+    def dlogits_buffer(self, B, T):
+        A = self.acts(B, T)
+        return A.bwd(self.cfg, self.device, self.act)["dlogits"]
+
+
+class _TransformerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, flat, idx, meta, engine):
+        logits = engine.forward(idx, meta)
+        A = engine.acts(*idx.shape)
+        ctx.engine, ctx.gen, ctx.shape = engine, A.gen, tuple(idx.shape)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        eng = ctx.engine
+        A = eng.acts(*ctx.shape)
+        if A.gen != ctx.gen:
+            raise RuntimeError("activations were overwritten by a later forward; call backward before the next forward")
+        B, T = ctx.shape
+        cfg = eng.cfg
+        if dlogits.dtype == eng.act and dlogits.stride(2) == 1 and dlogits.stride(1) % 8 == 0 and \
+                dlogits.stride(0) == T * dlogits.stride(1):
+            dl2 = dlogits.as_strided((B * T, dlogits.stride(1)), (dlogits.stride(1), 1))
+        else:
+            buf = eng.dlogits_buffer(B, T)
+            buf.view(B, T, cfg.v_pad)[:, :, :cfg.vocab_size].copy_(dlogits)
+            dl2 = buf
+        grads = torch.zeros_like(eng.flat.data)
+        eng.backward(dl2, grads)
+        return grads, None, None, None
+
+
+class Transformer(nn.Module):
+    """Transformer(params) drop-in (model_transformer.py:136-168).
+
+    forward(idx [B,T] int64, metadata_idx [B,6] int64) -> logits [B,T,V] (fp32
+    in the exact mode, bf16 in the bf16 mode; a view into a padded buffer)."""
+
+    def __init__(self, params, device=None, precision=None):
+        super().__init__()
+        cfg = params if isinstance(params, TransformerConfig) else TransformerConfig.from_params(params)
+        if precision is not None:
+            cfg.precision = precision
+        self.cfg = cfg
+        self.vocab_size = cfg.vocab_size
+        self.metadata_vocab_size = cfg.metadata_vocab_size
+        layout = ParamLayout(cfg)
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        self.flat = nn.Parameter(torch.zeros(layout.numel, device=dev))
+        self._engine = None
+        self.reset_parameters()
+
+    # -- parameters --------------------------------------------------------
+    def reset_parameters(self, seed=0):
+        """PyTorch-default-like init (nn.Linear / nn.Embedding / randn rel_pos_emb)."""
+        g = torch.Generator().manual_seed(seed)
+        V = self.layout.views(self.flat.data)
+        with torch.no_grad():
+            for name, (_, shape) in self.layout.offsets.items():
+                t = V[name]
+                leaf = name.split(".")[-1]
+                if leaf in ("ln1_w", "ln2_w", "lnf_w"):
+                    t.fill_(1.0)
+                elif leaf in ("ln1_b", "ln2_b", "lnf_b"):
+                    t.zero_()
+                elif name in ("tok_emb", "meta_emb") or leaf == "R":
+                    t.copy_(torch.randn(shape, generator=g))
+                elif leaf in ("wqkv", "wproj", "w1", "w2", "lm_w"):
+                    bound = 1.0 / math.sqrt(shape[1])
+                    t.copy_(torch.empty(shape).uniform_(-bound, bound, generator=g))
+                else:  # biases
+                    fan_in = self.cfg.n_embd if leaf != "b2" else 4 * self.cfg.n_embd
+                    bound = 1.0 / math.sqrt(fan_in)
+                    t.copy_(torch.empty(shape).uniform_(-bound, bound, generator=g))
+            if self.cfg.v_pad > self.cfg.vocab_size:
+                V["lm_w"][self.cfg.vocab_size:].zero_()
+                V["lm_b"][self.cfg.vocab_size:].zero_()
+        self._engine = None
+
+    @property
+    def layout(self):
+        return ParamLayout(self.cfg)
+
+    @property
+    def engine(self):
+        if self._engine is None or self._engine.flat is not self.flat or self._engine.device != self.flat.device:
+            self._engine = TransformerEngine(self.cfg, self.flat)
+        return self._engine
+
+    def _apply(self, fn, *a, **k):
+        out = super()._apply(fn, *a, **k)
+        self._engine = None
+        return out
+
+    def forward(self, idx, metadata_idx, targets=None):
+        return _TransformerFn.apply(self.flat, idx, metadata_idx, self.engine)
+
+    def get_name(self):
+        return "Transformer"
+
+    # -- reference-compatible state_dict ------------------------------------
+    def state_dict(self, *args, destination=None, prefix="", keep_vars=False, with_tril=True):
+        V = self.layout.views(self.flat if keep_vars else self.flat.detach())
+        out = OrderedDict() if destination is None else destination
+        tril = None
+        for key, (name, sel) in reference_keys(self.cfg).items():
+            if name == "__tril__":
+                if not with_tril:
+                    continue
+                if tril is None:
+                    tril = tril_mask(self.cfg.s_max, self.flat.device)
+                out[prefix + key] = tril
+                continue
+            out[prefix + key] = _select(V[name], sel)
+        return out
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        V = self.layout.views(self.flat.data)
+        keys = reference_keys(self.cfg)
+        missing = [k for k, (n, _) in keys.items() if n != "__tril__" and k not in state_dict]
+        unexpected = [k for k in state_dict if k not in keys]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"state_dict mismatch: missing {missing[:5]}, unexpected {unexpected[:5]}")
+        with torch.no_grad():
+            for k, (name, sel) in keys.items():
+                if name == "__tril__" or k not in state_dict:
+                    continue
+                dst = _select(V[name], sel)
+                src = state_dict[k]
+                if tuple(src.shape) != tuple(dst.shape):
+                    raise RuntimeError(f"{k}: shape {tuple(src.shape)} != {tuple(dst.shape)}")
+                dst.copy_(src)
+        if self._engine is not None:
+            self._engine.refresh_shadow(force=True)
+        return torch.nn.modules.module._IncompatibleKeys(missing, unexpected)
+
+    def grad_dict(self):
+        """Reference-named views of flat.grad (for parity checks)."""
+        V = self.layout.views(self.flat.grad)
+        return OrderedDict((k, _select(V[n], s)) for k, (n, s) in reference_keys(self.cfg).items() if n != "__tril__")

@@ -57,15 +57,19 @@ int msq_embed_bwd(float* g_tok, float* g_meta, const float* dx, const int64_t* i
                   int64_t B, int64_t T, int64_t n_meta, int64_t d, void* stream);
 
 /* ---- LayerNorm (nn.LayerNorm, model_transformer.py:115-116,146; mamba.py:25)
- * y = (x - mean) * rstd * gamma + beta; x fp32 [rows, d]; y in y_dtype.      */
+ * y = (x - mean) * rstd * gamma + beta; x fp32; y in y_dtype, compact [rows, d].
+ * Output row r reads input row (r/seg_len)*(seg_len+seg_skip)+seg_skip+r%seg_len
+ * (seg_skip = 0: identity) -- LN_f normalises only the token rows that feed
+ * lm_head (model_transformer.py:160-164 slices them off afterwards).         */
 int msq_layernorm_fwd(void* y, int y_dtype, float* mean, float* rstd, const float* x, const float* gamma,
-                      const float* beta, int64_t rows, int64_t d, float eps, void* stream);
+                      const float* beta, int64_t rows, int64_t d, float eps, int64_t seg_len, int64_t seg_skip,
+                      void* stream);
 size_t msq_layernorm_bwd_workspace(int64_t rows, int64_t d);
-/* dx_acc[r,:] += LN'(dy) (fp32, in place); if dx_copy != NULL also writes the
- * updated dx_acc in copy_dtype; dgamma/dbeta accumulate (+=).                 */
+/* dx_acc[map(r),:] += LN'(dy[r]) (fp32, in place); if dx_copy != NULL also
+ * writes the updated rows in copy_dtype; dgamma/dbeta accumulate (+=).       */
 int msq_layernorm_bwd(float* dx_acc, void* dx_copy, int copy_dtype, float* dgamma, float* dbeta, const void* dy,
                       int dy_dtype, const float* x, const float* mean, const float* rstd, const float* gamma,
-                      int64_t rows, int64_t d, void* workspace, void* stream);
+                      int64_t rows, int64_t d, int64_t seg_len, int64_t seg_skip, void* workspace, void* stream);
 
 /* ---- GEMM (nn.Linear fwd/bwd: model_transformer.py:46,57-59,97-100,147;
  * Mamba2 in_proj/out_proj). C[b] = op(A[b]) . op(B[b]) with
@@ -110,6 +114,31 @@ int msq_relattn_bwd(int dtype, void* dqkv, int64_t ld_dqkv, float* dR, const voi
                     const void* out, const float* lse, const void* qkv, int64_t ld_qkv, const void* R, int64_t B,
                     int64_t S, int64_t H, int64_t hs, int64_t S_max, float scale, int64_t n_meta, void* workspace,
                     void* stream);
+
+/* ---- grammar-weighted filtered loss (train.py:79-138; CrossEntropyLoss,
+ * train_parallel.py:156,179). logits [B,T,ld] (ld >= V, ld % 4 == 0) in dtype;
+ * wtab fp32 [5,V] (make_distributions); b0..b3 = bucketize boundaries
+ * (dyn-1, length-1, time-1, tempo-1); col_lse fp32 [B,V] receives the
+ * log-sum-exp over the time axis.                                            */
+size_t msq_filtered_workspace(int64_t B, int64_t T, int64_t V);
+int msq_filtered_colstats(float* col_lse, const void* logits, int dtype, int64_t ld, int64_t B, int64_t T, int64_t V,
+                          void* workspace, void* stream);
+/* loss (fp32 scalar, device) = mean over B*T of the row CE of Z. If dlogits
+ * != NULL also writes grad_scale * d(sum of row CE)/dlogits (so grad_scale =
+ * 1/(B*T) gives the gradient of the mean).                                  */
+int msq_filtered_ce(float* loss, void* dlogits, int64_t ldd, const void* logits, int dtype, int64_t ld,
+                    const int64_t* src, const int64_t* trg, const float* wtab, int64_t b0, int64_t b1, int64_t b2,
+                    int64_t b3, int64_t B, int64_t T, int64_t V, float grad_scale, float* col_lse, void* workspace,
+                    void* stream);
+/* Z rows t_begin..T-1 (fp32, [B, T-t_begin, ldz]) = filtered_logit(src, logits). */
+int msq_filtered_logit(float* z, int64_t ldz, const void* logits, int dtype, int64_t ld, const int64_t* src,
+                       const float* wtab, int64_t b0, int64_t b1, int64_t b2, int64_t b3, int64_t B, int64_t T,
+                       int64_t V, int64_t t_begin, float* col_lse, void* workspace, void* stream);
+/* dlogits = d filtered_logit^T dz (col_lse from msq_filtered_logit).        */
+int msq_filtered_logit_bwd(void* dlogits, int64_t ldd, const float* dz, int64_t ldz, const void* logits, int dtype,
+                           int64_t ld, const int64_t* src, const float* wtab, int64_t b0, int64_t b1, int64_t b2,
+                           int64_t b3, int64_t B, int64_t T, int64_t V, const float* col_lse, void* workspace,
+                           void* stream);
 
 #ifdef __cplusplus
 }

@@ -39,5 +39,5 @@ def test_error_plumbing(built):
     # argument validation runs on the host, no GPU needed
     rc = L.msq_gemm(7, 0, 0, 1, 1, 1, None, 1, 0, None, 1, 0, None, 0, 1, 0, 1, 0, None, None, 0, 0, 0, None)
     assert rc == -1 and b"dtype" in L.msq_last_error()
-    rc = L.msq_layernorm_fwd(None, 0, None, None, None, None, None, 4, 6, 1e-5, None)
+    rc = L.msq_layernorm_fwd(None, 0, None, None, None, None, None, 4, 6, 1e-5, 0, 0, None)
     assert rc == -1
