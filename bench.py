@@ -1,0 +1,193 @@
+"""Headline benchmark: MIDI tokens/s of the Transformer training step
+(configs/transformer default: d=1024, 8 heads, 8 layers, T=2048 (+6 meta),
+V=17914) at B=32 per GPU, bf16 MFMA path, synthetic grammar-cycled tokens,
+random-init weights. One process per GPU (torchrun); weak scaling.
+
+Prints ONE JSON line on rank 0 (contract in the task statement)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import _pkgload  # noqa: E402
+
+_pkgload.load()
+from midiseq import ops  # noqa: E402
+from midiseq import _lib as L  # noqa: E402
+from midiseq.transformer import Transformer, TransformerConfig  # noqa: E402
+from midiseq.train_parallel import TrainStep, SyntheticMIDI, setup_distributed  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def flops_per_token(cfg, T):
+    """Algorithmic training FLOPs per MIDI token (SURVEY.md §8(d) cfg 2):
+    3 x forward; forward = L (24 S d^2 + 3 d S (S+1)) + 2 T d V per sequence."""
+    S, d = T + 6, cfg.n_embd
+    fwd = cfg.n_layer * (24 * S * d * d + 3 * d * S * (S + 1)) + 2 * T * d * cfg.vocab_size
+    return 3.0 * fwd / T
+
+
+class OpTimer:
+    """HIP events around one named op inside the timed region (on the stream
+    it is launched on)."""
+
+    def __init__(self, name):
+        self.name, self.pairs, self.on = name, [], False
+
+    def wrap(self, fn):
+        def inner(*a, **k):
+            if not self.on:
+                return fn(*a, **k)
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = fn(*a, **k)
+            e.record()
+            self.pairs.append((s, e))
+            return r
+        return inner
+
+    def avg_ms(self):
+        ts = [s.elapsed_time(e) for s, e in self.pairs]
+        return sum(ts) / max(1, len(ts)), len(ts)
+
+
+def cpu_baseline(seconds_budget=20.0):
+    """The CPU oracle (plain PyTorch fp32 restatement of the reference, the
+    'port') timed on this host: default model, B=1, T=2048, full train step
+    (forward, filtered CE, backward, Adam)."""
+    import numpy as np
+    from oracle import loss as oloss, transformer as otr
+    from oracle.fill import REAL, grammar_tokens
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    hp = dict(n_embd=1024, n_heads=8, n_layer=8, block_len=2048)
+    T = 2048
+    shapes = otr.param_shapes(hp["n_embd"], hp["n_heads"], hp["n_layer"], hp["block_len"], REAL.size, 568)
+    g = torch.Generator().manual_seed(0)
+    p = {k: (torch.randn(s, generator=g) * 0.02).requires_grad_(True) for k, s in shapes.items()}
+    opt = torch.optim.Adam(list(p.values()), lr=5e-5)
+    rng = np.random.default_rng(0)
+    w = grammar_tokens(rng, REAL, T + 1)[None]
+    src, trg = torch.from_numpy(w[:, :-1].copy()), torch.from_numpy(w[:, 1:].copy())
+    meta = torch.tensor([[519, 279, 202, 202, 202, 178]])
+    steps, t0 = 0, time.time()
+    while True:
+        logits = otr.forward(p, src, meta, hp["n_layer"], hp["n_heads"])
+        loss = oloss.loss(src, trg, logits, REAL)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        steps += 1
+        if time.time() - t0 > seconds_budget or steps >= 5:
+            break
+    dt = time.time() - t0
+    return {"value": round(steps * T / dt, 2), "unit": "MIDI tokens/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ fp32 train step (fwd+filtered CE+bwd+Adam), default model, B=1, T=2048, {steps} steps"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--seq", type=int, default=2048)
+    ap.add_argument("--layers", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank, local, world = setup_distributed()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    cfg = TransformerConfig(n_layer=args.layers, block_len=args.seq, precision="bf16", dropout=0.0)
+    model = Transformer(cfg).to(dev)
+    step = TrainStep(model)
+    data = iter(SyntheticMIDI(args.batch, args.seq, dev, rank))
+
+    # dominant kernel for the roofline: relative-attention backward pass A
+    # (flash_bwd_a) is timed through the op that launches it
+    timer = OpTimer("ffn1_gemm")
+    import midiseq.transformer as mt
+    orig_gemm = mt.ops.gemm
+
+    def gemm_tap(A, B, **kw):
+        if kw.get("epilogue") == L.EPI_BIAS_RELU:
+            return timer.wrap(orig_gemm)(A, B, **kw)
+        return orig_gemm(A, B, **kw)
+    mt.ops.gemm = gemm_tap
+
+    for _ in range(args.warmup):
+        step(*next(data))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer.on = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step(*next(data))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    timer.on = False
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    tokens = world * args.batch * args.seq * args.steps
+    value = tokens / el
+    ms_step = el / args.steps * 1e3
+    fpt = flops_per_token(cfg, args.seq)
+
+    ffn_ms, n_launch = timer.avg_ms()
+    M = args.batch * (args.seq + 6)
+    ffn_flops = 2.0 * M * (4 * cfg.n_embd) * cfg.n_embd
+    achieved = ffn_flops / (ffn_ms * 1e-3) / 1e12 if ffn_ms > 0 else 0.0
+    if rank == 0:
+        out = {
+            "metric": "MIDI tokens/sec (train, seq_len=2048)",
+            "value": round(value, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic grammar-cycled MIDI tokens, random-init weights",
+            "config": {"workload": "configs/transformer default (d=1024, h=8, L=8, V=17914) train step, "
+                                   "filtered CE + Adam, dropout=0",
+                       "model": "Transformer", "global_batch": args.batch * world, "seq_len": args.seq,
+                       "parallelism": f"dp{world}"},
+            "model_tflops": round(value * fpt / 1e12, 1),
+            "mfu": round(value * fpt / 1e12 / (PEAK_BF16_TFLOPS * world), 4),
+            "loss_last": round(float(loss.item()), 4),
+            "roofline": {"kernel": "gemm_bf16 FFN1 (NT, bias+ReLU epilogue) 65728x4096x1024",
+                         "bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "avg_launch_ms": round(ffn_ms, 4), "launches": n_launch},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -31,7 +31,7 @@ SIGNATURES = {
     "msq_colsum_workspace": (_sz, [_i64, _i64]),
     "msq_colsum": (_i, [_p, _i, _p, _i, _i64, _i64, _i64, _p, _p]),
     "msq_cast": (_i, [_p, _i, _p, _i, _i64, _p]),
-    "msq_adam_step": (_i, [_p, _p, _p, _p, _p, _i64, _f, _f, _f, _f, _i64, _p]),
+    "msq_adam_step": (_i, [_p, _p, _p, _p, _p, _i64, _f, _f, _f, _f, _i64, _f, _p]),
     "msq_relattn_fwd": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64, _p]),
     "msq_filtered_workspace": (_sz, [_i64, _i64, _i64]),
     "msq_filtered_colstats": (_i, [_p, _p, _i, _i64, _i64, _i64, _i64, _p, _p]),

@@ -328,9 +328,9 @@ extern "C" int msq_cast(void* dst, int dst_dtype, const void* src, int src_dtype
 //   p -= (lr / (1-b1^t)) * m / (sqrt(v) / sqrt(1-b2^t) + eps)
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, bf16* __restrict__ shadow, int64_t n, float b1, float b2, float eps,
-                            float step_size, float bc2_sqrt) {
+                            float step_size, float bc2_sqrt, float gscale) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float gi = g[i];
+        const float gi = g[i] * gscale;
         const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1-b1)
         const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
         m[i] = mi;
@@ -343,7 +343,7 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
 }
 
 extern "C" int msq_adam_step(float* p, const float* g, float* m, float* v, void* p_shadow, int64_t n, float lr,
-                             float beta1, float beta2, float eps, int64_t step, void* stream) {
+                             float beta1, float beta2, float eps, int64_t step, float grad_scale, void* stream) {
     MSQ_CHECK_ARG(n >= 0 && step >= 1, "msq_adam_step: bad args");
     if (n == 0) return MSQ_OK;
     const double bc1 = 1.0 - pow((double)beta1, (double)step);
@@ -352,7 +352,7 @@ extern "C" int msq_adam_step(float* p, const float* g, float* m, float* v, void*
     const float bc2s = (float)sqrt(bc2);
     const int grid = (int)std::min<int64_t>((n + 255) / 256, 16384);
     hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (bf16*)p_shadow, n,
-                       beta1, beta2, eps, step_size, bc2s);
+                       beta1, beta2, eps, step_size, bc2s, grad_scale);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }

@@ -105,6 +105,6 @@ def cast(dst, src):
     return dst
 
 
-def adam_step(p, g, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, shadow=None):
+def adam_step(p, g, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, shadow=None, grad_scale=1.0):
     call("msq_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow), p.numel(), float(lr), float(beta1),
-         float(beta2), float(eps), int(step), stream())
+         float(beta2), float(eps), int(step), float(grad_scale), stream())

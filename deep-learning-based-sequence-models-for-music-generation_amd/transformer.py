@@ -277,6 +277,8 @@ class TransformerEngine:
         ops.layernorm_bwd(gres, Bw["df"], A.x[cfg.n_layer], A.stf[0], A.stf[1], P["lnf_w"], G["lnf_w"], G["lnf_b"],
                           dx_copy=Bw["gb"], seg=(T, N_META))
         hook = getattr(self, "layer_grad_ready", None)
+        if hook is not None:
+            hook("head")
         for l in reversed(range(cfg.n_layer)):
             # FFN (model_transformer.py:92-105,120)
             ops.gemm(gb, A.h[l], ta=True, tb=True, out=G[f"{l}.w2"], epilogue=L.EPI_ACCUM)

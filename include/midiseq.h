@@ -93,9 +93,10 @@ int msq_colsum(float* out, int accumulate, const void* x, int dtype, int64_t row
 int msq_cast(void* dst, int dst_dtype, const void* src, int src_dtype, int64_t n, void* stream);
 
 /* ---- Adam (torch.optim.Adam, train_parallel.py:157,183; foreach formula)
+ * g is multiplied by grad_scale first (1/world after a SUM all-reduce).
  * Optional p_shadow receives the updated parameters in bf16.                 */
 int msq_adam_step(float* p, const float* g, float* m, float* v, void* p_shadow, int64_t n, float lr, float beta1,
-                  float beta2, float eps, int64_t step, void* stream);
+                  float beta2, float eps, int64_t step, float grad_scale, void* stream);
 
 
 /* ---- relative-position causal attention (HeadRelPos x n_heads +
