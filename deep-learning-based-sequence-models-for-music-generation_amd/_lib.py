@@ -41,6 +41,7 @@ SIGNATURES = {
                                 _p, _p]),
     "msq_filtered_logit_bwd": (_i, [_p, _i64, _p, _i64, _p, _i, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64,
                                     _i64, _p, _p, _p]),
+    "msq_decode_sample": (_i, [_p, _i64, _i64, _p, _i64, _i64, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "msq_relattn_bwd_workspace": (_sz, [_i, _i64, _i64, _i64]),
     "msq_relattn_bwd": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64,
                              _p, _p]),

@@ -543,18 +543,14 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     const unsigned nqb = (unsigned)((S + B_QB - 1) / B_QB);
     hipLaunchKernelGGL(flash_bwd_b_kernel, dim3(nqb, (unsigned)H, (unsigned)B), dim3(NT), 0, s, a, dqr, ldr, dq_ac,
                        H * HS);
-    // dq (bf16, q columns of dqkv) = dQR . R + dq_ac   (one GEMM per head)
-    for (int64_t h = 0; h < H; ++h) {
-        int rc = msq_gemm(MSQ_BF16, 0, 1, B * S, HS, S, dqr + h * B * S * ldr, ldr, 0,
-                          (const bf16*)a.R + h * a.S_max * HS, HS, 0, dqkv + h * HS, MSQ_BF16, ldd, 0, 1,
-                          MSQ_EPI_BIAS_RESID, nullptr, dq_ac + h * HS, MSQ_F32, H * HS, 0, s);
-        if (rc) return rc;
-        // dR[h][r] += sum_{b,i} dQR[b,i][r] q_{b,i}
-        rc = msq_gemm(MSQ_BF16, 1, 1, S, HS, B * S, dqr + h * B * S * ldr, ldr, 0, (const bf16*)a.qkv + h * HS,
-                      a.ldq, 0, dR + h * a.S_max * HS, MSQ_F32, HS, 0, 1, MSQ_EPI_ACCUM, nullptr, nullptr, MSQ_F32, 0,
-                      0, s);
-        if (rc) return rc;
-    }
+    // dq (bf16, q columns of dqkv) = dQR . R + dq_ac   (batched over heads)
+    int rc = msq_gemm(MSQ_BF16, 0, 1, B * S, HS, S, dqr, ldr, B * S * ldr, a.R, HS, a.S_max * HS, dqkv, MSQ_BF16,
+                      ldd, HS, H, MSQ_EPI_BIAS_RESID, nullptr, dq_ac, MSQ_F32, H * HS, HS, s);
+    if (rc) return rc;
+    // dR[h][r] += sum_{b,i} dQR[h][b,i][r] q_{b,i}   (batched over heads, split-K)
+    rc = msq_gemm(MSQ_BF16, 1, 1, S, HS, B * S, dqr, ldr, B * S * ldr, a.qkv, a.ldq, HS, dR, MSQ_F32, HS,
+                  a.S_max * HS, H, MSQ_EPI_ACCUM, nullptr, nullptr, MSQ_F32, 0, 0, s);
+    if (rc) return rc;
     hipLaunchKernelGGL(flash_bwd_meta_kernel, dim3(1, (unsigned)H, (unsigned)B), dim3(HS), 0, s, a, meta_ds, dqkv, ldd,
                        dR);
     return 0;

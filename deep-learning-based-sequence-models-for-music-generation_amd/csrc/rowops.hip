@@ -185,14 +185,24 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
 }
 
 // out[c] += sum_p part[p, c] for c < 2d (dgamma | dbeta)
-__global__ void ln_reduce_kernel(float* __restrict__ dg, float* __restrict__ db, const float* __restrict__ part,
-                                 int nparts, int d) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= 2 * d) return;
+// block = 64 columns x 4 waves; each wave sums every 4th partial row
+__global__ __launch_bounds__(256) void ln_reduce_kernel(float* __restrict__ dg, float* __restrict__ db,
+                                                        const float* __restrict__ part, int nparts, int d) {
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
     float s = 0.f;
-    for (int p = 0; p < nparts; ++p) s += part[(int64_t)p * 2 * d + c];
-    if (c < d) dg[c] += s;
-    else db[c - d] += s;
+    if (c < 2 * d) {
+#pragma unroll 8
+        for (int p = w; p < nparts; p += 4) s += part[(int64_t)p * 2 * d + c];
+    }
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && c < 2 * d) {
+        s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+        if (c < d) dg[c] += s;
+        else db[c - d] += s;
+    }
 }
 
 extern "C" size_t msq_layernorm_bwd_workspace(int64_t rows, int64_t d) {
@@ -247,7 +257,7 @@ extern "C" int msq_layernorm_bwd(float* dx_acc, void* dx_copy, int copy_dtype, f
         if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, s);
         else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, s);
     }
-    hipLaunchKernelGGL(ln_reduce_kernel, dim3((unsigned)((2 * d + 255) / 256)), dim3(256), 0, s, dgamma, dbeta, part,
+    hipLaunchKernelGGL(ln_reduce_kernel, dim3((unsigned)((2 * d + 63) / 64)), dim3(256), 0, s, dgamma, dbeta, part,
                        LN_BWD_BLOCKS, di);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;

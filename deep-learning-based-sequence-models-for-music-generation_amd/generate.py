@@ -1,0 +1,92 @@
+"""Drop-in for scripts/generate.py:14-95 (``generate``) on the MI355X engine.
+
+Exact sliding-window mode (the reference's semantics): every step runs the
+full forward over the last ``context_len`` tokens (the Transformer is
+length-anchored: its relative positions are measured from the window end, so
+a KV cache cannot reproduce this loop), takes the filtered
+logit of the last row (its log-softmax runs over the whole window's time
+axis), applies the repetition penalties, picks k with Python's ``random``
+exactly like the reference (same call order, so seeded runs draw the same
+k's) and samples on the device by inverse CDF on a uniform per row (replacing
+torch.multinomial). The history stays on the device; the only per-step
+device->host traffic is the B last tokens needed for the host-side k choice.
+"""
+import random as _random
+
+import torch
+
+from . import _lib as L
+from ._lib import ptr, call, stream, dt
+from .config import Grammar
+from .loss import grammar_table
+from .ops import workspace
+
+
+def choose_k(last_tokens, start, rng):
+    """generate.py:47-56 — consumes ``rng`` only for tempo/dyn/pitch tokens."""
+    ks = []
+    for t in last_tokens:
+        if t >= start["tempo"]:
+            ks.append(rng.choice([1, 1, 1, 2, 2]))
+        elif t >= start["time"] or t >= start["length"]:
+            ks.append(1)
+        elif t >= start["dyn"]:
+            ks.append(rng.choice([1, 3]))
+        else:
+            ks.append(rng.choice([1, 2]))
+    return ks
+
+
+@torch.no_grad()
+def generate(model, context_len, token_ids, meta_ids, num_tokens=1000, device="cuda", rng=None, uniforms=None,
+             grammar: Grammar = None, return_tensor=False):
+    """Returns a list of B token lists of length T0 + num_tokens (like the
+    reference). ``rng`` defaults to the global ``random`` module (as in the
+    reference); ``uniforms`` is an optional iterator of floats (one per row
+    per step, rows in order) for reproducible sampling, else a device
+    torch.Generator is used."""
+    grammar = grammar or Grammar()
+    rng = rng or _random
+    eng = model.engine
+    cfg = eng.cfg
+    V = cfg.vocab_size
+    start = grammar.disc.start_idx
+    dev = torch.device(device)
+    token_ids = token_ids.to(dev)
+    meta_ids = meta_ids.to(dev).contiguous()
+    B, T0 = token_ids.shape
+    ldh = T0 + num_tokens + 1
+    hist = torch.zeros(B, ldh, dtype=torch.int64, device=dev)
+    hist[:, :T0] = token_ids
+    out_tok = torch.empty(B, dtype=torch.int64, device=dev)
+    wtab = grammar_table(dev, grammar)
+    b = grammar.bounds
+    last_host = token_ids[:, -1].tolist()
+    gen = None
+    for step in range(num_tokens):
+        cur = T0 + step
+        W = min(cur, context_len)
+        window = hist[:, cur - W:cur].contiguous()
+        logits = eng.forward(window, meta_ids, save=False)
+        A = eng.acts(B, W, save=False)
+        ldz = (V + 3) // 4 * 4
+        z = torch.empty(B, 1, ldz, device=dev, dtype=torch.float32)
+        col_lse = torch.empty(B, V, device=dev, dtype=torch.float32)
+        ws = workspace(L.lib().msq_filtered_workspace(B, W, V), dev, "loss")
+        call("msq_filtered_logit", ptr(z), ldz, ptr(A.logits), dt(A.logits), cfg.v_pad, ptr(window), ptr(wtab),
+             b[0], b[1], b[2], b[3], B, W, V, W - 1, ptr(col_lse), ptr(ws), stream())
+        ks = choose_k(last_host, start, rng)
+        if uniforms is not None:
+            u = torch.tensor([next(uniforms) for _ in range(B)], dtype=torch.float32).to(dev)
+        else:
+            if gen is None:
+                gen = torch.Generator(device=dev)
+                gen.manual_seed(rng.getrandbits(63) if hasattr(rng, "getrandbits") else 1234)
+            u = torch.rand(B, device=dev, generator=gen)
+        kt = torch.tensor(ks, dtype=torch.int32).to(dev)
+        call("msq_decode_sample", ptr(hist), ldh, cur, ptr(z), ldz, B, V, ptr(kt), ptr(u), ptr(out_tok),
+             start["dyn"], start["length"], start["time"], start["tempo"], stream())
+        last_host = out_tok.tolist()  # the one device->host sync per step (host-side k choice)
+        del logits
+    seq = hist[:, :T0 + num_tokens]
+    return seq if return_tensor else seq.tolist()

@@ -143,14 +143,14 @@ def tril_mask(n, device="cpu"):
 class _Acts:
     """Activation + scratch buffers for one (B, T), reused across steps."""
 
-    def __init__(self, cfg, B, T, device, act):
+    def __init__(self, cfg, B, T, device, act, save=True):
         d, H = cfg.n_embd, cfg.n_heads
         S = T + N_META
         M = B * S
-        Lc = cfg.n_layer
+        Lc = cfg.n_layer if save else 1  # inference: one layer's buffers, reused
         f32 = torch.float32
         e = lambda *s, dt=act: torch.empty(*s, device=device, dtype=dt)  # noqa: E731
-        self.B, self.T, self.S, self.M = B, T, S, M
+        self.B, self.T, self.S, self.M, self.save = B, T, S, M, save
         self.x = e(Lc + 1, M, d, dt=f32)
         self.xm = e(Lc, M, d, dt=f32)
         self.a, self.c = e(Lc, M, d), e(Lc, M, d)
@@ -212,15 +212,17 @@ class TransformerEngine:
     def mark_shadow_fresh(self):
         self._shadow_version = self.flat._version
 
-    def acts(self, B, T):
-        key = (B, T)
+    def acts(self, B, T, save=True):
+        key = (B, T, save)
         if key not in self._acts:
-            self._acts.clear()
-            self._acts[key] = _Acts(self.cfg, B, T, self.device, self.act)
+            self._acts = {k: v for k, v in self._acts.items() if k[2] != save}
+            self._acts[key] = _Acts(self.cfg, B, T, self.device, self.act, save)
         return self._acts[key]
 
     # ------------------------------------------------------------- forward
-    def forward(self, idx, meta):
+    def forward(self, idx, meta, save=True):
+        """save=False (inference): one layer's activation buffers are reused
+        and nothing is kept for a backward pass."""
         cfg, P, W = self.cfg, self.P, self.W
         if not idx.is_cuda:
             raise RuntimeError("the MI355X engine runs on the GPU only (no CPU fallback)")
@@ -228,25 +230,28 @@ class TransformerEngine:
         B, T = idx.shape
         if T + N_META > cfg.s_max:
             raise ValueError(f"sequence of {T} tokens exceeds block_len {cfg.block_len}")
-        A = self.acts(B, T)
+        A = self.acts(B, T, save)
         A.gen += 1
         d, H, hs, S = cfg.n_embd, cfg.n_heads, cfg.head_size, T + N_META
         scale = d ** -0.5  # C**-0.5 with C = n_embd (model_transformer.py:65,77)
         idx = idx.contiguous()
         meta = meta.contiguous()
-        self._idx, self._meta = idx, meta
+        if save:
+            self._idx, self._meta = idx, meta
         ops.embed_fwd(A.x[0].view(B, S, d), P["tok_emb"], P["meta_emb"], idx, meta)
         for l in range(cfg.n_layer):
-            x = A.x[l]
-            ops.layernorm_fwd(x, P[f"{l}.ln1_w"], P[f"{l}.ln1_b"], out=A.a[l], mean=A.st1[l, 0], rstd=A.st1[l, 1])
-            ops.gemm(A.a[l], W[f"{l}.wqkv"], out=A.qkv[l])
-            relattn_fwd(A.qkv[l], W[f"{l}.R"], B, S, H, hs, scale, out=A.o[l], lse=A.lse[l])
-            ops.gemm(A.o[l], W[f"{l}.wproj"], out=A.xm[l], epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.bproj"], aux=x)
-            ops.layernorm_fwd(A.xm[l], P[f"{l}.ln2_w"], P[f"{l}.ln2_b"], out=A.c[l], mean=A.st2[l, 0],
-                              rstd=A.st2[l, 1])
-            ops.gemm(A.c[l], W[f"{l}.w1"], out=A.h[l], epilogue=L.EPI_BIAS_RELU, bias=P[f"{l}.b1"])
-            ops.gemm(A.h[l], W[f"{l}.w2"], out=A.x[l + 1], epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.b2"], aux=A.xm[l])
-        ops.layernorm_fwd(A.x[cfg.n_layer], P["lnf_w"], P["lnf_b"], out=A.f, mean=A.stf[0], rstd=A.stf[1],
+            k = l if save else 0
+            x, xo = (A.x[l], A.x[l + 1]) if save else (A.x[l % 2], A.x[(l + 1) % 2])
+            ops.layernorm_fwd(x, P[f"{l}.ln1_w"], P[f"{l}.ln1_b"], out=A.a[k], mean=A.st1[k, 0], rstd=A.st1[k, 1])
+            ops.gemm(A.a[k], W[f"{l}.wqkv"], out=A.qkv[k])
+            relattn_fwd(A.qkv[k], W[f"{l}.R"], B, S, H, hs, scale, out=A.o[k], lse=A.lse[k])
+            ops.gemm(A.o[k], W[f"{l}.wproj"], out=A.xm[k], epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.bproj"], aux=x)
+            ops.layernorm_fwd(A.xm[k], P[f"{l}.ln2_w"], P[f"{l}.ln2_b"], out=A.c[k], mean=A.st2[k, 0],
+                              rstd=A.st2[k, 1])
+            ops.gemm(A.c[k], W[f"{l}.w1"], out=A.h[k], epilogue=L.EPI_BIAS_RELU, bias=P[f"{l}.b1"])
+            ops.gemm(A.h[k], W[f"{l}.w2"], out=xo, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.b2"], aux=A.xm[k])
+        x_last = A.x[cfg.n_layer] if save else A.x[cfg.n_layer % 2]
+        ops.layernorm_fwd(x_last, P["lnf_w"], P["lnf_b"], out=A.f, mean=A.stf[0], rstd=A.stf[1],
                           seg=(T, N_META))
         V = cfg.vocab_size
         ops.gemm(A.f, W["lm_w"][:V], out=A.logits[:, :V], epilogue=L.EPI_BIAS, bias=P["lm_b"][:V])
@@ -401,6 +406,8 @@ class Transformer(nn.Module):
         return out
 
     def forward(self, idx, metadata_idx, targets=None):
+        if not (torch.is_grad_enabled() and self.flat.requires_grad):
+            return self.engine.forward(idx, metadata_idx, save=False)
         return _TransformerFn.apply(self.flat, idx, metadata_idx, self.engine)
 
     def get_name(self):

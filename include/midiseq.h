@@ -141,6 +141,17 @@ int msq_filtered_logit_bwd(void* dlogits, int64_t ldd, const float* dz, int64_t 
                            int64_t b3, int64_t B, int64_t T, int64_t V, const float* col_lse, void* workspace,
                            void* stream);
 
+/* ---- autoregressive decode step (scripts/generate.py:33-89) ---------------
+ * For every row b: recent window of hist[b, :cur_len] (time-shift sum >= 1024),
+ * repetition penalties on z_last[b] (in place), top-k (k = ks[b] in 1..3,
+ * chosen by the host with Python's random), p = v / sum v, inverse-CDF pick
+ * with uniforms[b]; the token is written to hist[b, cur_len] and out_tok[b].
+ * hist: int64 [B, ld_hist]; z_last: fp32 [B, ld_z] (filtered logits of the
+ * last window row, msq_filtered_logit with t_begin = T-1).                 */
+int msq_decode_sample(int64_t* hist, int64_t ld_hist, int64_t cur_len, float* z_last, int64_t ld_z, int64_t B,
+                      int64_t V, const int* ks, const float* uniforms, int64_t* out_tok, int64_t dyn_start,
+                      int64_t length_start, int64_t time_start, int64_t tempo_start, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
