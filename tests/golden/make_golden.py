@@ -11,6 +11,7 @@ file path with the unrelated imports stubbed, and records their outputs on
 deterministic inputs into tests/golden/*.npz. Only data is written; nothing
 from the reference is copied into the repository.
 """
+import importlib.machinery
 import importlib.util
 import json
 import os
@@ -65,7 +66,10 @@ class RefShim:
         sys.modules["configs"] = configs
         sys.modules["configs.common"] = cc
         for stub in ("models", "processing", "mamba_ssm", "pretty_midi"):
+            if stub == "mamba_ssm" and hasattr(sys.modules.get(stub), "Mamba2"):
+                continue
             sys.modules[stub] = types.ModuleType(stub)
+            sys.modules[stub].__spec__ = importlib.machinery.ModuleSpec(stub, None)
         self.cc = cc
         self.mt = self._load("ref_model_transformer", "models/transformer/model_transformer.py")
         orig_to = torch.Tensor.to
@@ -246,6 +250,80 @@ def g4(ref_path):
     np.savez_compressed(OUT / "g4_generate.npz", **out)
 
 
+def _hf_mamba2_stub():
+    """mamba_ssm.Mamba2 stand-in: HF transformers' pure-torch Mamba2Mixer with
+    mamba_ssm's defaults (headdim 64, ngroups 1, chunk 256, no bias, conv
+    bias, rmsnorm eps 1e-5, norm_before_gate=False, dt_limit (0, inf))."""
+    from transformers.models.mamba2.configuration_mamba2 import Mamba2Config
+    from transformers.models.mamba2.modeling_mamba2 import Mamba2Mixer
+
+    class Mamba2(Mamba2Mixer):
+        def __init__(self, d_model, d_state=64, d_conv=4, expand=2, layer_idx=0, headdim=64, ngroups=1, **kw):
+            cfg = Mamba2Config(hidden_size=d_model, state_size=d_state, conv_kernel=d_conv, expand=expand,
+                               head_dim=headdim, num_heads=expand * d_model // headdim, n_groups=ngroups,
+                               use_bias=False, use_conv_bias=True, chunk_size=256, layer_norm_epsilon=1e-5,
+                               time_step_limit=(0.0, float("inf")), num_hidden_layers=max(1, layer_idx + 1))
+            super().__init__(cfg, layer_idx)
+
+        def forward(self, x):
+            return super().forward(x)
+
+    m = types.ModuleType("mamba_ssm")
+    m.Mamba2 = Mamba2
+    for name in ("mamba_ssm.utils", "mamba_ssm.utils.generation"):
+        sys.modules[name] = types.ModuleType(name)
+    sys.modules["mamba_ssm.utils.generation"].InferenceParams = object
+    sys.modules["mamba_ssm"] = m
+
+
+def g5(ref_path):
+    """Reference Mamba (models/mamba/mamba.py) fwd/bwd with HF-backed Mamba2."""
+    from oracle import mamba2 as om
+    os.environ.setdefault("HF_HUB_OFFLINE", "1")
+    out = {}
+    vocab = Vocab()
+    sh = RefShim(ref_path, vocab, 568)
+    _hf_mamba2_stub()
+    orig_to = torch.nn.Module.to
+
+    def to_cpu(mod, *a, **k):
+        a = tuple("cpu" if x == "cuda" else x for x in a)
+        return orig_to(mod, *a, **k)
+    torch.nn.Module.to = to_cpu
+    try:
+        mm = sh._load("ref_mamba", "models/mamba/mamba.py")
+        full = mm.Mamba()  # defaults d_model=1024, n_layers=10
+        out["default_param_count"] = np.array(sum(p.numel() for p in full.parameters()), dtype=np.int64)
+        del full
+        d_model, n_layers, T, B = 128, 2, 300, 2
+        m = mm.Mamba(d_model=d_model, n_layers=n_layers)
+    finally:
+        torch.nn.Module.to = orig_to
+    shapes = om.param_shapes(d_model, n_layers, vocab.size, 568)
+    sd = m.state_dict()
+    assert set(sd) == set(shapes), (set(sd) ^ set(shapes))
+    for k, s in shapes.items():
+        assert tuple(sd[k].shape) == tuple(s), (k, sd[k].shape, s)
+        sd[k] = torch.from_numpy(fill_param(k, s))
+    m.load_state_dict(sd)
+    m.train()
+    src, trg, meta = make_inputs(vocab, B, T, 568, 31)
+    logits = m(torch.from_numpy(src), torch.from_numpy(meta))
+    z = sh.train.filtered_logit(torch.from_numpy(src), logits)
+    loss = torch.nn.CrossEntropyLoss()(z.reshape(-1, vocab.size), torch.from_numpy(trg).view(-1))
+    loss.backward()
+    out["src"], out["trg"], out["meta"] = src, trg, meta
+    out["loss"] = np.array(loss.item(), dtype=np.float64)
+    P = projection(vocab.size)
+    out["logits_proj"] = (logits.detach() @ P).numpy()
+    out["logits_rows"] = logits.detach()[:, [0, 149, T - 1], :].numpy()
+    for k, p in m.named_parameters():
+        gf = p.grad.reshape(-1).double()
+        out[f"gsum:{k}"] = np.array([gf.sum().item(), gf.abs().sum().item(), (gf * gf).sum().item()])
+        out[f"gpick:{k}"] = p.grad.reshape(-1)[:: max(1, gf.numel() // 64)][:64].numpy()
+    np.savez_compressed(OUT / "g5_mamba.npz", **out)
+
+
 if __name__ == "__main__":
     ref = Path(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")
     torch.manual_seed(0)
@@ -257,4 +335,6 @@ if __name__ == "__main__":
         g3(ref)
     if which in ("all", "g4"):
         g4(ref)
+    if which in ("all", "g5"):
+        g5(ref)
     print("golden fixtures written to", OUT)
