@@ -42,6 +42,14 @@ SIGNATURES = {
     "msq_filtered_logit_bwd": (_i, [_p, _i64, _p, _i64, _p, _i, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64,
                                     _i64, _p, _p, _p]),
     "msq_decode_sample": (_i, [_p, _i64, _i64, _p, _i64, _i64, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "msq_mamba_states_size": (_sz, [_i64, _i64, _i64]),
+    "msq_mamba_conv_fwd": (_i, [_p, _i64, _p, _i64, _i, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "msq_mamba_ssd_fwd": (_i, [_p, _i64, _p, _p, _i64, _p, _i64, _i, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "msq_mamba_gnorm_fwd": (_i, [_p, _i64, _p, _p, _i64, _p, _i64, _i, _p, _i64, _i64, _f, _p]),
+    "msq_mamba_gnorm_bwd": (_i, [_p, _p, _p, _i64, _p, _i64, _i, _p, _p, _p, _i64, _p, _i64, _i64, _p]),
+    "msq_mamba_ssd_bwd": (_i, [_p, _i64, _p, _p, _i64, _p, _p, _i64, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _i64,
+                               _i64, _i64, _i64, _p]),
+    "msq_mamba_conv_bwd": (_i, [_p, _p, _i64, _p, _i64, _i, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "msq_relattn_bwd_workspace": (_sz, [_i, _i64, _i64, _i64]),
     "msq_relattn_bwd": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64,
                              _p, _p]),

@@ -1,0 +1,385 @@
+"""Drop-in for models/mamba/mamba.py:8-35 (``Mamba(d_model=1024, n_layers=10)``)
+over the HIP kernels: 10 stacked Mamba2 mixers with NO residual and no
+per-layer norm, a final LayerNorm and the output head, sliced [:, 6:].
+
+Same engine structure as the Transformer: one flat fp32 parameter buffer
+(reference state_dict keys map onto views of it), a bf16 shadow for the MFMA
+GEMMs (in_proj 1024->4256, out_proj 2048->1024, the 17 914-way head), the SSD
+scan in fp32 from chunk-entry states kept in HBM for the backward."""
+import math
+from collections import OrderedDict
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from . import ops
+from ._lib import ptr, call, stream
+from .config import N_META, VOCAB_SIZE, METADATA_VOCAB_SIZE
+from .transformer import TransformerEngine, _align, _select
+
+D_STATE, D_CONV, HEADDIM = 64, 4, 64
+
+
+@dataclass
+class MambaConfig:
+    d_model: int = 1024
+    n_layers: int = 10
+    vocab_size: int = VOCAB_SIZE
+    metadata_vocab_size: int = METADATA_VOCAB_SIZE
+    precision: str = "bf16"
+    norm_eps: float = 1e-5  # RMSNormGated eps of mamba_ssm.Mamba2
+
+    @property
+    def d_inner(self):
+        return 2 * self.d_model
+
+    @property
+    def nheads(self):
+        return self.d_inner // HEADDIM
+
+    @property
+    def conv_dim(self):
+        return self.d_inner + 2 * D_STATE
+
+    @property
+    def d_in_proj(self):
+        return 2 * self.d_inner + 2 * D_STATE + self.nheads
+
+    @property
+    def v_pad(self):
+        return (self.vocab_size + 7) // 8 * 8
+
+
+class MambaLayout:
+    def __init__(self, cfg: MambaConfig):
+        d, di, H, cd = cfg.d_model, cfg.d_inner, cfg.nheads, cfg.conv_dim
+        entries = [("tok_emb", (cfg.vocab_size, d)), ("meta_emb", (cfg.metadata_vocab_size, d))]
+        for l in range(cfg.n_layers):
+            entries += [(f"{l}.in_w", (cfg.d_in_proj, d)), (f"{l}.conv_w", (cd, D_CONV)), (f"{l}.conv_b", (cd,)),
+                        (f"{l}.dt_bias", (H,)), (f"{l}.A_log", (H,)), (f"{l}.D", (H,)), (f"{l}.norm_w", (di,)),
+                        (f"{l}.out_w", (d, di))]
+        entries += [("lnf_w", (d,)), ("lnf_b", (d,)), ("lm_w", (cfg.v_pad, d)), ("lm_b", (cfg.v_pad,))]
+        self.offsets, off = {}, 0
+        for name, shape in entries:
+            self.offsets[name] = (off, shape)
+            off += _align(math.prod(shape))
+        self.numel = off
+
+    def views(self, flat):
+        return {n: flat[o:o + math.prod(s)].view(s) for n, (o, s) in self.offsets.items()}
+
+    def layer_range(self, l):
+        s = self.offsets[f"{l}.in_w"][0]
+        o, sh = self.offsets[f"{l}.out_w"]
+        return s, o + _align(math.prod(sh))
+
+
+def reference_keys(cfg: MambaConfig):
+    m = OrderedDict()
+    m["token_embedding.weight"] = ("tok_emb", None)
+    m["metadata_embedding.weight"] = ("meta_emb", None)
+    m["output_layer.weight"] = ("lm_w", ("rows", 0, cfg.vocab_size))
+    m["output_layer.bias"] = ("lm_b", ("rows", 0, cfg.vocab_size))
+    for l in range(cfg.n_layers):
+        p = f"layers.{l}."
+        m[p + "dt_bias"] = (f"{l}.dt_bias", None)
+        m[p + "A_log"] = (f"{l}.A_log", None)
+        m[p + "D"] = (f"{l}.D", None)
+        m[p + "in_proj.weight"] = (f"{l}.in_w", None)
+        m[p + "conv1d.weight"] = (f"{l}.conv_w", ("conv",))
+        m[p + "conv1d.bias"] = (f"{l}.conv_b", None)
+        m[p + "norm.weight"] = (f"{l}.norm_w", None)
+        m[p + "out_proj.weight"] = (f"{l}.out_w", None)
+    m["norm.weight"] = ("lnf_w", None)
+    m["norm.bias"] = ("lnf_b", None)
+    return m
+
+
+def _sel(t, sel):
+    if sel is not None and sel[0] == "conv":
+        return t.view(t.shape[0], 1, t.shape[1])
+    return _select(t, sel)
+
+
+class _MActs:
+    def __init__(self, cfg, B, T, device, act, save):
+        L_ = T + N_META
+        M = B * L_
+        n = cfg.n_layers if save else 1
+        f32 = torch.float32
+        e = lambda *s, dt=act: torch.empty(*s, device=device, dtype=dt)  # noqa: E731
+        self.B, self.T, self.L, self.M, self.save = B, T, L_, M, save
+        self.x = e(2, M, cfg.d_model, dt=f32)                # fp32 layer output ping-pong
+        self.xa = e(n + 1 if save else 2, M, cfg.d_model)    # act copies (in_proj inputs)
+        self.zx = e(n, M, cfg.d_in_proj)
+        self.xc = e(n, M, cfg.conv_dim)
+        self.y = e(n, M, cfg.d_inner, dt=f32)
+        self.yn = e(n, M, cfg.d_inner)
+        self.rstd = e(n, M, dt=f32)
+        nst = L.lib().msq_mamba_states_size(B, L_, cfg.nheads) // 4
+        self.states = e(n, nst, dt=f32)
+        self.xlast = e(M, cfg.d_model, dt=f32)
+        self.f = e(B * T, cfg.d_model)
+        self.stf = e(2, B * T, dt=f32)
+        self.logits = e(B * T, cfg.v_pad)
+        self.gen = 0
+        self._bwd = None
+
+    def bwd(self, cfg, device, act):
+        if self._bwd is None:
+            M = self.M
+            f32 = torch.float32
+            e = lambda *s, dt=act: torch.empty(*s, device=device, dtype=dt)  # noqa: E731
+            self._bwd = dict(gx=e(M, cfg.d_model, dt=f32), gxb=e(M, cfg.d_model), dyn=e(M, cfg.d_inner, dt=f32),
+                             dy=e(M, cfg.d_inner, dt=f32), dzx=e(M, cfg.d_in_proj), dxc=e(M, cfg.conv_dim, dt=f32),
+                             df=e(self.B * self.T, cfg.d_model), dlogits=e(self.B * self.T, cfg.v_pad))
+        return self._bwd
+
+
+class MambaEngine:
+    def __init__(self, cfg: MambaConfig, flat):
+        self.cfg = cfg
+        self.layout = MambaLayout(cfg)
+        self.act = torch.bfloat16 if cfg.precision == "bf16" else torch.float32
+        self.flat = flat
+        self.device = flat.device
+        self.P = self.layout.views(flat.data)
+        if self.act == torch.bfloat16:
+            self.shadow = torch.empty(self.layout.numel, device=flat.device, dtype=torch.bfloat16)
+            self.W = self.layout.views(self.shadow)
+        else:
+            self.shadow, self.W = None, self.P
+        self._shadow_version = None
+        self._acts = {}
+        self.layer_grad_ready = None
+
+    refresh_shadow = TransformerEngine.refresh_shadow
+    mark_shadow_fresh = TransformerEngine.mark_shadow_fresh
+
+    def acts(self, B, T, save=True):
+        key = (B, T, save)
+        if key not in self._acts:
+            self._acts = {k: v for k, v in self._acts.items() if k[2] != save}
+            self._acts[key] = _MActs(self.cfg, B, T, self.device, self.act, save)
+        return self._acts[key]
+
+    def dlogits_buffer(self, B, T):
+        return self.acts(B, T).bwd(self.cfg, self.device, self.act)["dlogits"]
+
+    def bucket_ranges(self):
+        lay, off = self.layout, self.layout.offsets
+        r = {"head": (off["lnf_w"][0], lay.numel), -1: (0, off["0.in_w"][0])}
+        for l in range(self.cfg.n_layers):
+            r[l] = lay.layer_range(l)
+        return r
+
+    def _dims(self, A):
+        c = self.cfg
+        return A.B, A.L, c.d_inner, c.nheads
+
+    def forward(self, idx, meta, save=True):
+        cfg, P, W = self.cfg, self.P, self.W
+        if not idx.is_cuda:
+            raise RuntimeError("the MI355X engine runs on the GPU only (no CPU fallback)")
+        self.refresh_shadow()
+        B, T = idx.shape
+        A = self.acts(B, T, save)
+        A.gen += 1
+        idx, meta = idx.contiguous(), meta.contiguous()
+        if save:
+            self._idx, self._meta = idx, meta
+        d, M = cfg.d_model, A.M
+        Bb, Ll, di, H = self._dims(A)
+        dtc = L.BF16 if self.act == torch.bfloat16 else L.F32
+        s = stream()
+        x = A.x[0]
+        ops.embed_fwd(x.view(B, A.L, d), P["tok_emb"], P["meta_emb"], idx, meta)
+        xa = A.xa[0]
+        ops.cast(xa, x)
+        for l in range(cfg.n_layers):
+            k = l if save else 0
+            zx, xc, y, yn = A.zx[k], A.xc[k], A.y[k], A.yn[k]
+            ops.gemm(xa, W[f"{l}.in_w"], out=zx)
+            call("msq_mamba_conv_fwd", ptr(xc), cfg.conv_dim, ptr(zx), cfg.d_in_proj, dtc, ptr(P[f"{l}.conv_w"]),
+                 ptr(P[f"{l}.conv_b"]), Bb, Ll, di, H, s)
+            call("msq_mamba_ssd_fwd", ptr(y), di, ptr(A.states[k]), ptr(xc), cfg.conv_dim, ptr(zx), cfg.d_in_proj, dtc,
+                 ptr(P[f"{l}.dt_bias"]), ptr(P[f"{l}.A_log"]), ptr(P[f"{l}.D"]), Bb, Ll, di, H, s)
+            call("msq_mamba_gnorm_fwd", ptr(yn), di, ptr(A.rstd[k]), ptr(y), di, ptr(zx), cfg.d_in_proj, dtc,
+                 ptr(P[f"{l}.norm_w"]), M, di, float(cfg.norm_eps), s)
+            xo = A.xlast if l == cfg.n_layers - 1 else A.x[(l + 1) % 2]
+            ops.gemm(yn, W[f"{l}.out_w"], out=xo)
+            if l < cfg.n_layers - 1:
+                xa = A.xa[l + 1] if save else A.xa[(l + 1) % 2]
+                ops.cast(xa, xo)
+        ops.layernorm_fwd(A.xlast, P["lnf_w"], P["lnf_b"], out=A.f, mean=A.stf[0], rstd=A.stf[1], seg=(T, N_META))
+        V = cfg.vocab_size
+        ops.gemm(A.f, W["lm_w"][:V], out=A.logits[:, :V], epilogue=L.EPI_BIAS, bias=P["lm_b"][:V])
+        return A.logits.view(B, T, cfg.v_pad)[:, :, :V]
+
+    def backward(self, dlogits, grads):
+        cfg, P, W = self.cfg, self.P, self.W
+        G = self.layout.views(grads)
+        idx, meta = self._idx, self._meta
+        B, T = idx.shape
+        A = self.acts(B, T)
+        Bw = A.bwd(cfg, self.device, self.act)
+        Bb, Ll, di, H = self._dims(A)
+        M, V = A.M, cfg.vocab_size
+        dtc = L.BF16 if self.act == torch.bfloat16 else L.F32
+        s = stream()
+        hook = self.layer_grad_ready
+        dl = dlogits[:, :V]
+        ops.gemm(dl, A.f, ta=True, tb=True, out=G["lm_w"][:V], epilogue=L.EPI_ACCUM)
+        ops.colsum(dl, G["lm_b"][:V], accumulate=True)
+        ops.gemm(dl, W["lm_w"][:V], tb=True, out=Bw["df"])
+        gx, gxb = Bw["gx"], Bw["gxb"]
+        gx.zero_()
+        ops.layernorm_bwd(gx, Bw["df"], A.xlast, A.stf[0], A.stf[1], P["lnf_w"], G["lnf_w"], G["lnf_b"],
+                          seg=(T, N_META))
+        if hook is not None:
+            hook("head")
+        for l in reversed(range(cfg.n_layers)):
+            gin = gxb
+            if self.act == torch.bfloat16:
+                ops.cast(gxb, gx)
+            else:
+                gin = gx
+            ops.gemm(gin, A.yn[l], ta=True, tb=True, out=G[f"{l}.out_w"], epilogue=L.EPI_ACCUM)
+            ops.gemm(gin, W[f"{l}.out_w"], tb=True, out=Bw["dyn"])
+            call("msq_mamba_gnorm_bwd", ptr(Bw["dy"]), ptr(Bw["dzx"]), ptr(A.y[l]), di, ptr(A.zx[l]), cfg.d_in_proj,
+                 dtc, ptr(P[f"{l}.norm_w"]), ptr(A.rstd[l]), ptr(Bw["dyn"]), di, ptr(G[f"{l}.norm_w"]), M, di, s)
+            call("msq_mamba_ssd_bwd", ptr(Bw["dxc"]), cfg.conv_dim, ptr(Bw["dzx"]), ptr(Bw["dy"]), di,
+                 ptr(A.states[l]), ptr(A.xc[l]), cfg.conv_dim, ptr(A.zx[l]), cfg.d_in_proj, dtc,
+                 ptr(P[f"{l}.dt_bias"]), ptr(P[f"{l}.A_log"]), ptr(P[f"{l}.D"]), ptr(G[f"{l}.A_log"]), ptr(G[f"{l}.D"]),
+                 ptr(G[f"{l}.dt_bias"]), Bb, Ll, di, H, s)
+            call("msq_mamba_conv_bwd", ptr(Bw["dzx"]), ptr(Bw["dxc"]), cfg.conv_dim, ptr(A.zx[l]), cfg.d_in_proj, dtc,
+                 ptr(P[f"{l}.conv_w"]), ptr(P[f"{l}.conv_b"]), ptr(G[f"{l}.conv_w"]), ptr(G[f"{l}.conv_b"]), Bb, Ll,
+                 di, H, s)
+            ops.gemm(Bw["dzx"], A.xa[l], ta=True, tb=True, out=G[f"{l}.in_w"], epilogue=L.EPI_ACCUM)
+            ops.gemm(Bw["dzx"], W[f"{l}.in_w"], tb=True, out=gx)
+            if hook is not None:
+                hook(l)
+        ops.embed_bwd(G["tok_emb"], G["meta_emb"], gx, idx, meta)
+        if hook is not None:
+            hook(-1)
+
+
+class _MambaFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, flat, idx, meta, engine):
+        out = engine.forward(idx, meta)
+        ctx.engine, ctx.gen, ctx.shape = engine, engine.acts(*idx.shape).gen, tuple(idx.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        eng = ctx.engine
+        B, T = ctx.shape
+        if eng.acts(B, T).gen != ctx.gen:
+            raise RuntimeError("activations were overwritten by a later forward")
+        cfg = eng.cfg
+        buf = eng.dlogits_buffer(B, T)
+        buf.view(B, T, cfg.v_pad)[:, :, :cfg.vocab_size].copy_(dlogits)
+        grads = torch.zeros_like(eng.flat.data)
+        eng.backward(buf, grads)
+        return grads, None, None, None
+
+
+class Mamba(nn.Module):
+    """Mamba(d_model=1024, n_layers=10) drop-in; vocab sizes default to the
+    reference's cc globals (mamba.py:12-14)."""
+
+    def __init__(self, d_model=1024, n_layers=10, vocab_size=VOCAB_SIZE, metadata_vocab_size=METADATA_VOCAB_SIZE,
+                 precision="bf16", device=None):
+        super().__init__()
+        self.cfg = MambaConfig(d_model=d_model, n_layers=n_layers, vocab_size=vocab_size,
+                               metadata_vocab_size=metadata_vocab_size, precision=precision)
+        lay = MambaLayout(self.cfg)
+        self.flat = nn.Parameter(torch.zeros(lay.numel, device=device))
+        self._engine = None
+        self.reset_parameters()
+
+    @property
+    def layout(self):
+        return MambaLayout(self.cfg)
+
+    def reset_parameters(self, seed=0):
+        """mamba_ssm-like init: A_log = log(1..H), D = 1, dt_bias = inv_softplus(dt ~ logU[1e-3, 1e-1])."""
+        g = torch.Generator().manual_seed(seed)
+        V = self.layout.views(self.flat.data)
+        c = self.cfg
+        with torch.no_grad():
+            for name, (_, shape) in self.layout.offsets.items():
+                t, leaf = V[name], name.split(".")[-1]
+                if name in ("tok_emb", "meta_emb"):
+                    t.copy_(torch.randn(shape, generator=g))
+                elif leaf in ("in_w", "out_w", "lm_w"):
+                    b = 1.0 / math.sqrt(shape[1])
+                    t.copy_(torch.empty(shape).uniform_(-b, b, generator=g))
+                elif leaf == "conv_w":
+                    b = 1.0 / math.sqrt(D_CONV)
+                    t.copy_(torch.empty(shape).uniform_(-b, b, generator=g))
+                elif leaf in ("conv_b", "lm_b"):
+                    b = 1.0 / math.sqrt(D_CONV if leaf == "conv_b" else c.d_model)
+                    t.copy_(torch.empty(shape).uniform_(-b, b, generator=g))
+                elif leaf == "A_log":
+                    t.copy_(torch.log(torch.arange(1, shape[0] + 1, dtype=torch.float32)))
+                elif leaf == "D" or leaf in ("norm_w", "lnf_w"):
+                    t.fill_(1.0)
+                elif leaf == "dt_bias":
+                    dt = torch.exp(torch.rand(shape, generator=g) * (math.log(0.1) - math.log(1e-3)) + math.log(1e-3))
+                    dt = dt.clamp(min=1e-4)
+                    t.copy_(dt + torch.log(-torch.expm1(-dt)))
+                else:
+                    t.zero_()
+            if c.v_pad > c.vocab_size:
+                V["lm_w"][c.vocab_size:].zero_()
+                V["lm_b"][c.vocab_size:].zero_()
+        self._engine = None
+
+    @property
+    def engine(self):
+        if self._engine is None or self._engine.flat is not self.flat or self._engine.device != self.flat.device:
+            self._engine = MambaEngine(self.cfg, self.flat)
+        return self._engine
+
+    def _apply(self, fn, *a, **k):
+        out = super()._apply(fn, *a, **k)
+        self._engine = None
+        return out
+
+    def forward(self, tokens, meta):
+        if not (torch.is_grad_enabled() and self.flat.requires_grad):
+            return self.engine.forward(tokens, meta, save=False)
+        return _MambaFn.apply(self.flat, tokens, meta, self.engine)
+
+    def get_name(self):
+        return "Mamba"
+
+    def state_dict(self, *args, destination=None, prefix="", keep_vars=False):
+        V = self.layout.views(self.flat if keep_vars else self.flat.detach())
+        out = OrderedDict() if destination is None else destination
+        for k, (n, sel) in reference_keys(self.cfg).items():
+            out[prefix + k] = _sel(V[n], sel)
+        return out
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        V = self.layout.views(self.flat.data)
+        keys = reference_keys(self.cfg)
+        missing = [k for k in keys if k not in state_dict]
+        unexpected = [k for k in state_dict if k not in keys]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"state_dict mismatch: missing {missing[:5]}, unexpected {unexpected[:5]}")
+        with torch.no_grad():
+            for k, (n, sel) in keys.items():
+                if k in state_dict:
+                    _sel(V[n], sel).copy_(state_dict[k])
+        if self._engine is not None:
+            self._engine.refresh_shadow(force=True)
+        return torch.nn.modules.module._IncompatibleKeys(missing, unexpected)
+
+    def grad_dict(self):
+        V = self.layout.views(self.flat.grad)
+        return OrderedDict((k, _sel(V[n], s)) for k, (n, s) in reference_keys(self.cfg).items())

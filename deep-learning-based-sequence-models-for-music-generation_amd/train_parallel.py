@@ -16,16 +16,16 @@ import torch.distributed as dist
 
 from . import ops
 from .config import LEARNING_RATE, Grammar
-from .ddp import GradBuckets, transformer_buckets
+from .ddp import GradBuckets
 from .loss import ce_forward_backward
 from .transformer import Transformer, TransformerConfig
 
 
 class TrainStep:
     """One optimisation step of train_parallel.py:173-183 (zero_grad, backward
-    with DDP all-reduce, Adam(lr=5e-5)) for a Transformer drop-in."""
+    with DDP all-reduce, Adam(lr=5e-5)) for a Transformer or Mamba drop-in."""
 
-    def __init__(self, model: Transformer, lr=LEARNING_RATE, betas=(0.9, 0.999), eps=1e-8, grammar=None,
+    def __init__(self, model, lr=LEARNING_RATE, betas=(0.9, 0.999), eps=1e-8, grammar=None,
                  group=None):
         self.model = model
         self.eng = model.engine
@@ -38,7 +38,7 @@ class TrainStep:
         self.step_no = 0
         self.buckets = None
         if dist.is_initialized() and dist.get_world_size(group) > 1:
-            self.buckets = GradBuckets(self.grads, transformer_buckets(self.eng.layout), group)
+            self.buckets = GradBuckets(self.grads, self.eng.bucket_ranges(), group)
             self.buckets.broadcast_params(flat)
             self.eng.refresh_shadow(force=True)
             self.eng.layer_grad_ready = self.buckets.ready
@@ -107,11 +107,13 @@ def setup_distributed():
 
 
 def new_model(type_name="transformer", precision="bf16", **kw):
-    """train_parallel.py:56-65 (transformer only in this build)."""
+    """train_parallel.py:56-65: "transformer" | "mamba" (xlstm is out of scope)."""
+    if type_name == "mamba":
+        from .mamba import Mamba
+        return Mamba(precision=precision, **kw)
     if type_name != "transformer":
-        raise NotImplementedError(f"model type {type_name!r} is not built on the MI355X path yet")
-    cfg = TransformerConfig(precision=precision, **kw)
-    return Transformer(cfg)
+        raise NotImplementedError(f"model type {type_name!r} is not on the MI355X path (see DESIGN.md)")
+    return Transformer(TransformerConfig(precision=precision, **kw))
 
 
 def train(model, type_name="transformer", data=None, steps=100, log_every=10, lr=LEARNING_RATE):

@@ -310,6 +310,10 @@ class TransformerEngine:
         if hook is not None:
             hook(-1)
 
+    def bucket_ranges(self):
+        from .ddp import transformer_buckets
+        return transformer_buckets(self.layout)
+
     def dlogits_buffer(self, B, T):
         A = self.acts(B, T)
         return A.bwd(self.cfg, self.device, self.act)["dlogits"]

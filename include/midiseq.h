@@ -152,6 +152,38 @@ int msq_decode_sample(int64_t* hist, int64_t ld_hist, int64_t cur_len, float* z_
                       int64_t V, const int* ks, const float* uniforms, int64_t* out_tok, int64_t dyn_start,
                       int64_t length_start, int64_t time_start, int64_t tempo_start, void* stream);
 
+/* ---- Mamba2 mixer (mamba_ssm.Mamba2 via models/mamba/mamba.py:16-24;
+ * d_state 64, d_conv 4, expand 2, headdim 64, ngroups 1). zxbcdt is the
+ * in_proj output [B*L, ldz] = z | xBC | dt_raw; xc the conv output [B*L, ldxc]
+ * = x | B | C (post-SiLU). dtype selects bf16 (fast) or fp32 (exact) storage;
+ * the scan itself always runs in fp32.                                       */
+size_t msq_mamba_states_size(int64_t B, int64_t L, int64_t nheads);
+int msq_mamba_conv_fwd(void* xc, int64_t ldxc, const void* zxbcdt, int64_t ldz, int dtype, const float* conv_w,
+                       const float* conv_b, int64_t B, int64_t L, int64_t d_inner, int64_t nheads, void* stream);
+/* y fp32 [B*L, ldy] = SSD(x, dt, A, B, C) + D x; states receive the fp32
+ * chunk-entry states (msq_mamba_states_size bytes) used by the backward.    */
+int msq_mamba_ssd_fwd(float* y, int64_t ldy, float* states, const void* xc, int64_t ldxc, const void* zxbcdt,
+                      int64_t ldz, int dtype, const float* dt_bias, const float* A_log, const float* D, int64_t B,
+                      int64_t L, int64_t d_inner, int64_t nheads, void* stream);
+/* out = (y * silu(z)) * rsqrt(mean((y*silu(z))^2) + eps) * w  (RMSNormGated) */
+int msq_mamba_gnorm_fwd(void* out, int64_t ldo, float* rstd, const float* y, int64_t ldy, const void* zxbcdt,
+                        int64_t ldz, int dtype, const float* w, int64_t rows, int64_t d_inner, float eps,
+                        void* stream);
+/* dy (fp32, ld = ldy) and dz (into dzxbcdt[:, :d_inner]); dw accumulates.   */
+int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const float* y, int64_t ldy, const void* zxbcdt, int64_t ldz,
+                        int dtype, const float* w, const float* rstd, const float* dout, int64_t ldd, float* dw,
+                        int64_t rows, int64_t d_inner, void* stream);
+/* dxc fp32 [B*L, ldxc]: dx (written) | dB, dC (reduced over heads); dt_raw
+ * grads into dzxbcdt[:, d_inner+conv_dim+h]; gA_log / gD / gdt_bias accumulate. */
+int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, const float* dY, int64_t ldy, const float* states,
+                      const void* xc, int64_t ldxc, const void* zxbcdt, int64_t ldz, int dtype, const float* dt_bias,
+                      const float* A_log, const float* D, float* gA_log, float* gD, float* gdt_bias, int64_t B,
+                      int64_t L, int64_t d_inner, int64_t nheads, void* stream);
+/* d(xBC_raw) into dzxbcdt[:, d_inner : d_inner+conv_dim]; conv grads accumulate. */
+int msq_mamba_conv_bwd(void* dzxbcdt, const float* dxc, int64_t ld_dxc, const void* zxbcdt, int64_t ldz, int dtype,
+                       const float* conv_w, const float* conv_b, float* g_conv_w, float* g_conv_b, int64_t B,
+                       int64_t L, int64_t d_inner, int64_t nheads, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
