@@ -26,6 +26,18 @@ from midiseq.train_parallel import TrainStep, SyntheticMIDI, setup_distributed  
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+METRIC = "MIDI tokens/sec/GPU (train, seq_len=2048) + AR decode tokens/sec at 1/2/4/8 GPU"
+# HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC
+# passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, KB -> bytes)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1", "pmc_ffn1_traffic.json")
+
+
+def pmc_traffic():
+    try:
+        with open(PMC_TRAFFIC) as f:
+            return int(json.load(f)["hbm_bytes_per_launch"])
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def flops_per_token(cfg, T):
@@ -95,6 +107,59 @@ def cpu_baseline(seconds_budget=20.0):
             "sample": f"oracle/ fp32 train step (fwd+filtered CE+bwd+Adam), default model, B=1, T=2048, {steps} steps"}
 
 
+def timed(fn, steps, warmup, world, dev):
+    """Runs fn() warmup times untimed, then steps times between barrier +
+    synchronize brackets; returns the max-over-ranks wall seconds."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    return el
+
+
+def decode_leg(dev, rank, world, steps=3, B=64, T=2048):
+    """Config 5: B=64 composer-conditioned prompts of 2048 tokens per GPU
+    (replicas, no communication), exact sliding-window decode (full forward
+    + filtered logit + penalties + top-k + sampling per new token)."""
+    import random
+    from midiseq.generate import generate
+    m = Transformer(TransformerConfig(precision="bf16", dropout=0.0)).to(dev)
+    src, _, meta = SyntheticMIDI(B, T, dev, rank, n_batches=1).batches[0]
+    el = timed(lambda: generate(m, T, src, meta, num_tokens=1, rng=random.Random(rank), device=dev), steps, 1,
+               world, dev)
+    del m
+    return {"value": round(world * B * steps / el, 2), "unit": "new tokens/s", "ms_per_token_step": round(el / steps * 1e3, 3),
+            "config": {"workload": "cfg 5 exact sliding-window decode (full fwd per step)", "batch_per_gpu": B,
+                       "context": T}}
+
+
+def mamba_leg(dev, rank, world, steps=3, B=8, T=4096):
+    """Config 3: models/mamba (d=1024, 10 Mamba2 layers) train step at
+    T=4096, B=8 per GPU, bf16."""
+    from midiseq.mamba import Mamba
+    m = Mamba(precision="bf16").to(dev)
+    st = TrainStep(m)
+    data = iter(SyntheticMIDI(B, T, dev, rank, n_batches=2))
+    el = timed(lambda: st(*next(data)), steps, 1, world, dev)
+    del st, m
+    return {"value": round(world * B * T * steps / el, 1), "unit": "tokens/s", "ms_per_step": round(el / steps * 1e3, 3),
+            "config": {"workload": "cfg 3 Mamba train step (filtered CE + Adam)", "batch_per_gpu": B, "seq_len": T}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -104,6 +169,7 @@ def main():
     ap.add_argument("--seq", type=int, default=2048)
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the decode and Mamba legs")
     args = ap.parse_args()
 
     rank, local, world = setup_distributed()
@@ -152,12 +218,19 @@ def main():
     fpt = flops_per_token(cfg, args.seq)
 
     ffn_ms, n_launch = timer.avg_ms()
+    extra = {}
+    if not args.no_extra:
+        del step, model
+        torch.cuda.empty_cache()
+        extra["decode"] = decode_leg(dev, rank, world)
+        torch.cuda.empty_cache()
+        extra["mamba_train"] = mamba_leg(dev, rank, world)
     M = args.batch * (args.seq + 6)
     ffn_flops = 2.0 * M * (4 * cfg.n_embd) * cfg.n_embd
     achieved = ffn_flops / (ffn_ms * 1e-3) / 1e12 if ffn_ms > 0 else 0.0
     if rank == 0:
         out = {
-            "metric": "MIDI tokens/sec (train, seq_len=2048)",
+            "metric": METRIC,
             "value": round(value, 1),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -178,9 +251,11 @@ def main():
             "loss_last": round(float(loss.item()), 4),
             "roofline": {"kernel": "gemm_bf16 FFN1 (NT, bias+ReLU epilogue) 65728x4096x1024",
                          "bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(),
+                         "algorithmic_bytes": int(2 * (M * cfg.n_embd + 4 * cfg.n_embd * cfg.n_embd + M * 4 * cfg.n_embd)),
                          "avg_launch_ms": round(ffn_ms, 4), "launches": n_launch},
         }
+        out.update(extra)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
