@@ -1,0 +1,67 @@
+// Shared declarations of the bf16 / fp32 GEMM kernels (gemm.hip: 128x128
+// register-staged tile; gemm256.hip: 256x256 LDS-DMA ping-pong tile).
+#pragma once
+#include "common.h"
+
+struct GemmArgs {
+    int64_t M, N, K;
+    const void* A; int64_t lda, sA;
+    const void* B; int64_t ldb, sB;
+    void* C; int64_t ldc, sC;
+    const float* bias;
+    const void* aux; int64_t ldx, sX;
+    int tiles_m, tiles_n, batch;
+    int vec;     // C / aux / bias rows allow 16-B vector access
+    int ksplit;  // >1: K range split over blocks, ACCUM epilogue via fp32 atomics
+    int64_t kper;
+    uint32_t a_ext, b_ext;  // bytes of one batch's A / B extent (256-tile buffer descriptors)
+};
+
+template <typename TC>
+__device__ __forceinline__ void epi_store(TC* p, f32x4 v, int nv) {
+    if (nv == 4) {
+        store4(p, v);
+    } else {
+        const int n = nv < 0 ? -nv : nv;
+        for (int i = 0; i < n; ++i) p[i] = (TC)v[i];
+    }
+}
+// load up to 4 elements (nv as in epi_store)
+template <typename T>
+__device__ __forceinline__ f32x4 epi_load(const T* p, int nv) {
+    if (nv == 4) return load4(p);
+    const int n = nv < 0 ? -nv : nv;
+    f32x4 x = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < n; ++i) x[i] = (float)p[i];
+    return x;
+}
+
+// Applies the epilogue to one lane's 4 consecutive outputs C[m][n..n+3].
+template <int EPI, typename TC, typename TX>
+__device__ __forceinline__ void epi_apply(const GemmArgs& g, TC* C, const TX* X, int64_t m, int64_t n, f32x4 v) {
+    const int nv = g.vec ? (int)min<int64_t>(4, g.N - n) : -(int)min<int64_t>(4, g.N - n);
+    if ((EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID) && g.bias)
+        v += epi_load(g.bias + n, nv);
+    if (EPI == MSQ_EPI_BIAS_RELU) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);
+    }
+    if (EPI == MSQ_EPI_BIAS_RESID) v += epi_load(X + m * g.ldx + n, nv);
+    if (EPI == MSQ_EPI_RELU_MASK) {
+        const f32x4 x = epi_load(X + m * g.ldx + n, nv);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = x[t] > 0.f ? v[t] : 0.f;
+    }
+    TC* cp = C + m * g.ldc + n;
+    if (EPI == MSQ_EPI_ACCUM && g.ksplit > 1) {
+        const int na = nv < 0 ? -nv : nv;
+        for (int t = 0; t < na; ++t) atomicAdd((float*)cp + t, v[t]);
+        return;
+    }
+    if (EPI == MSQ_EPI_ACCUM) v += epi_load(cp, nv);
+    epi_store(cp, v, nv);
+}
+
+// 256x256 kernel family: returns false when the problem does not fit its
+// preconditions (the caller then uses the 128x128 kernel).
+bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s);

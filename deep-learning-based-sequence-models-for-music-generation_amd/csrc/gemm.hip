@@ -13,24 +13,14 @@
 // ReLU-mask, accumulate) works on float4 and stores 8/16 B per lane.
 //
 // fp32 exact path: plain LDS-tiled FMA kernel, fp32 end to end (parity mode).
-#include "common.h"
+#include "gemm.h"
+#include <stdlib.h>
 
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 
-struct GemmArgs {
-    int64_t M, N, K;
-    const void* A; int64_t lda, sA;
-    const void* B; int64_t ldb, sB;
-    void* C; int64_t ldc, sC;
-    const float* bias;
-    const void* aux; int64_t ldx, sX;
-    int tiles_m, tiles_n, batch;
-    int vec;     // C / aux / bias rows allow 16-B vector access
-    int ksplit;  // >1: K range split over blocks, ACCUM epilogue via fp32 atomics
-    int64_t kper;
-};
+
 
 __device__ __forceinline__ int swz_k(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 __device__ __forceinline__ int swz_mn(int k, int chunk) { return chunk ^ ((((k & 3) | ((k >> 1) & 4))) << 1); }
@@ -123,25 +113,6 @@ __device__ __forceinline__ bf16x8 read_frag(const char* s, int rb, int ks, int l
         u.h[1] = b;
         return u.v;
     }
-}
-
-template <typename TC>
-__device__ __forceinline__ void epi_store(TC* p, f32x4 v, int nv) {
-    if (nv == 4) {
-        store4(p, v);
-    } else {
-        const int n = nv < 0 ? -nv : nv;
-        for (int i = 0; i < n; ++i) p[i] = (TC)v[i];
-    }
-}
-// load up to 4 elements (nv as in epi_store)
-template <typename T>
-__device__ __forceinline__ f32x4 epi_load(const T* p, int nv) {
-    if (nv == 4) return load4(p);
-    const int n = nv < 0 ? -nv : nv;
-    f32x4 x = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int i = 0; i < n; ++i) x[i] = (float)p[i];
-    return x;
 }
 
 template <int TA, int TB, int EPI, typename TC, typename TX>
@@ -391,6 +362,10 @@ extern "C" int msq_gemm(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t
         }
     }
     hipStream_t s = (hipStream_t)stream;
+    if (dtype == MSQ_BF16 && !getenv("MSQ_GEMM128") && gemm256_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, s)) {
+        MSQ_LAUNCH_CHECK();
+        return MSQ_OK;
+    }
     int rc;
     if (dtype == MSQ_BF16)
         rc = c_dtype == MSQ_BF16 ? dispatch_epi<true, bf16>(g, ta, tb, epilogue, aux_dtype, s)

@@ -1,0 +1,371 @@
+// 256x256x64 bf16 GEMM tile for the large products of the train step
+// (QKV / proj / FFN / lm_head forward, their dX and dW products).
+//
+// Structure (cdna_hip_programming.md §5 "256² 8-phase template", rebuilt for
+// the three operand layouts this path needs):
+//   * 512 threads = 8 waves as 2 (M) x 4 (N); a wave owns 128x64 outputs as
+//     2x2 quadrants of 64x32 (32 accumulators of v_mfma_f32_16x16x32_bf16).
+//   * LDS (128 KiB, one dynamic array) = 2 K-tile buffers x 4 half-tile slots
+//     {A rows 0-127, B rows 0-127, A rows 128-255, B rows 128-255}, 16 KiB each.
+//     A wave's quadrant (mi, ni) reads A-half mi and B-half ni only.
+//   * Half-tiles are filled by buffer_load_dwordx4 ... lds (LDS DMA, 2 per
+//     thread per half) whose buffer descriptor zero-fills every out-of-range
+//     chunk, so M / N / K edges and split-K slices need no masking in LDS.
+//     The XOR swizzle is applied on the SOURCE address (the LDS image is
+//     lane-linear) and again on the ds_read address (rule 21).
+//   * A K-tile is 4 phases, one per quadrant: (0,0) (1,0) (1,1) (0,1). Each
+//     phase = {ds_reads of the fragments it introduces; LDS-DMA of one
+//     half-tile 5 phases ahead; s_waitcnt vmcnt(8)} barrier {16 MFMA} barrier.
+//     Waves 4-7 run one barrier behind waves 0-3 (ping-pong), so on every SIMD
+//     one wave issues MFMAs while the other issues LDS / global traffic.
+//   * vmcnt(8) in a phase retires the half-tile read in the next phase and
+//     leaves four half-tiles (8 DMA per thread) in flight; a slot is re-filled
+//     >= 2 phases after its last ds_read (the staggered groups' WAR distance).
+// Operands: K-contiguous ([rows][K], e.g. activations, nn.Linear weights) use
+// 128-B LDS rows read with ds_read_b128; M/N-contiguous ([K][rows], the dY of
+// a dW product or W in dX = dY.W) use 256-B LDS rows read with
+// ds_read_b64_tr_b16 (hardware transpose), so no operand is ever transposed.
+#include "gemm.h"
+
+namespace {
+
+constexpr int NT = 512;
+constexpr int HALF = 16384;          // bytes of one half-tile slot
+constexpr uint32_t OOB = 0xFFFF0000u;  // voffset past every descriptor's num_records
+
+typedef __attribute__((address_space(3))) char lds_t;
+
+__device__ __forceinline__ int swz_k(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+__device__ __forceinline__ int gmn(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
+
+__device__ __forceinline__ void vm_wait8() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+__device__ __forceinline__ void vm_wait0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void barrier() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// Per-lane staging state of one operand (both halves, both DMA per half).
+template <int KC>
+struct Stage {
+    uint32_t off[2][2];  // byte offset of this lane's chunk at k0 = 0, [half][j]
+    int kk[2];           // k of this lane's chunk relative to k0 (validity), [j]
+    bool rv[2][2];       // row / column in range, [half][j]
+    uint32_t kstep;      // bytes per unit of k (K-contig: 2, MN-contig: 2*ld)
+
+    __device__ __forceinline__ void init(int64_t r0, int64_t R, int64_t ld, int w, int lane) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int li = (j * 8 + w) * 1024 + lane * 16;  // byte in the half-tile image
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (KC) {  // image [128 rows][128 B]
+                    const int row = li >> 7, slot = (li >> 4) & 7;
+                    const int ch = slot ^ ((row >> 1) & 7);
+                    const int64_t gr = r0 + h * 128 + row;
+                    rv[h][j] = gr < R;
+                    off[h][j] = (uint32_t)((rv[h][j] ? gr : 0) * ld * 2 + ch * 16);
+                    kk[j] = ch * 8;
+                } else {  // image [64 k][256 B]
+                    const int k = li >> 8, slot = (li >> 4) & 15;
+                    const int ch = slot ^ gmn(k);
+                    const int64_t gc = r0 + h * 128 + ch * 8;
+                    rv[h][j] = gc < R;
+                    off[h][j] = (uint32_t)((int64_t)k * ld * 2 + (rv[h][j] ? gc : 0) * 2);
+                    kk[j] = k;
+                }
+            }
+        }
+        kstep = KC ? 2u : (uint32_t)(ld * 2);
+    }
+
+    // DMA half h of the K-tile starting at k0 (krem = valid k left from k0)
+    __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, lds_t* slot, int h, int64_t k0, int64_t krem,
+                                          int wu) const {
+        const uint32_t kadv = (uint32_t)k0 * kstep;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t vo = (rv[h][j] && kk[j] < krem) ? off[h][j] + kadv : OOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(slot + (j * 8 + wu) * 1024), 16, vo, 0, 0, 0);
+        }
+    }
+};
+
+// descriptor from provably wave-uniform words (no waterfall loops, T20)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const char* base, uint32_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void* p = (void*)(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+__device__ __forceinline__ bf16x8 rd_b128(const lds_t* p) { return *(const bf16x8 __attribute__((address_space(3)))*)p; }
+__device__ __forceinline__ bf16x8 rd_tr(const lds_t* p) {
+    i16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((i16x4 __attribute__((address_space(3)))*)p);
+    i16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((i16x4 __attribute__((address_space(3)))*)(p + 1024));
+    union { i16x4 h[2]; bf16x8 v; } u;
+    u.h[0] = a;
+    u.h[1] = b;
+    return u.v;
+}
+
+// fragment set of one quadrant-operand: NF 16-row groups x 2 k-steps
+template <int KC, int NF>
+__device__ __forceinline__ void read_set(bf16x8 (&f)[2][NF], const lds_t* slot, int rbase, const int (&lo)[4]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            if (KC) f[ks][i] = rd_b128(slot + (rbase + i * 16) * 128 + lo[ks]);
+            else f[ks][i] = rd_tr(slot + ks * 8192 + lo[i]);
+        }
+}
+
+// LAB: ablation switches for tools/gemm256_lab.hip only (0 in the library):
+// 1 = no LDS-DMA in the K loop, 2 = no MFMA, 4 = no ping-pong stagger
+template <int TA, int TB, int EPI, typename TC, typename TX, int LAB = 0>
+__global__ __launch_bounds__(NT, 1) void gemm256_kernel(GemmArgs g) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    lds_t* smem = (lds_t*)smem_raw;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 2, wc = w & 3;
+
+    const int tiles = g.tiles_m * g.tiles_n;
+    // every tile / slice index is wave-uniform: keep it scalar (T20)
+    int bid = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x));
+    const int kslice = bid % g.ksplit;
+    bid /= g.ksplit;
+    const int bz = bid / tiles;
+    bid -= bz * tiles;
+    const int GROUP = 8;
+    const int per_group = GROUP * g.tiles_n;
+    const int grp = bid / per_group, first_m = grp * GROUP;
+    const int gsz = min(g.tiles_m - first_m, GROUP);
+    const int tm = first_m + (bid % per_group) % gsz;
+    const int tn = (bid % per_group) / gsz;
+    const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
+
+    const char* Ab = (const char*)g.A + (int64_t)bz * g.sA * 2;
+    const char* Bb = (const char*)g.B + (int64_t)bz * g.sB * 2;
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(Ab, g.a_ext);
+    const __amdgpu_buffer_rsrc_t rb = make_rsrc(Bb, g.b_ext);
+
+    Stage<TA == 0> sa;
+    Stage<TB == 0> sb;
+    sa.init(m0, g.M, g.lda, w, lane);
+    sb.init(n0, g.N, g.ldb, w, lane);
+
+    // per-lane fragment offsets inside a half-tile slot
+    int loA[4], loB[4];
+    {
+        const int r = lane & 15, gq = lane >> 4;
+        if (TA == 0) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) loA[ks] = r * 128 + ((ks * 4 + gq) ^ ((r >> 1) & 7)) * 16;
+            loA[2] = loA[3] = 0;
+        } else {
+            const int q = r >> 2, p = r & 3, k = 8 * gq + q;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                loA[i] = k * 256 + ((((wr * 64 + i * 16) >> 3) ^ gmn(k)) | (p >> 1)) * 16 + (p & 1) * 8;
+        }
+        if (TB == 0) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) loB[ks] = r * 128 + ((ks * 4 + gq) ^ ((r >> 1) & 7)) * 16;
+            loB[2] = loB[3] = 0;
+        } else {
+            const int q = r >> 2, p = r & 3, k = 8 * gq + q;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                loB[i] = k * 256 + ((((wc * 32 + i * 16) >> 3) ^ gmn(k)) | (p >> 1)) * 16 + (p & 1) * 8;
+            loB[2] = loB[3] = 0;
+        }
+    }
+
+    const int64_t kbeg = (int64_t)kslice * g.kper;
+    const int64_t kend = min<int64_t>(g.K, kbeg + g.kper);
+    const int nk = (int)((kend - kbeg + 63) / 64);
+
+    // slot s of buffer b: b*4 + {0: A0, 1: B0, 2: A1, 3: B1}
+    auto slot = [&](int b, int s) { return smem + (b * 4 + s) * HALF; };
+    // stage index s = 4u + h; h: 0 A0, 1 B0, 2 A1, 3 B1
+    auto issue = [&](int u, int h) {
+        const int64_t k0 = kbeg + (int64_t)u * 64;
+        lds_t* dst = slot(u & 1, h);
+        if (h == 0) sa.issue(ra, dst, 0, k0, kend - k0, w);
+        else if (h == 1) sb.issue(rb, dst, 0, k0, kend - k0, w);
+        else if (h == 2) sa.issue(ra, dst, 1, k0, kend - k0, w);
+        else sb.issue(rb, dst, 1, k0, kend - k0, w);
+    };
+
+    f32x4 acc[2][2][4][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    // prologue: stages 0..5
+    issue(0, 0);
+    issue(0, 1);
+    issue(0, 2);
+    issue(0, 3);
+    if (nk > 1) {
+        issue(1, 0);
+        issue(1, 1);
+        vm_wait8();
+    } else {
+        vm_wait0();
+    }
+    barrier();
+    if (!(LAB & 4) && wr == 1) barrier();
+
+    bf16x8 af[2][2][4];  // [mi][ks][i]
+    bf16x8 bfr[2][2][2];  // [ni][ks][j]
+
+    // one phase: quadrant Q of K-tile t held in buffer BUF
+#define MSQ_PHASE(Q, BUF)                                                                               \
+    {                                                                                                   \
+        constexpr int mi = (Q == 1 || Q == 2) ? 1 : 0;                                                  \
+        constexpr int ni = (Q >= 2) ? 1 : 0;                                                            \
+        if (Q == 0) {                                                                                   \
+            read_set<TA == 0, 4>(af[0], slot(BUF, 0), wr * 64, loA);                                    \
+            read_set<TB == 0, 2>(bfr[0], slot(BUF, 1), wc * 32, loB);                                   \
+        } else if (Q == 1) {                                                                            \
+            read_set<TA == 0, 4>(af[1], slot(BUF, 2), wr * 64, loA);                                    \
+        } else if (Q == 2) {                                                                            \
+            read_set<TB == 0, 2>(bfr[1], slot(BUF, 3), wc * 32, loB);                                   \
+        }                                                                                               \
+        const int su = (Q < 2) ? t + 1 : t + 2;                                                         \
+        if (su < nk && !(LAB & 1)) {                                                                    \
+            issue(su, (Q + 2) & 3);                                                                     \
+            vm_wait8();                                                                                 \
+        } else {                                                                                        \
+            vm_wait0();                                                                                 \
+        }                                                                                               \
+        barrier();                                                                                      \
+        __builtin_amdgcn_s_setprio(1);                                                                  \
+        _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                                \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i)                                               \
+                _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                         \
+                    if (LAB & 2) {                                                                      \
+                        asm volatile("" ::"v"(bfr[ni][ks][j]), "v"(af[mi][ks][i]));                     \
+                    } else {                                                                            \
+                        acc[mi][ni][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                    \
+                            bfr[ni][ks][j], af[mi][ks][i], acc[mi][ni][i][j], 0, 0, 0);                 \
+                    }                                                                                   \
+                }                                                                                       \
+        __builtin_amdgcn_s_setprio(0);                                                                  \
+        barrier();                                                                                      \
+    }
+
+    for (int t = 0; t < nk; t += 2) {
+        MSQ_PHASE(0, 0)
+        MSQ_PHASE(1, 0)
+        MSQ_PHASE(2, 0)
+        MSQ_PHASE(3, 0)
+        if (t + 1 < nk) {
+            ++t;
+            MSQ_PHASE(0, 1)
+            MSQ_PHASE(1, 1)
+            MSQ_PHASE(2, 1)
+            MSQ_PHASE(3, 1)
+            --t;
+        }
+    }
+#undef MSQ_PHASE
+    if (!(LAB & 4) && wr == 0) barrier();
+
+    // epilogue: lane holds C[m][n..n+3]
+    TC* C = (TC*)g.C + bz * g.sC;
+    const TX* X = (const TX*)g.aux + (g.aux ? bz * g.sX : 0);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t m = m0 + a * 128 + wr * 64 + i * 16 + (lane & 15);
+            if (m >= g.M) continue;
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int64_t n = n0 + b * 128 + wc * 32 + j * 16 + 4 * (lane >> 4);
+                    if (n >= g.N) continue;
+                    epi_apply<EPI, TC, TX>(g, C, X, m, n, acc[a][b][i][j]);
+                }
+        }
+}
+
+template <int TA, int TB, int EPI, typename TC, typename TX>
+void launch(const GemmArgs& g, hipStream_t s) {
+    static bool attr = false;
+    auto k = gemm256_kernel<TA, TB, EPI, TC, TX>;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * HALF);
+        attr = true;
+    }
+    const int nblk = g.tiles_m * g.tiles_n * g.batch * g.ksplit;
+    hipLaunchKernelGGL(k, dim3(nblk), dim3(NT), 8 * HALF, s, g);
+}
+
+template <int EPI, typename TC, typename TX>
+void dispatch_t(const GemmArgs& g, int ta, int tb, hipStream_t s) {
+    if (ta == 0 && tb == 0) launch<0, 0, EPI, TC, TX>(g, s);
+    else if (ta == 0 && tb == 1) launch<0, 1, EPI, TC, TX>(g, s);
+    else if (ta == 1 && tb == 1) launch<1, 1, EPI, TC, TX>(g, s);
+    else launch<1, 0, EPI, TC, TX>(g, s);
+}
+
+template <typename TC>
+void dispatch_epi(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hipStream_t s) {
+    switch (epi) {
+        case MSQ_EPI_NONE: dispatch_t<MSQ_EPI_NONE, TC, float>(g, ta, tb, s); break;
+        case MSQ_EPI_BIAS: dispatch_t<MSQ_EPI_BIAS, TC, float>(g, ta, tb, s); break;
+        case MSQ_EPI_BIAS_RELU: dispatch_t<MSQ_EPI_BIAS_RELU, TC, float>(g, ta, tb, s); break;
+        case MSQ_EPI_BIAS_RESID: dispatch_t<MSQ_EPI_BIAS_RESID, TC, float>(g, ta, tb, s); break;
+        case MSQ_EPI_RELU_MASK:
+            if (aux_dtype == MSQ_BF16) dispatch_t<MSQ_EPI_RELU_MASK, TC, bf16>(g, ta, tb, s);
+            else dispatch_t<MSQ_EPI_RELU_MASK, TC, float>(g, ta, tb, s);
+            break;
+        case MSQ_EPI_ACCUM: dispatch_t<MSQ_EPI_ACCUM, TC, float>(g, ta, tb, s); break;
+    }
+}
+
+}  // namespace
+
+bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s) {
+    // preconditions: chunks of 8 never straddle an edge; extents fit a descriptor
+    if ((ta ? g.M : g.K) % 8 || (tb ? g.N : g.K) % 8) return false;
+    const int64_t aext = ((ta ? g.K : g.M) - 1) * g.lda + (ta ? g.M : g.K);
+    const int64_t bext = ((tb ? g.K : g.N) - 1) * g.ldb + (tb ? g.N : g.K);
+    if (aext * 2 >= (int64_t)OOB || bext * 2 >= (int64_t)OOB) return false;
+    g.tiles_m = (int)((g.M + 255) / 256);
+    g.tiles_n = (int)((g.N + 255) / 256);
+    const int64_t tiles = (int64_t)g.tiles_m * g.tiles_n * g.batch;
+    g.ksplit = 1;
+    g.kper = (g.K + 63) / 64 * 64;
+    if (epi == MSQ_EPI_ACCUM) {
+        // split-K for the weight-gradient products: about one block per CU
+        int64_t ks = (256 + tiles - 1) / tiles;
+        ks = std::min<int64_t>(ks, std::max<int64_t>(1, g.K / 2048));
+        if (ks > 1) {
+            g.kper = ((g.K + ks - 1) / ks + 63) / 64 * 64;
+            g.ksplit = (int)((g.K + g.kper - 1) / g.kper);
+        }
+    }
+    // below ~half a wave of blocks the 128x128 tile (4x the blocks) wins
+    if (tiles * g.ksplit < 128) return false;
+    g.a_ext = (uint32_t)(aext * 2);
+    g.b_ext = (uint32_t)(bext * 2);
+    if (c_dtype == MSQ_BF16) dispatch_epi<bf16>(g, ta, tb, epi, aux_dtype, s);
+    else dispatch_epi<float>(g, ta, tb, epi, aux_dtype, s);
+    return true;
+}

@@ -134,7 +134,7 @@ class _MActs:
             e = lambda *s, dt=act: torch.empty(*s, device=device, dtype=dt)  # noqa: E731
             self._bwd = dict(gx=e(M, cfg.d_model, dt=f32), gxb=e(M, cfg.d_model), dyn=e(M, cfg.d_inner, dt=f32),
                              dy=e(M, cfg.d_inner, dt=f32), dzx=e(M, cfg.d_in_proj), dxc=e(M, cfg.conv_dim, dt=f32),
-                             df=e(self.B * self.T, cfg.d_model), dlogits=e(self.B * self.T, cfg.v_pad))
+                             df=e(self.B * self.T, cfg.d_model), dlogits=torch.zeros(self.B * self.T, cfg.v_pad, device=device, dtype=act))
         return self._bwd
 
 
@@ -215,7 +215,8 @@ class MambaEngine:
                 ops.cast(xa, xo)
         ops.layernorm_fwd(A.xlast, P["lnf_w"], P["lnf_b"], out=A.f, mean=A.stf[0], rstd=A.stf[1], seg=(T, N_META))
         V = cfg.vocab_size
-        ops.gemm(A.f, W["lm_w"][:V], out=A.logits[:, :V], epilogue=L.EPI_BIAS, bias=P["lm_b"][:V])
+        # full V_pad rows (pad rows of lm_w / lm_b are zero): 16-B aligned rows, 256-tile eligible
+        ops.gemm(A.f, W["lm_w"], out=A.logits, epilogue=L.EPI_BIAS, bias=P["lm_b"])
         return A.logits.view(B, T, cfg.v_pad)[:, :, :V]
 
     def backward(self, dlogits, grads):
@@ -231,9 +232,9 @@ class MambaEngine:
         s = stream()
         hook = self.layer_grad_ready
         dl = dlogits[:, :V]
-        ops.gemm(dl, A.f, ta=True, tb=True, out=G["lm_w"][:V], epilogue=L.EPI_ACCUM)
+        ops.gemm(dlogits, A.f, ta=True, tb=True, out=G["lm_w"], epilogue=L.EPI_ACCUM)  # pad columns are 0
         ops.colsum(dl, G["lm_b"][:V], accumulate=True)
-        ops.gemm(dl, W["lm_w"][:V], tb=True, out=Bw["df"])
+        ops.gemm(dlogits, W["lm_w"], tb=True, out=Bw["df"])
         gx, gxb = Bw["gx"], Bw["gxb"]
         gx.zero_()
         ops.layernorm_bwd(gx, Bw["df"], A.xlast, A.stf[0], A.stf[1], P["lnf_w"], G["lnf_w"], G["lnf_b"],

@@ -173,7 +173,7 @@ class _Acts:
             e = lambda *s, dt=act: torch.empty(*s, device=device, dtype=dt)  # noqa: E731
             self._bwd = dict(gres=e(M, d, dt=f32), gb=e(M, d) if act != f32 else None, dtmp=e(M, d),
                              dh=e(M, 4 * d), dqkv=e(M, 3 * d), df=e(self.B * self.T, d),
-                             dlogits=e(self.B * self.T, cfg.v_pad))
+                             dlogits=torch.zeros(self.B * self.T, cfg.v_pad, device=device, dtype=act))
         return self._bwd
 
 
@@ -254,7 +254,8 @@ class TransformerEngine:
         ops.layernorm_fwd(x_last, P["lnf_w"], P["lnf_b"], out=A.f, mean=A.stf[0], rstd=A.stf[1],
                           seg=(T, N_META))
         V = cfg.vocab_size
-        ops.gemm(A.f, W["lm_w"][:V], out=A.logits[:, :V], epilogue=L.EPI_BIAS, bias=P["lm_b"][:V])
+        # full V_pad rows (pad rows of lm_w / lm_b are zero): 16-B aligned rows, 256-tile eligible
+        ops.gemm(A.f, W["lm_w"], out=A.logits, epilogue=L.EPI_BIAS, bias=P["lm_b"])
         return A.logits.view(B, T, cfg.v_pad)[:, :, :V]
 
     # ------------------------------------------------------------ backward
@@ -271,9 +272,9 @@ class TransformerEngine:
         scale = d ** -0.5
         dl = dlogits[:, :V]
         # lm_head (model_transformer.py:147,161)
-        ops.gemm(dl, A.f, ta=True, tb=True, out=G["lm_w"][:V], epilogue=L.EPI_ACCUM)
+        ops.gemm(dlogits, A.f, ta=True, tb=True, out=G["lm_w"], epilogue=L.EPI_ACCUM)  # pad columns are 0
         ops.colsum(dl, G["lm_b"][:V], accumulate=True)
-        ops.gemm(dl, W["lm_w"][:V], tb=True, out=Bw["df"])
+        ops.gemm(dlogits, W["lm_w"], tb=True, out=Bw["df"])
         gres = Bw["gres"]
         gres.zero_()
         gb = Bw["gb"] if Bw["gb"] is not None else gres
@@ -335,13 +336,11 @@ class _TransformerFn(torch.autograd.Function):
             raise RuntimeError("activations were overwritten by a later forward; call backward before the next forward")
         B, T = ctx.shape
         cfg = eng.cfg
-        if dlogits.dtype == eng.act and dlogits.stride(2) == 1 and dlogits.stride(1) % 8 == 0 and \
-                dlogits.stride(0) == T * dlogits.stride(1):
-            dl2 = dlogits.as_strided((B * T, dlogits.stride(1)), (dlogits.stride(1), 1))
-        else:
-            buf = eng.dlogits_buffer(B, T)
-            buf.view(B, T, cfg.v_pad)[:, :, :cfg.vocab_size].copy_(dlogits)
-            dl2 = buf
+        # copy into the engine's zero-padded buffer: the lm_head GEMMs run over
+        # all V_pad columns and rely on the pad columns being zero
+        buf = eng.dlogits_buffer(B, T)
+        buf.view(B, T, cfg.v_pad)[:, :, :cfg.vocab_size].copy_(dlogits)
+        dl2 = buf
         grads = torch.zeros_like(eng.flat.data)
         eng.backward(dl2, grads)
         return grads, None, None, None

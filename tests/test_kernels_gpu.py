@@ -62,6 +62,55 @@ def test_gemm_epilogues(dtype):
     assert _rel(ob.float(), base + bias) < 1e-2
 
 
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 1), (1, 0)])
+@pytest.mark.parametrize("M,N,K", [(4104, 2056, 1000), (2304, 4096, 512)])
+def test_gemm256_layouts_and_edges(ta, tb, M, N, K):
+    """Large products take the 256x256 LDS-DMA tile; M/N/K edges are
+    zero-filled by the buffer descriptor (K % 64 != 0, M % 256 != 0)."""
+    g = torch.Generator().manual_seed(M + N + K + ta + 2 * tb)
+    a = torch.randn(M, K, generator=g).bfloat16()
+    b = torch.randn(N, K, generator=g).bfloat16()
+    ref = a.float() @ b.float().t()
+    A = (a.t().contiguous() if ta else a).to(dev)
+    Bm = (b.t().contiguous() if tb else b).to(dev)
+    out = ops.gemm(A, Bm, ta=bool(ta), tb=bool(tb), out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert _rel(out, ref) < 2e-3
+    acc = torch.randn(M, N, generator=g).to(dev)
+    ref2 = acc.cpu() + ref
+    ops.gemm(A, Bm, ta=bool(ta), tb=bool(tb), out=acc, epilogue=L.EPI_ACCUM)
+    assert _rel(acc, ref2) < 2e-3
+
+
+def test_gemm256_splitk_weight_grad():
+    """dW = dY^T X with K = tokens (split-K over 16 slices, fp32 atomics)."""
+    g = torch.Generator().manual_seed(11)
+    Kt, M, N = 32776, 1024, 1024
+    dy = (torch.randn(Kt, M, generator=g) * 0.1).bfloat16()
+    x = torch.randn(Kt, N, generator=g).bfloat16()
+    ref = dy.float().t() @ x.float()
+    G = torch.full((M, N), 0.5, device=dev)
+    ops.gemm(dy.to(dev), x.to(dev), ta=True, tb=True, out=G, epilogue=L.EPI_ACCUM)
+    assert _rel(G.cpu() - 0.5, ref) < 2e-3
+
+
+def test_gemm256_epilogues_bf16_out():
+    g = torch.Generator().manual_seed(12)
+    M, N, K = 3000, 3072, 1024
+    a = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * 0.05).bfloat16()
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g)
+    base = a.float() @ w.float().t()
+    A, W, bi, R = a.to(dev), w.to(dev), bias.to(dev), res.to(dev)
+    o = ops.gemm(A, W, out_dtype=torch.bfloat16, epilogue=L.EPI_BIAS_RELU, bias=bi)
+    assert _rel(o.float(), torch.relu(base + bias)) < 1e-2
+    o = ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_BIAS_RESID, bias=bi, aux=R)
+    assert _rel(o, base + bias + res) < 2e-3
+    o = ops.gemm(A, W, out_dtype=torch.bfloat16, epilogue=L.EPI_RELU_MASK, aux=R.bfloat16())
+    assert _rel(o.float(), base * (res.bfloat16().float() > 0)) < 1e-2
+
+
 def test_gemm_batched_strided():
     g = torch.Generator().manual_seed(5)
     Bt, S, T, d, V = 3, 70, 64, 128, 200
