@@ -19,5 +19,7 @@ int exact_bwd(const AttnArgs& a, const float* lse, const float* dout, int64_t ld
 int64_t flash_dqr_ld(int64_t S);
 size_t flash_bwd_workspace(int64_t B, int64_t S, int64_t H);
 int flash_fwd(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s);
+// v2 forward (attn_fwd.hip): 128-query blocks, LDS-DMA K/V/R-ring pipeline; -1 if unsupported
+int flash_fwd2(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s);
 int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo, const bf16* out, bf16* dqkv,
               int64_t ldd, float* dR, void* ws, hipStream_t s);

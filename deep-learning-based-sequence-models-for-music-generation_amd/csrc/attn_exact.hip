@@ -10,6 +10,7 @@
 // from the saved log-sum-exp and stores P / dS rows in the workspace for the
 // column reductions (dK, dV, dR).
 #include "attn.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -218,7 +219,7 @@ extern "C" int msq_relattn_fwd(int dtype, void* out, int64_t ld_out, float* lse,
         exact_fwd(a, (float*)out, ld_out, lse, s);
     } else {
         MSQ_CHECK_ARG(hs == 128 && ld_qkv % 8 == 0 && ld_out % 4 == 0, "msq_relattn_fwd: bf16 path needs hs == 128");
-        flash_fwd(a, (bf16*)out, ld_out, lse, s);
+        if (getenv("MSQ_ATTN_FWD_V1") || flash_fwd2(a, (bf16*)out, ld_out, lse, s)) flash_fwd(a, (bf16*)out, ld_out, lse, s);
     }
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;

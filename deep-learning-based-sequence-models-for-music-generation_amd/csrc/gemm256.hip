@@ -126,7 +126,8 @@ __device__ __forceinline__ void read_set(bf16x8 (&f)[2][NF], const lds_t* slot, 
 }
 
 // LAB: ablation switches for tools/gemm256_lab.hip only (0 in the library):
-// 1 = no LDS-DMA in the K loop, 2 = no MFMA, 4 = no ping-pong stagger
+// 1 = no LDS-DMA in the K loop, 2 = no MFMA, 4 = no ping-pong stagger,
+// 8 = K slice innermost in the block order
 template <int TA, int TB, int EPI, typename TC, typename TX, int LAB = 0>
 __global__ __launch_bounds__(NT, 1) void gemm256_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -138,8 +139,16 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(GemmArgs g) {
     const int tiles = g.tiles_m * g.tiles_n;
     // every tile / slice index is wave-uniform: keep it scalar (T20)
     int bid = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x));
-    const int kslice = bid % g.ksplit;
-    bid /= g.ksplit;
+    // K slice outermost: the blocks that run together on an XCD share the
+    // same K range, so their A / B panels meet in that XCD's L2
+    int kslice;
+    if (LAB & 8) {
+        kslice = bid % g.ksplit;
+        bid /= g.ksplit;
+    } else {
+        kslice = bid / (tiles * g.batch);
+        bid -= kslice * tiles * g.batch;
+    }
     const int bz = bid / tiles;
     bid -= bz * tiles;
     const int GROUP = 8;

@@ -16,9 +16,10 @@ __global__ void fill(bf16* p, int64_t n, uint32_t seed) {
     }
 }
 
-template <int LAB>
-float run(GemmArgs g, int iters) {
-    auto k = gemm256_kernel<0, 0, MSQ_EPI_NONE, bf16, float, LAB>;
+static int g_ta = 0, g_tb = 0;
+template <int LAB, int TA, int TB>
+float run_t(GemmArgs g, int iters) {
+    auto k = gemm256_kernel<TA, TB, MSQ_EPI_NONE, float, float, LAB>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * HALF);
     const int nblk = g.tiles_m * g.tiles_n * g.batch * g.ksplit;
     hipEvent_t a, b;
@@ -33,26 +34,37 @@ float run(GemmArgs g, int iters) {
     (void)hipEventElapsedTime(&ms, a, b);
     return ms / iters;
 }
+template <int LAB>
+float run(GemmArgs g, int iters) {
+    if (g_ta && g_tb) return run_t<LAB, 1, 1>(g, iters);
+    if (g_tb) return run_t<LAB, 0, 1>(g, iters);
+    return run_t<LAB, 0, 0>(g, iters);
+}
 
 int main(int argc, char** argv) {
     int64_t M = 65728, N = 4096, K = 1024;
+    int ksplit = 1;
     if (argc > 3) { M = atoll(argv[1]); N = atoll(argv[2]); K = atoll(argv[3]); }
+    if (argc > 5) { g_ta = atoi(argv[4]); g_tb = atoi(argv[5]); }
+    if (argc > 6) ksplit = atoi(argv[6]);
     bf16 *A, *B, *C;
     (void)hipMalloc(&A, M * K * 2);
     (void)hipMalloc(&B, N * K * 2);
-    (void)hipMalloc(&C, M * N * 2);
+    (void)hipMalloc(&C, M * N * 4);
     hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, A, M * K, 1u);
     hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, B, N * K, 2u);
     GemmArgs g{};
     g.M = M; g.N = N; g.K = K;
-    g.A = A; g.lda = K; g.B = B; g.ldb = K; g.C = C; g.ldc = N;
-    g.batch = 1; g.vec = 1; g.ksplit = 1; g.kper = (K + 63) / 64 * 64;
+    g.A = A; g.lda = g_ta ? M : K; g.B = B; g.ldb = g_tb ? N : K; g.C = C; g.ldc = N;
+    g.batch = 1; g.vec = 1; g.ksplit = ksplit;
+    g.kper = ((K + ksplit - 1) / ksplit + 63) / 64 * 64;
     g.tiles_m = (int)((M + 255) / 256); g.tiles_n = (int)((N + 255) / 256);
     g.a_ext = (uint32_t)(M * K * 2); g.b_ext = (uint32_t)(N * K * 2);
     const double fl = 2.0 * M * N * K;
     struct V { const char* name; float (*fn)(GemmArgs, int); };
     V vs[] = {{"full", run<0>}, {"no-dma", run<1>}, {"no-mfma", run<2>}, {"no-dma,no-mfma", run<3>},
-              {"no-stagger", run<4>}, {"no-dma,no-stagger", run<5>}, {"full(again)", run<0>}};
+              {"no-stagger", run<4>}, {"kslice-inner", run<8>}, {"full(again)", run<0>}};
+    printf("M=%lld N=%lld K=%lld ta=%d tb=%d ksplit=%d\n", (long long)M, (long long)N, (long long)K, g_ta, g_tb, ksplit);
     for (auto& v : vs) {
         float ms = v.fn(g, 20);
         printf("%-22s %8.3f ms  %7.1f TFLOP/s\n", v.name, ms, fl / ms / 1e9);

@@ -55,8 +55,14 @@ def main():
     scale = d ** -0.5
     out, lse = attention.relattn_fwd(qkv, R, B, S, H, 128, scale)
     flops_att = 3 * d * S * (S + 1) * B  # causal-useful QK^T, q.R^T, PV
+    os.environ["MSQ_ATTN_FWD_V1"] = "1"
     ms = timeit(lambda: attention.relattn_fwd(qkv, R, B, S, H, 128, scale, out=out, lse=lse))
-    rows.append(("attn fwd", ms, flops_att / ms / 1e9))
+    rows.append(("attn fwd v1", ms, flops_att / ms / 1e9))
+    o1 = out.clone()
+    del os.environ["MSQ_ATTN_FWD_V1"]
+    ms = timeit(lambda: attention.relattn_fwd(qkv, R, B, S, H, 128, scale, out=out, lse=lse))
+    rows.append(("attn fwd v2", ms, flops_att / ms / 1e9))
+    print("fwd v2 vs v1 max abs diff", (out.float() - o1.float()).abs().max().item(), flush=True)
     dout = torch.randn(M, d, device=dev).to(bf)
     dqkv = torch.empty_like(qkv)
     dR = torch.zeros(H, S, 128, device=dev)
