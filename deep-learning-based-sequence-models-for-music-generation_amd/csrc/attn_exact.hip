@@ -219,7 +219,13 @@ extern "C" int msq_relattn_fwd(int dtype, void* out, int64_t ld_out, float* lse,
         exact_fwd(a, (float*)out, ld_out, lse, s);
     } else {
         MSQ_CHECK_ARG(hs == 128 && ld_qkv % 8 == 0 && ld_out % 4 == 0, "msq_relattn_fwd: bf16 path needs hs == 128");
-        if (getenv("MSQ_ATTN_FWD_V1") || flash_fwd2(a, (bf16*)out, ld_out, lse, s)) flash_fwd(a, (bf16*)out, ld_out, lse, s);
+        // MSQ_ATTN_FWD=1|2|3 selects a kernel generation for A/B runs (default 3)
+        const char* v = getenv("MSQ_ATTN_FWD");
+        const int ver = v ? atoi(v) : 3;
+        int rc = -1;
+        if (ver >= 3) rc = flash_fwd3(a, (bf16*)out, ld_out, lse, s);
+        if (rc && ver >= 2) rc = flash_fwd2(a, (bf16*)out, ld_out, lse, s);
+        if (rc) flash_fwd(a, (bf16*)out, ld_out, lse, s);
     }
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;

@@ -22,6 +22,7 @@
 //   GEMM: dq = dQR . R + dq_ac (batched over heads);  dR += dQR^T . Q;
 //   fix : meta-block terms (j > i inside the metadata prefix).
 #include "attn_tiles.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -490,9 +491,13 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     hipMemsetAsync(dqr, 0, (size_t)H * B * S * ldr * 2, s);
     hipMemsetAsync(meta_ds, 0, (size_t)B * H * 64 * 4, s);
     hipLaunchKernelGGL(flash_bwd_pre_kernel, dim3((unsigned)((B * S * H + 3) / 4)), dim3(256), 0, s, a, dout, ldo, out, Dv);
-    const unsigned nkb = (unsigned)((S + A_KB - 1) / A_KB);
-    hipLaunchKernelGGL(flash_bwd_a_kernel, dim3(nkb, (unsigned)H, (unsigned)B), dim3(NT), 0, s, a, lse, Dv, dout, ldo,
-                       dqkv, ldd, dqr, ldr, meta_ds);
+    // MSQ_ATTN_BWD=1 selects the first-generation key/value pass (A/B runs)
+    const char* bv = getenv("MSQ_ATTN_BWD");
+    if ((bv && atoi(bv) == 1) || flash_bwd_kv3(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, ldr, meta_ds, s)) {
+        const unsigned nkb = (unsigned)((S + A_KB - 1) / A_KB);
+        hipLaunchKernelGGL(flash_bwd_a_kernel, dim3(nkb, (unsigned)H, (unsigned)B), dim3(NT), 0, s, a, lse, Dv, dout,
+                           ldo, dqkv, ldd, dqr, ldr, meta_ds);
+    }
     const unsigned nqb = (unsigned)((S + B_QB - 1) / B_QB);
     hipLaunchKernelGGL(flash_bwd_b_kernel, dim3(nqb, (unsigned)H, (unsigned)B), dim3(NT), 0, s, a, dqr, ldr, dq_ac,
                        H * HS);

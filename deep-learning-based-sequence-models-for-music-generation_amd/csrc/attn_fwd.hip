@@ -52,6 +52,9 @@ __device__ __forceinline__ void bar() {
     asm volatile("" ::: "memory");
 }
 
+// LAB: ablation switches for tools/lab/attn_lab.hip only (0 in the library):
+// 1 no K.Q^T MFMA, 2 no QR MFMA, 4 no skew / softmax, 8 no PV MFMA, 16 no DMA in the loop
+template <int LAB = 0>
 __global__ __launch_bounds__(NT, 1) void flash_fwd2_kernel(AttnArgs a, bf16* __restrict__ out, int64_t ldo,
                                                            float* __restrict__ lse) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -146,7 +149,7 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd2_kernel(AttnArgs a, bf16* __r
     for (int kt = 0; kt < nkt; ++kt) {
         const int64_t j0 = (int64_t)kt * KB;
         const int cur = kt & 1;
-        if (kt + 1 < nkt) {  // prefetch tile kt+1 (its buffers were released by the barrier ending tile kt-1)
+        if (kt + 1 < nkt && !(LAB & 16)) {  // prefetch tile kt+1 (its buffers were released by the barrier ending tile kt-1)
             const int64_t j1 = j0 + KB;
             const int j1i = (int)j1, rc = rb0i + (kt + 3) * KB;
             dma64(rq, sK + (cur ^ 1) * KB * 256, offK, lrow, (uint32_t)j1i * ldq2, 16 * ldq2, 0, Si32 - j1i, w);
@@ -170,8 +173,12 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd2_kernel(AttnArgs a, bf16* __r
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
                 const bf16x8 kfr = *(const bf16x8*)(cK + nt * 4096 + fro[ks]);
-                sacc[0][nt] = mfma(kfr, qf[0][ks], sacc[0][nt]);
-                sacc[1][nt] = mfma(kfr, qf[1][ks], sacc[1][nt]);
+                if (LAB & 1) {
+                    asm volatile("" ::"v"(kfr));
+                } else {
+                    sacc[0][nt] = mfma(kfr, qf[0][ks], sacc[0][nt]);
+                    sacc[1][nt] = mfma(kfr, qf[1][ks], sacc[1][nt]);
+                }
             }
         }
         // QR^T[window row][query]: union window of the wave starts at block
@@ -186,8 +193,12 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd2_kernel(AttnArgs a, bf16* __r
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
                 const bf16x8 rfr = *(const bf16x8*)(sR + rowb * 256 + fro[ks]);
-                if (t >= 1) qacc[0][t - 1] = mfma(rfr, qf[0][ks], qacc[0][t - 1]);
-                if (t <= 4) qacc[1][t] = mfma(rfr, qf[1][ks], qacc[1][t]);
+                if (LAB & 2) {
+                    asm volatile("" ::"v"(rfr));
+                } else {
+                    if (t >= 1) qacc[0][t - 1] = mfma(rfr, qf[0][ks], qacc[0][t - 1]);
+                    if (t <= 4) qacc[1][t] = mfma(rfr, qf[1][ks], qacc[1][t]);
+                }
             }
         }
 
@@ -196,6 +207,15 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd2_kernel(AttnArgs a, bf16* __r
         bf16x8 pf[2][2];
 #pragma unroll
         for (int q2 = 0; q2 < 2; ++q2) {
+            if (LAB & 4) {
+                float x = 0.f;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) x += sacc[q2][t][0] + qacc[q2][t][1];
+                pf[q2][0] = pf[q2][1] = (bf16x8){(bf16)x, (bf16)x, (bf16)x, (bf16)x, (bf16)x, (bf16)x, (bf16)x, (bf16)x};
+                l_part[q2] += 1.f;
+                m_run[q2] = 0.f;
+                continue;
+            }
             const int iq = iwi + 16 * q2 + il;
             const int jt = (int)j0;
 #pragma unroll
@@ -264,8 +284,12 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd2_kernel(AttnArgs a, bf16* __r
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 const bf16x8 vfr = cat8(tr_read(cV, ks * 8192 + vqo[n]), tr_read(cV, ks * 8192 + 4096 + vqo[n]));
-                oacc[0][n] = mfma(vfr, pf[0][ks], oacc[0][n]);
-                oacc[1][n] = mfma(vfr, pf[1][ks], oacc[1][n]);
+                if (LAB & 8) {
+                    asm volatile("" ::"v"(vfr), "v"(pf[0][ks]), "v"(pf[1][ks]));
+                } else {
+                    oacc[0][n] = mfma(vfr, pf[0][ks], oacc[0][n]);
+                    oacc[1][n] = mfma(vfr, pf[1][ks], oacc[1][n]);
+                }
             }
         }
         bar();  // tile kt's K / V / oldest R chunk may now be overwritten
@@ -291,12 +315,12 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd2_kernel(AttnArgs a, bf16* __r
 int flash_fwd2(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)flash_fwd2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)flash_fwd2_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   LDS_BYTES);
         attr = true;
     }
     if (a.S * a.ldq * 2 >= (int64_t)OOB || a.S * HS * 2 >= (int64_t)OOB || a.n_meta > 8) return -1;
     const dim3 grid((unsigned)((a.S + QB - 1) / QB), (unsigned)a.H, (unsigned)a.B);
-    hipLaunchKernelGGL(flash_fwd2_kernel, grid, dim3(NT), LDS_BYTES, s, a, out, ldo, lse);
+    hipLaunchKernelGGL(flash_fwd2_kernel<0>, grid, dim3(NT), LDS_BYTES, s, a, out, ldo, lse);
     return 0;
 }

@@ -135,7 +135,8 @@ def test_bf16_path_against_oracle():
     for k, g in gd.items():
         g = g.cpu().double().reshape(-1)
         if k in ("ln_f.bias", "lm_head.bias"):
-            assert g.abs().max().item() < 1e-3 * gmax, k
+            # analytically zero; bf16 dlogits summed over B*T rows leave ~1e-3 noise
+            assert g.abs().max().item() < 5e-3 * gmax, k
             continue
         r = pr[k].grad.double().reshape(-1)
         nr = ((g - r).norm() / r.norm()).item()

@@ -55,20 +55,32 @@ def main():
     scale = d ** -0.5
     out, lse = attention.relattn_fwd(qkv, R, B, S, H, 128, scale)
     flops_att = 3 * d * S * (S + 1) * B  # causal-useful QK^T, q.R^T, PV
-    os.environ["MSQ_ATTN_FWD_V1"] = "1"
-    ms = timeit(lambda: attention.relattn_fwd(qkv, R, B, S, H, 128, scale, out=out, lse=lse))
-    rows.append(("attn fwd v1", ms, flops_att / ms / 1e9))
-    o1 = out.clone()
-    del os.environ["MSQ_ATTN_FWD_V1"]
-    ms = timeit(lambda: attention.relattn_fwd(qkv, R, B, S, H, 128, scale, out=out, lse=lse))
-    rows.append(("attn fwd v2", ms, flops_att / ms / 1e9))
-    print("fwd v2 vs v1 max abs diff", (out.float() - o1.float()).abs().max().item(), flush=True)
+    outs = {}
+    for ver in ("1", "2", "3"):
+        os.environ["MSQ_ATTN_FWD"] = ver
+        ms = timeit(lambda: attention.relattn_fwd(qkv, R, B, S, H, 128, scale, out=out, lse=lse))
+        rows.append((f"attn fwd v{ver}", ms, flops_att / ms / 1e9))
+        outs[ver] = (out.clone(), lse.clone())
+    del os.environ["MSQ_ATTN_FWD"]
+    for ver in ("2", "3"):
+        print(f"fwd v{ver} vs v1 max abs diff out", (outs[ver][0].float() - outs["1"][0].float()).abs().max().item(),
+              "lse", (outs[ver][1] - outs["1"][1]).abs().max().item(), flush=True)
     dout = torch.randn(M, d, device=dev).to(bf)
     dqkv = torch.empty_like(qkv)
     dR = torch.zeros(H, S, 128, device=dev)
-    ms = timeit(lambda: attention.relattn_bwd(dout, out, lse, qkv, R, B, S, H, 128, scale, dqkv=dqkv, dR=dR), iters=3,
-                warm=1)
-    rows.append(("attn bwd", ms, 2 * flops_att / ms / 1e9))
+    res = {}
+    for ver in ("1", "3"):
+        os.environ["MSQ_ATTN_BWD"] = ver
+        dR.zero_()
+        ms = timeit(lambda: attention.relattn_bwd(dout, out, lse, qkv, R, B, S, H, 128, scale, dqkv=dqkv, dR=dR),
+                    iters=3, warm=1)
+        rows.append((f"attn bwd v{ver}", ms, 2 * flops_att / ms / 1e9))
+        dR.zero_()
+        attention.relattn_bwd(dout, out, lse, qkv, R, B, S, H, 128, scale, dqkv=dqkv, dR=dR)
+        res[ver] = (dqkv.clone(), dR.clone())
+    del os.environ["MSQ_ATTN_BWD"]
+    print("bwd v3 vs v1: dqkv max diff", (res["3"][0].float() - res["1"][0].float()).abs().max().item(),
+          "dR rel", ((res["3"][1] - res["1"][1]).norm() / res["1"][1].norm()).item(), flush=True)
     for n, ms, tf in rows:
         print(f"{n:32s} {ms:9.3f} ms  {tf:8.1f} TFLOP/s")
 
