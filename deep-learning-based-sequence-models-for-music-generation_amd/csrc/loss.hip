@@ -11,6 +11,7 @@
 // registers; the column sums of W*dZ are accumulated in registers over the 32
 // rows and flushed with one atomic per column), and an elementwise finisher.
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -233,6 +234,252 @@ __global__ void mean_kernel(const float* __restrict__ x, int64_t n, float* __res
     if (threadIdx.x == 0) *out = s / (float)n;
 }
 
+// ---- streaming CE path (train step): three passes over the logits, each
+// one coalesced 16-B-per-lane read (+ one write in pass 3):
+//   colstats2  per (b, v) online max / sum over a time split       (read o)
+//   rowstats2  per row: logsumexp_v Z, loss, and colsum_t(W dZ)     (read o)
+//   finish2    dO = -W dZ + softmax_t(o) colsum_t(W dZ)             (read o, write dO)
+// W rows come from the L2-resident 5 x V table; col_lse and colsum of a
+// thread's columns stay in registers across rows. VEC columns per thread
+// (8 bf16 / 4 fp32 = 16 B).
+template <typename T> struct VecOf { static constexpr int N = 16 / sizeof(T); };
+
+// 16-B aligned vector load / store of N = 16/sizeof(T) elements (callers keep
+// every access inside a padded row)
+template <typename T, int N>
+__device__ __forceinline__ void ldv(const T* p, float (&x)[N]) {
+    if constexpr (sizeof(T) == 2) {
+        const bf16x8 u = *(const bf16x8*)p;
+#pragma unroll
+        for (int i = 0; i < N; ++i) x[i] = (float)u[i];
+    } else {
+        const f32x4 u = *(const f32x4*)p;
+#pragma unroll
+        for (int i = 0; i < N; ++i) x[i] = u[i];
+    }
+}
+template <int N>
+__device__ __forceinline__ void ldf(const float* p, float (&x)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; i += 4) {
+        const f32x4 u = *(const f32x4*)(p + i);
+        x[i] = u[0], x[i + 1] = u[1], x[i + 2] = u[2], x[i + 3] = u[3];
+    }
+}
+template <typename T, int N>
+__device__ __forceinline__ void stv(T* p, const float (&x)[N]) {
+    if constexpr (sizeof(T) == 2) {
+        bf16x8 u;
+#pragma unroll
+        for (int i = 0; i < N; ++i) u[i] = (bf16)x[i];
+        *(bf16x8*)p = u;
+    } else {
+        *(f32x4*)p = (f32x4){x[0], x[1], x[2], x[3]};
+    }
+}
+__device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+
+constexpr int TS2 = 32;    // time splits of colstats2 / finish2
+constexpr int ROWS2 = 64;  // rows per workgroup of rowstats2
+constexpr int NT2 = 512;   // rowstats2: 8 waves, a whole row of V columns in registers
+
+// Padded layouts (Vp = V rounded up to 16): col_lse copy, colsum and the 5-row
+// weight table live in the workspace with zero pads, so every 16-B access is
+// in bounds and unconditional; only the last column chunk masks v >= V.
+__global__ void pad_table_kernel(const float* __restrict__ src, float* __restrict__ dst, int64_t rows, int64_t V,
+                                 int64_t Vp) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= rows * Vp) return;
+    const int64_t r = e / Vp, v = e % Vp;
+    dst[e] = v < V ? src[r * V + v] : 0.f;
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void colstats2_kernel(LossArgs a, float* __restrict__ part) {
+    constexpr int N = VecOf<T>::N;
+    const int v = (blockIdx.x * NT + threadIdx.x) * N;
+    const int64_t b = blockIdx.y, ts = blockIdx.z;
+    const int64_t per = (a.T + TS2 - 1) / TS2;
+    const int64_t t0 = ts * per, t1 = min(a.T, t0 + per);
+    if (v >= a.V) return;
+    const T* o = (const T*)a.o + b * a.T * a.ld + v;
+    float m[N], s[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) m[i] = -INFINITY, s[i] = 0.f;
+    for (int64_t t = t0; t < t1; ++t) {
+        float x[N];
+        ldv<T, N>(o + t * a.ld, x);
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const float mn = fmaxf(m[i], x[i]);
+            s[i] = s[i] * fexp(m[i] - mn) + fexp(x[i] - mn);
+            m[i] = mn;
+        }
+    }
+    float* pm = part + ((b * TS2 + ts) * 2) * a.V;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (v + i < a.V) {
+            pm[v + i] = m[i];
+            pm[a.V + v + i] = s[i];
+        }
+}
+
+__global__ void colstats2_merge_kernel(LossArgs a, const float* __restrict__ part, float* __restrict__ col_lse,
+                                       float* __restrict__ clp, int64_t Vp) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= a.B * Vp) return;
+    const int64_t b = e / Vp, v = e % Vp;
+    if (v >= a.V) {
+        clp[e] = 0.f;
+        return;
+    }
+    float m = -INFINITY;
+    for (int ts = 0; ts < TS2; ++ts) m = fmaxf(m, part[((b * TS2 + ts) * 2) * a.V + v]);
+    float s = 0.f;
+    for (int ts = 0; ts < TS2; ++ts) {
+        const float pm = part[((b * TS2 + ts) * 2) * a.V + v];
+        if (pm != -INFINITY) s += part[((b * TS2 + ts) * 2 + 1) * a.V + v] * expf(pm - m);
+    }
+    const float l = m + logf(s);
+    col_lse[b * a.V + v] = l;
+    clp[e] = l;
+}
+
+__device__ __forceinline__ float block8_max(float v, float* red) {
+    v = wave_max(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    float r = red[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) r = fmaxf(r, red[i]);
+    return r;
+}
+__device__ __forceinline__ float block8_sum(float v, float* red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return ((red[0] + red[1]) + (red[2] + red[3])) + ((red[4] + red[5]) + (red[6] + red[7]));
+}
+
+// NC = column chunks of NT2*N: chunks 0..NC-2 are full for every thread
+template <typename T, int NC>
+__global__ __launch_bounds__(NT2) void rowstats2_kernel(LossArgs a, const float* __restrict__ clp,
+                                                        const float* __restrict__ wtp, int Vp,
+                                                        float* __restrict__ loss_rows, float* __restrict__ row_lse,
+                                                        float* __restrict__ colsum, float gs) {
+    constexpr int N = VecOf<T>::N, CH = NT2 * N;
+    __shared__ float red[8];
+    const int blocks_per_b = (int)((a.T + ROWS2 - 1) / ROWS2);
+    const int b = blockIdx.x / blocks_per_b;
+    const int r0 = (blockIdx.x % blocks_per_b) * ROWS2, r1 = min((int)a.T, r0 + ROWS2);
+    const int tid = threadIdx.x, V = (int)a.V;
+    const int v0 = tid * N;
+    const bool last_ok = v0 + (NC - 1) * CH < V;  // this thread's part of the last chunk
+    float cl[NC][N], cs[NC][N];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) cs[c][i] = 0.f, cl[c][i] = 0.f;
+        if (c < NC - 1 || last_ok) ldf<N>(clp + (int64_t)b * Vp + v0 + c * CH, cl[c]);
+    }
+    for (int t = r0; t < r1; ++t) {
+        const int64_t row = (int64_t)b * a.T + t;
+        const T* o = (const T*)a.o + row * a.ld + v0;
+        const float* w = wtp + (int64_t)bucket_of(a, a.src[row]) * Vp + v0;
+        const int y = (int)a.trg[row];
+        float z[NC][N];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (c < NC - 1 || last_ok) {
+                float ov[N], wv[N];
+                ldv<T, N>(o + c * CH, ov);
+                ldf<N>(w + c * CH, wv);
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    const bool in = c < NC - 1 || v0 + c * CH + i < V;
+                    z[c][i] = in ? -(ov[i] - cl[c][i]) * wv[i] : -INFINITY;
+                    mx = fmaxf(mx, z[c][i]);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < N; ++i) z[c][i] = -INFINITY;
+            }
+        }
+        mx = block8_max(mx, red);
+        float se = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int i = 0; i < N; ++i) se += fexp(z[c][i] - mx);
+        const float lse = mx + logf(block8_sum(se, red));
+        if (tid == 0) {
+            const float zy = -((float)((const T*)a.o)[row * a.ld + y] - clp[(int64_t)b * Vp + y]) *
+                             wtp[(int64_t)bucket_of(a, a.src[row]) * Vp + y];
+            loss_rows[row] = lse - zy;
+            row_lse[row] = lse;
+        }
+        // colsum_t(W dZ), dZ = (softmax_v Z - onehot y) gs   (pads: W = 0)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (c < NC - 1 || last_ok) {
+                float wv[N];
+                ldf<N>(w + c * CH, wv);
+                const int vb = v0 + c * CH;
+#pragma unroll
+                for (int i = 0; i < N; ++i) cs[c][i] += wv[i] * (fexp(z[c][i] - lse) - (vb + i == y ? 1.f : 0.f)) * gs;
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int vb = v0 + c * CH;
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (vb + i < V) atomicAdd(colsum + (int64_t)b * Vp + vb + i, cs[c][i]);
+    }
+}
+
+template <typename T, typename TD>
+__global__ __launch_bounds__(NT) void finish2_kernel(LossArgs a, const float* __restrict__ clp,
+                                                     const float* __restrict__ wtp, int Vp,
+                                                     const float* __restrict__ row_lse,
+                                                     const float* __restrict__ colsum, TD* __restrict__ dout,
+                                                     int64_t ldd, float gs) {
+    constexpr int N = VecOf<T>::N;
+    const int v = (blockIdx.x * NT + threadIdx.x) * N;
+    const int64_t b = blockIdx.y, ts = blockIdx.z;
+    const int64_t per = (a.T + TS2 - 1) / TS2;
+    const int64_t t0 = ts * per, t1 = min(a.T, t0 + per);
+    if (v >= a.V) return;
+    float cl[N], cs[N], wt[5][N];
+    ldf<N>(clp + b * Vp + v, cl);
+    ldf<N>(colsum + b * Vp + v, cs);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) ldf<N>(wtp + (int64_t)k * Vp + v, wt[k]);
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t row = b * a.T + t;
+        const int bk = bucket_of(a, a.src[row]);
+        const int y = (int)a.trg[row];
+        const float lse = row_lse[row];
+        float ov[N], d[N];
+        ldv<T, N>((const T*)a.o + row * a.ld + v, ov);
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const float wv = bk == 0 ? wt[0][i] : bk == 1 ? wt[1][i] : bk == 2 ? wt[2][i] : bk == 3 ? wt[3][i] : wt[4][i];
+            const float oc = ov[i] - cl[i];
+            const float dz = (fexp(-oc * wv - lse) - (v + i == y ? 1.f : 0.f)) * gs;
+            d[i] = (v + i < a.V) ? -wv * dz + fexp(oc) * cs[i] : 0.f;  // pad columns stay 0
+        }
+        stv<TD, N>(dout + row * ldd + v, d);
+    }
+}
+
 LossArgs mk(const void* o, int64_t ld, const int64_t* src, const int64_t* trg, const float* wtab, int64_t b0,
             int64_t b1, int64_t b2, int64_t b3, int64_t B, int64_t T, int64_t V) {
     LossArgs a;
@@ -255,7 +502,10 @@ void colstats_launch(const LossArgs& a, float* col_lse, float* part, hipStream_t
 extern "C" size_t msq_filtered_workspace(int64_t B, int64_t T, int64_t V) {
     // colstats partials | colsum [B,V] | loss rows [B*T]
     (void)T;
-    return (size_t)B * TSPLIT * 2 * V * 4 + (size_t)B * V * 4 + (size_t)B * T * 4 + 256;
+    // | row_lse [B*T] | colstats2 partials [B][TS2][2][V] | clp, colsum [B][Vp] | wtab [5][Vp]
+    const size_t Vp = (V + 15) / 16 * 16;
+    return (size_t)B * TSPLIT * 2 * V * 4 + (size_t)B * V * 4 + (size_t)B * T * 4 * 2 + 256 +
+           (size_t)B * 32 * 2 * V * 4 + (2 * (size_t)B + 5) * Vp * 4 + 256;
 }
 
 #define LOSS_CHECK()                                                                                  \
@@ -285,13 +535,63 @@ extern "C" int msq_filtered_ce(float* loss, void* dlogits, int64_t ldd, const vo
     float* part = (float*)ws;
     float* colsum = (float*)(ws + (size_t)B * TSPLIT * 2 * V * 4);
     float* rows = colsum + B * V;
+    float* part2 = (float*)(ws + (size_t)B * TSPLIT * 2 * V * 4 + (size_t)B * V * 4 + (size_t)B * T * 4 * 2 + 256);
     const bool bfl = dtype == MSQ_BF16;
-    if (bfl) colstats_launch<bf16>(a, col_lse, part, s);
-    else colstats_launch<float>(a, col_lse, part, s);
+    const bool stream2 = dlogits && ld % 8 == 0 && ldd % 8 == 0 && ((uintptr_t)logits % 16) == 0 &&
+                         ((uintptr_t)dlogits % 16) == 0 &&
+                         (V + (bfl ? 4095 : 2047)) / (bfl ? 4096 : 2048) <= (bfl ? 5 : 9) && !getenv("MSQ_CE_V1");
+    if (!stream2) {
+        if (bfl) colstats_launch<bf16>(a, col_lse, part, s);
+        else colstats_launch<float>(a, col_lse, part, s);
+    }
     const unsigned nblk = (unsigned)(B * ((T + ROWS - 1) / ROWS));
     if (!dlogits) {
         if (bfl) hipLaunchKernelGGL((row_kernel<0, bf16, float>), dim3(nblk), dim3(NT), 0, s, a, col_lse, rows, (float*)nullptr, 0, nullptr, 0, nullptr, 0.f, 0);
         else hipLaunchKernelGGL((row_kernel<0, float, float>), dim3(nblk), dim3(NT), 0, s, a, col_lse, rows, (float*)nullptr, 0, nullptr, 0, nullptr, 0.f, 0);
+    } else if (stream2) {
+        // streaming path: colstats2 -> rowstats2 -> finish2 on zero-padded copies
+        const int64_t Vp = (V + 15) / 16 * 16;
+        float* clp = part2 + (size_t)B * TS2 * 2 * V;
+        float* csp = clp + B * Vp;
+        float* wtp = csp + B * Vp;
+        float* row_lse = rows + B * T;
+        hipMemsetAsync(csp, 0, (size_t)B * Vp * 4, s);
+        hipLaunchKernelGGL(pad_table_kernel, dim3((unsigned)((5 * Vp + 255) / 256)), dim3(256), 0, s, wtab, wtp,
+                           (int64_t)5, V, Vp);
+        const int N = bfl ? 8 : 4;
+        const dim3 gc((unsigned)((V + NT * N - 1) / (NT * N)), (unsigned)B, TS2);
+        const unsigned nb2 = (unsigned)(B * ((T + ROWS2 - 1) / ROWS2));
+        const int nc = (int)((V + NT2 * N - 1) / (NT2 * N));
+        const dim3 gm((unsigned)((B * Vp + 255) / 256));
+#define ROWSTATS(TT, NCV) hipLaunchKernelGGL((rowstats2_kernel<TT, NCV>), dim3(nb2), dim3(NT2), 0, s, a, clp, wtp, (int)Vp, rows, row_lse, csp, grad_scale)
+        if (bfl) {
+            hipLaunchKernelGGL(colstats2_kernel<bf16>, gc, dim3(NT), 0, s, a, part2);
+            hipLaunchKernelGGL(colstats2_merge_kernel, gm, dim3(256), 0, s, a, part2, col_lse, clp, Vp);
+            switch (nc) {
+                case 1: ROWSTATS(bf16, 1); break;
+                case 2: ROWSTATS(bf16, 2); break;
+                case 3: ROWSTATS(bf16, 3); break;
+                case 4: ROWSTATS(bf16, 4); break;
+                default: ROWSTATS(bf16, 5); break;
+            }
+            hipLaunchKernelGGL((finish2_kernel<bf16, bf16>), gc, dim3(NT), 0, s, a, clp, wtp, (int)Vp, row_lse, csp, (bf16*)dlogits, ldd, grad_scale);
+        } else {
+            hipLaunchKernelGGL(colstats2_kernel<float>, gc, dim3(NT), 0, s, a, part2);
+            hipLaunchKernelGGL(colstats2_merge_kernel, gm, dim3(256), 0, s, a, part2, col_lse, clp, Vp);
+            switch (nc) {
+                case 1: ROWSTATS(float, 1); break;
+                case 2: ROWSTATS(float, 2); break;
+                case 3: ROWSTATS(float, 3); break;
+                case 4: ROWSTATS(float, 4); break;
+                case 5: ROWSTATS(float, 5); break;
+                case 6: ROWSTATS(float, 6); break;
+                case 7: ROWSTATS(float, 7); break;
+                case 8: ROWSTATS(float, 8); break;
+                default: ROWSTATS(float, 9); break;
+            }
+            hipLaunchKernelGGL((finish2_kernel<float, float>), gc, dim3(NT), 0, s, a, clp, wtp, (int)Vp, row_lse, csp, (float*)dlogits, ldd, grad_scale);
+        }
+#undef ROWSTATS
     } else {
         hipMemsetAsync(colsum, 0, (size_t)B * V * 4, s);
         const unsigned gf = (unsigned)std::min<int64_t>(B * T * ((V + 3) / 4) / 256 + 1, 16384);
