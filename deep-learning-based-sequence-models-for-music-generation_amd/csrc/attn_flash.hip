@@ -22,6 +22,7 @@
 //   GEMM: dq = dQR . R + dq_ac (batched over heads);  dR += dQR^T . Q;
 //   fix : meta-block terms (j > i inside the metadata prefix).
 #include "attn_tiles.h"
+#include "gemm.h"
 #include <stdlib.h>
 
 namespace {
@@ -454,6 +455,22 @@ __global__ void flash_bwd_meta_kernel(AttnArgs a, const float* __restrict__ meta
 
 }  // namespace
 
+namespace {
+// zero the part of dQR[h][b][i][r] that the consumers read but pass A does not
+// write: r in [S-1-i-DQR_BAND, S-1-i) (below the written band) and the row pad
+// [S, ldr). pass B and the triangular GEMMs never read further below the band.
+constexpr int DQR_BAND = 256;
+__global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, int64_t ldr, int64_t S, int64_t rows) {
+    const int64_t row = blockIdx.x * 4LL + (threadIdx.x >> 6);  // (h, b, i) flattened
+    if (row >= rows) return;
+    const int64_t i = row % S;
+    bf16* p = dqr + row * ldr;
+    const int64_t lo = max<int64_t>(0, S - 1 - i - DQR_BAND), hi = S - 1 - i;
+    for (int64_t r = lo + (threadIdx.x & 63); r < hi; r += 64) p[r] = (bf16)0.f;
+    for (int64_t r = S + (threadIdx.x & 63); r < ldr; r += 64) p[r] = (bf16)0.f;
+}
+}  // namespace
+
 int64_t flash_dqr_ld(int64_t S) { return (S + 7) / 8 * 8; }
 
 // workspace: dQR bf16 [H][B][S][ldr] | D f32 [B][H][S] | meta_ds f32 [B][H][8][8] | dq_ac f32 [B*S][H*HS]
@@ -488,7 +505,8 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     p += align256((size_t)B * H * 64 * 4);
     float* dq_ac = (float*)p;
 
-    hipMemsetAsync(dqr, 0, (size_t)H * B * S * ldr * 2, s);
+    hipLaunchKernelGGL(dqr_band_zero_kernel, dim3((unsigned)((H * B * S + 3) / 4)), dim3(256), 0, s, dqr, ldr, S,
+                       H * B * S);
     hipMemsetAsync(meta_ds, 0, (size_t)B * H * 64 * 4, s);
     hipLaunchKernelGGL(flash_bwd_pre_kernel, dim3((unsigned)((B * S * H + 3) / 4)), dim3(256), 0, s, a, dout, ldo, out, Dv);
     // MSQ_ATTN_BWD=1 selects the first-generation key/value pass (A/B runs)
@@ -502,13 +520,15 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     hipLaunchKernelGGL(flash_bwd_b_kernel, dim3(nqb, (unsigned)H, (unsigned)B), dim3(NT), 0, s, a, dqr, ldr, dq_ac,
                        H * HS);
     // dq (bf16, q columns of dqkv) = dQR . R + dq_ac   (batched over heads)
-    int rc = msq_gemm(MSQ_BF16, 0, 1, B * S, HS, S, dqr, ldr, B * S * ldr, a.R, HS, a.S_max * HS, dqkv, MSQ_BF16,
-                      ldd, HS, H, MSQ_EPI_BIAS_RESID, nullptr, dq_ac, MSQ_F32, H * HS, HS, s);
-    if (rc) return rc;
-    // dR[h][r] += sum_{b,i} dQR[h][b,i][r] q_{b,i}   (batched over heads, split-K)
-    rc = msq_gemm(MSQ_BF16, 1, 1, S, HS, B * S, dqr, ldr, B * S * ldr, a.qkv, a.ldq, HS, dR, MSQ_F32, HS,
-                  a.S_max * HS, H, MSQ_EPI_ACCUM, nullptr, nullptr, MSQ_F32, 0, 0, s);
-    if (rc) return rc;
+    // (row i of dQR is nonzero only for r >= S-1-i: triangular K ranges, tri 1)
+    int rc = gemm_bf16_tri(1, S, 0, 1, B * S, HS, S, dqr, ldr, B * S * ldr, a.R, HS, a.S_max * HS, dqkv, MSQ_BF16,
+                           ldd, HS, H, MSQ_EPI_BIAS_RESID, dq_ac, MSQ_F32, H * HS, HS, s);
+    if (rc) return msq_set_error(MSQ_ERR_ARG, "flash_bwd: dq product");
+    // dR[h][r] += sum_{b,i} dQR[h][b,i][r] q_{b,i}   (batched over heads; per batch
+    // segment only i >= S-1-r contributes: tri 2, split over segments)
+    rc = gemm_bf16_tri(2, S, 1, 1, S, HS, B * S, dqr, ldr, B * S * ldr, a.qkv, a.ldq, HS, dR, MSQ_F32, HS,
+                       a.S_max * HS, H, MSQ_EPI_ACCUM, nullptr, MSQ_F32, 0, 0, s);
+    if (rc) return msq_set_error(MSQ_ERR_ARG, "flash_bwd: dR product");
     hipLaunchKernelGGL(flash_bwd_meta_kernel, dim3(1, (unsigned)H, (unsigned)B), dim3(HS), 0, s, a, meta_ds, dqkv, ldd,
                        dR);
     return 0;

@@ -15,6 +15,11 @@ struct GemmArgs {
     int ksplit;  // >1: K range split over blocks, ACCUM epilogue via fp32 atomics
     int64_t kper;
     uint32_t a_ext, b_ext;  // bytes of one batch's A / B extent (256-tile buffer descriptors)
+    // triangular K ranges of the relative-attention products (128 tile only):
+    // 1 = rows m are (segment, i = m % seg) and need k >= seg-1-i (dq = dQR.R);
+    // 2 = K is nseg segments of seg rows, tile rows m = r need k%seg >= seg-1-r (dR)
+    int tri;
+    int64_t seg;
 };
 
 template <typename TC>
@@ -65,3 +70,8 @@ __device__ __forceinline__ void epi_apply(const GemmArgs& g, TC* C, const TX* X,
 // 256x256 kernel family: returns false when the problem does not fit its
 // preconditions (the caller then uses the 128x128 kernel).
 bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s);
+
+// bf16 GEMM with a triangular K range (GemmArgs::tri); same operand conventions as msq_gemm
+int gemm_bf16_tri(int tri, int64_t seg, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                  int64_t sA, const void* B, int64_t ldb, int64_t sB, void* C, int c_dtype, int64_t ldc, int64_t sC,
+                  int64_t batch, int epi, const void* aux, int aux_dtype, int64_t ldx, int64_t sX, hipStream_t s);

@@ -39,31 +39,31 @@ struct Stager {
     // Each thread moves 4 16-B chunks of A and 4 of B per K tile.
     u32x4 ra[4], rb[4];
 
-    __device__ __forceinline__ void load(const GemmArgs& g, const bf16* A, const bf16* B, int m0, int n0, int k0,
-                                         int tid) {
+    __device__ __forceinline__ void load(const GemmArgs& g, const bf16* A, const bf16* B, int m0, int n0, int64_t k0,
+                                         int64_t kend, int tid) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int c = tid + NT * i;
             if (TA == 0) {  // A [M][K]: 128 rows x 8 chunks
                 const int row = c >> 3, ch = c & 7;
                 const int64_t gm = m0 + row, gk = k0 + ch * 8;
-                const int valid = (gm < g.M) ? (int)min<int64_t>(8, g.K - gk) : 0;
+                const int valid = (gm < g.M) ? (int)min<int64_t>(8, kend - gk) : 0;
                 ra[i] = load_chunk(A + gm * g.lda + gk, valid);
             } else {  // A [K][M]: 64 rows x 16 chunks
                 const int kr = c >> 4, ch = c & 15;
                 const int64_t gk = k0 + kr, gm = m0 + ch * 8;
-                const int valid = (gk < g.K) ? (int)min<int64_t>(8, g.M - gm) : 0;
+                const int valid = (gk < kend) ? (int)min<int64_t>(8, g.M - gm) : 0;
                 ra[i] = load_chunk(A + gk * g.lda + gm, valid);
             }
             if (TB == 0) {  // B [N][K]
                 const int row = c >> 3, ch = c & 7;
                 const int64_t gn = n0 + row, gk = k0 + ch * 8;
-                const int valid = (gn < g.N) ? (int)min<int64_t>(8, g.K - gk) : 0;
+                const int valid = (gn < g.N) ? (int)min<int64_t>(8, kend - gk) : 0;
                 rb[i] = load_chunk(B + gn * g.ldb + gk, valid);
             } else {  // B [K][N]
                 const int kr = c >> 4, ch = c & 15;
                 const int64_t gk = k0 + kr, gn = n0 + ch * 8;
-                const int valid = (gk < g.K) ? (int)min<int64_t>(8, g.N - gn) : 0;
+                const int valid = (gk < kend) ? (int)min<int64_t>(8, g.N - gn) : 0;
                 rb[i] = load_chunk(B + gk * g.ldb + gn, valid);
             }
         }
@@ -147,18 +147,42 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
         for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     Stager<TA, TB> st;
-    const int64_t kbeg = (int64_t)kslice * g.kper;
-    const int64_t kend = min<int64_t>(g.K, kbeg + g.kper);
-    const int nk = (int)((kend - kbeg + BK - 1) / BK);
-    st.load(g, A, B, m0, n0, (int)kbeg, tid);
-    st.store(smem, smem + BM * BK * 2, tid);
+    // K range(s) of this block: segments [sg_lo, sg_hi), segment s covers
+    // [kb(s), ke(s)); tri 0 / 1 use a single segment
+    int64_t sg_lo = 0, sg_hi = 1, kb0 = (int64_t)kslice * g.kper, ke0 = min<int64_t>(g.K, kb0 + g.kper), imin = 0;
+    if (g.tri == 1) {
+        const int64_t mlast = min<int64_t>(g.M - 1, (int64_t)m0 + BM - 1);
+        if ((int64_t)m0 / g.seg == mlast / g.seg) kb0 = max<int64_t>(kb0, (g.seg - 1 - mlast % g.seg) / BK * BK);
+    } else if (g.tri == 2) {
+        const int64_t nseg = g.K / g.seg, spb = (nseg + g.ksplit - 1) / g.ksplit;
+        sg_lo = (int64_t)kslice * spb;
+        sg_hi = min<int64_t>(nseg, sg_lo + spb);
+        imin = max<int64_t>(0, g.seg - 1 - ((int64_t)m0 + BM - 1));
+    }
+    auto seg_kb = [&](int64_t sg) { return g.tri == 2 ? sg * g.seg + imin : kb0; };
+    auto seg_ke = [&](int64_t sg) { return g.tri == 2 ? (sg + 1) * g.seg : ke0; };
+    int64_t cs = sg_lo, ck = seg_kb(cs), cke = seg_ke(cs);
+    while (cs < sg_hi && ck >= cke) {
+        ++cs;
+        if (cs < sg_hi) ck = seg_kb(cs), cke = seg_ke(cs);
+    }
+    if (cs < sg_hi) {
+        st.load(g, A, B, m0, n0, ck, cke, tid);
+        st.store(smem, smem + BM * BK * 2, tid);
+    }
     __syncthreads();
 
-    for (int kt = 0; kt < nk; ++kt) {
+    for (int kt = 0; cs < sg_hi; ++kt) {
         const int cur = kt & 1;
         char* sa = smem + cur * STAGE;
         char* sb = sa + BM * BK * 2;
-        if (kt + 1 < nk) st.load(g, A, B, m0, n0, (int)(kbeg + (kt + 1) * BK), tid);
+        ck += BK;
+        while (cs < sg_hi && ck >= cke) {
+            ++cs;
+            if (cs < sg_hi) ck = seg_kb(cs), cke = seg_ke(cs);
+        }
+        const bool more = cs < sg_hi;
+        if (more) st.load(g, A, B, m0, n0, ck, cke, tid);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             bf16x8 af[4], bfr[4];
@@ -172,7 +196,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
                 for (int j = 0; j < 4; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         }
-        if (kt + 1 < nk) st.store(smem + (cur ^ 1) * STAGE, smem + (cur ^ 1) * STAGE + BM * BK * 2, tid);
+        if (more) st.store(smem + (cur ^ 1) * STAGE, smem + (cur ^ 1) * STAGE + BM * BK * 2, tid);
         __syncthreads();
     }
 
@@ -314,6 +338,32 @@ int dispatch_epi(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hipS
 
 }  // namespace
 
+int gemm_bf16_tri(int tri, int64_t seg, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                  int64_t sA, const void* B, int64_t ldb, int64_t sB, void* C, int c_dtype, int64_t ldc, int64_t sC,
+                  int64_t batch, int epi, const void* aux, int aux_dtype, int64_t ldx, int64_t sX, hipStream_t s) {
+    GemmArgs g{};
+    g.M = M; g.N = N; g.K = K;
+    g.A = A; g.lda = lda; g.sA = sA;
+    g.B = B; g.ldb = ldb; g.sB = sB;
+    g.C = C; g.ldc = ldc; g.sC = sC;
+    g.aux = aux; g.ldx = ldx; g.sX = sX;
+    g.tiles_m = (int)((M + BM - 1) / BM);
+    g.tiles_n = (int)((N + BN - 1) / BN);
+    g.batch = (int)batch;
+    g.vec = 0;
+    g.tri = tri;
+    g.seg = seg;
+    g.ksplit = 1;
+    g.kper = ((K + BK - 1) / BK) * BK;
+    if (tri == 2) {  // split the segments so that about 1024 blocks (4 per CU) run
+        const int64_t nb = (int64_t)g.tiles_m * g.tiles_n * batch, nseg = K / seg;
+        g.ksplit = (int)std::max<int64_t>(1, std::min<int64_t>(nseg, (1024 + nb - 1) / nb));
+    }
+    const int rc = c_dtype == MSQ_BF16 ? dispatch_epi<true, bf16>(g, ta, tb, epi, aux_dtype, s)
+                                       : dispatch_epi<true, float>(g, ta, tb, epi, aux_dtype, s);
+    return rc;
+}
+
 extern "C" int msq_gemm(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                         int64_t strideA, const void* B, int64_t ldb, int64_t strideB, void* C, int c_dtype,
                         int64_t ldc, int64_t strideC, int64_t batch, int epilogue, const float* bias,
@@ -332,7 +382,7 @@ extern "C" int msq_gemm(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t
                       "msq_gemm: bf16 path needs lda/ldb (and batch strides) %% 8 == 0");
         MSQ_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "msq_gemm: A/B must be 16-B aligned");
     }
-    GemmArgs g;
+    GemmArgs g{};
     g.M = M; g.N = N; g.K = K;
     g.A = A; g.lda = lda; g.sA = strideA;
     g.B = B; g.ldb = ldb; g.sB = strideB;

@@ -293,6 +293,70 @@ __global__ void colsum_reduce_kernel(float* __restrict__ out, const float* __res
     out[c] = accumulate ? out[c] + s : s;
 }
 
+// streaming variant: 1024-thread workgroups (16 waves) = row groups x column
+// vectors of N = 16/sizeof(T) columns, 8 independent 16-B loads in flight per
+// thread, the row groups folded in LDS, then one fp32 atomic per column per
+// workgroup (about 256 workgroups: few atomics per address).
+template <typename T>
+__global__ __launch_bounds__(1024) void colsum2_kernel(float* __restrict__ out, const T* __restrict__ x, int64_t rows,
+                                                       int64_t cols, int64_t ld, int tpr) {
+    constexpr int N = 16 / sizeof(T), U = 8;
+    __shared__ float red[1024 * 4];
+    const int tid = threadIdx.x, rg = tid / tpr, rgs = 1024 / tpr, ti = tid - rg * tpr;
+    const int64_t c = ((int64_t)blockIdx.x * tpr + ti) * N;
+    const int64_t per = (rows + gridDim.y - 1) / gridDim.y;
+    const int64_t r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+    float s[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) s[i] = 0.f;
+    if (c < cols) {
+        const T* p = x + c;
+        const bool full = c + N <= cols;
+        int64_t r = r0 + rg;
+        if (full) {
+            for (; r + (U - 1) * rgs < r1; r += U * rgs) {
+                float v[U][N];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if constexpr (N == 8) {
+                        const bf16x8 q = *(const bf16x8*)(p + (r + u * rgs) * ld);
+#pragma unroll
+                        for (int i = 0; i < N; ++i) v[u][i] = (float)q[i];
+                    } else {
+                        const f32x4 q = *(const f32x4*)(p + (r + u * rgs) * ld);
+#pragma unroll
+                        for (int i = 0; i < N; ++i) v[u][i] = q[i];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int i = 0; i < N; ++i) s[i] += v[u][i];
+            }
+        }
+        for (; r < r1; r += rgs)
+#pragma unroll
+            for (int i = 0; i < N; ++i)
+                if (c + i < cols) s[i] += (float)p[r * ld + i];
+    }
+    // fold the row groups: red[rg][ti][i] (N <= 8, at most 4 row groups when N == 8)
+    for (int h = 0; h < N; h += 4) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[(rg * tpr + ti) * 4 + i] = h + i < N ? s[h + i] : 0.f;
+        __syncthreads();
+        if (rg == 0 && c < cols) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (h + i >= N || c + h + i >= cols) continue;
+                float t = 0.f;
+                for (int q = 0; q < rgs; ++q) t += red[(q * tpr + ti) * 4 + i];
+                atomicAdd(out + c + h + i, t);
+            }
+        }
+    }
+}
+
 extern "C" size_t msq_colsum_workspace(int64_t rows, int64_t cols) {
     (void)rows;
     return (size_t)CS_SPLIT * cols * sizeof(float);
@@ -302,6 +366,21 @@ extern "C" int msq_colsum(float* out, int accumulate, const void* x, int dtype, 
                           int64_t ld, void* workspace, void* stream) {
     MSQ_CHECK_ARG(rows > 0 && cols > 0 && workspace && ld % 4 == 0, "msq_colsum: bad args (ld %% 4 == 0)");
     hipStream_t s = (hipStream_t)stream;
+    {
+        const int N = dtype == MSQ_BF16 ? 8 : 4;
+        if (ld % N == 0 && ((uintptr_t)x % 16) == 0) {
+            if (!accumulate) hipMemsetAsync(out, 0, (size_t)cols * 4, s);
+            const int64_t cvec = (cols + N - 1) / N;
+            const int tpr = (int)std::min<int64_t>(1024, std::max<int64_t>(64, (cvec + 63) / 64 * 64 > 512 ? 1024 : (cvec + 63) / 64 * 64 > 256 ? 512 : (cvec + 63) / 64 * 64 > 128 ? 256 : (cvec + 63) / 64 * 64 > 64 ? 128 : 64));
+            const int64_t nch = (cvec + tpr - 1) / tpr;
+            const int64_t split = std::max<int64_t>(1, std::min<int64_t>(rows / 64 + 1, 256 / nch + 1));
+            dim3 g2((unsigned)nch, (unsigned)split);
+            if (dtype == MSQ_BF16) hipLaunchKernelGGL(colsum2_kernel<bf16>, g2, dim3(1024), 0, s, out, (const bf16*)x, rows, cols, ld, tpr);
+            else hipLaunchKernelGGL(colsum2_kernel<float>, g2, dim3(1024), 0, s, out, (const float*)x, rows, cols, ld, tpr);
+            MSQ_LAUNCH_CHECK();
+            return MSQ_OK;
+        }
+    }
     const int split = (int)std::min<int64_t>(CS_SPLIT, rows);
     dim3 grid((unsigned)((cols + 1023) / 1024), (unsigned)split);
     if (dtype == MSQ_BF16) hipLaunchKernelGGL(colsum_part_kernel<bf16>, grid, dim3(256), 0, s, (float*)workspace, (const bf16*)x, rows, cols, ld);
