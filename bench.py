@@ -168,6 +168,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--seq", type=int, default=2048)
     ap.add_argument("--layers", type=int, default=8)
+    ap.add_argument("--dropout", type=float, default=0.01, help="configs/common/config.yaml values.dropout")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the decode and Mamba legs")
     args = ap.parse_args()
@@ -175,7 +176,7 @@ def main():
     rank, local, world = setup_distributed()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    cfg = TransformerConfig(n_layer=args.layers, block_len=args.seq, precision="bf16", dropout=0.0)
+    cfg = TransformerConfig(n_layer=args.layers, block_len=args.seq, precision="bf16", dropout=args.dropout)
     model = Transformer(cfg).to(dev)
     step = TrainStep(model)
     data = iter(SyntheticMIDI(args.batch, args.seq, dev, rank))
@@ -243,7 +244,7 @@ def main():
             "dtype": "bf16",
             "data": "synthetic grammar-cycled MIDI tokens, random-init weights",
             "config": {"workload": "configs/transformer default (d=1024, h=8, L=8, V=17914) train step, "
-                                   "filtered CE + Adam, dropout=0",
+                                   f"filtered CE + Adam, dropout={args.dropout}",
                        "model": "Transformer", "global_batch": args.batch * world, "seq_len": args.seq,
                        "parallelism": f"dp{world}"},
             "model_tflops": round(value * fpt / 1e12, 1),

@@ -13,9 +13,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmidiseq.so")
 
 F32, BF16 = 0, 1
-EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_RESID, EPI_RELU_MASK, EPI_ACCUM = range(6)
+EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_RESID, EPI_RELU_MASK, EPI_ACCUM, EPI_BIAS_DROP_RESID = range(7)
 
-_p, _i, _i64, _f, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
+_p, _i, _i64, _f, _sz, _u32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint32
 
 # symbol -> (restype, argtypes); must mirror include/midiseq.h exactly
 SIGNATURES = {
@@ -28,6 +28,16 @@ SIGNATURES = {
     "msq_layernorm_bwd": (_i, [_p, _p, _i, _p, _p, _p, _i, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _p]),
     "msq_gemm": (_i, [_i, _i, _i, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _p, _i, _i64, _i64, _i64, _i,
                       _p, _p, _i, _i64, _i64, _p]),
+    "msq_gemm_dropout": (_i, [_i, _i, _i, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _p, _i, _i64, _i64, _i64,
+                              _i, _p, _p, _i, _i64, _i64, _u32, _u32, _f, _p]),
+    "msq_layernorm_bwd_dropout": (_i, [_p, _p, _i, _p, _p, _p, _i, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _u32, _u32,
+                                       _f, _p, _p]),
+    "msq_dropout_mask_ld": (_i64, [_i64]),
+    "msq_dropout_attn_mask": (_i, [_p, _p, _i64, _i64, _i64, _u32, _u32, _f, _p]),
+    "msq_relattn_fwd_dropout": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64, _p, _p,
+                                     _f, _p]),
+    "msq_relattn_bwd_dropout": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64,
+                                     _f, _i64, _p, _p, _f, _p, _p]),
     "msq_colsum_workspace": (_sz, [_i64, _i64]),
     "msq_colsum": (_i, [_p, _i, _p, _i, _i64, _i64, _i64, _p, _p]),
     "msq_cast": (_i, [_p, _i, _p, _i, _i64, _p]),

@@ -9,19 +9,22 @@ from .ops import workspace
 N_META = 6  # metadata prefix (generate_matrix, model_transformer.py:14)
 
 
-def relattn_fwd(qkv, R, B, S, H, hs, scale, out=None, lse=None, n_meta=N_META):
+def relattn_fwd(qkv, R, B, S, H, hs, scale, out=None, lse=None, n_meta=N_META, drop=None):
     """qkv [B*S, >=3*H*hs] (bf16 -> flash MFMA path, fp32 -> exact path),
-    R [H, S_max, hs]. Returns (out [B*S, H*hs], lse fp32 [B, H, S])."""
+    R [H, S_max, hs]. Returns (out [B*S, H*hs], lse fp32 [B, H, S]).
+    drop=(masks [2, n] from ops.dropout_attn_mask, p): attention-probability dropout."""
     if out is None:
         out = torch.empty(B * S, H * hs, device=qkv.device, dtype=qkv.dtype)
     if lse is None:
         lse = torch.empty(B, H, S, device=qkv.device, dtype=torch.float32)
-    call("msq_relattn_fwd", dt(qkv), ptr(out), out.stride(0), ptr(lse), ptr(qkv), qkv.stride(0), ptr(R), B, S, H, hs,
-         R.shape[1], float(scale), n_meta, stream())
+    masks, p = drop if drop is not None else (None, 0.0)
+    call("msq_relattn_fwd_dropout", dt(qkv), ptr(out), out.stride(0), ptr(lse), ptr(qkv), qkv.stride(0), ptr(R), B,
+         S, H, hs, R.shape[1], float(scale), n_meta, ptr(masks[0]) if masks is not None else None,
+         ptr(masks[1]) if masks is not None else None, float(p), stream())
     return out, lse
 
 
-def relattn_bwd(dout, out, lse, qkv, R, B, S, H, hs, scale, dqkv=None, dR=None, n_meta=N_META):
+def relattn_bwd(dout, out, lse, qkv, R, B, S, H, hs, scale, dqkv=None, dR=None, n_meta=N_META, drop=None):
     """Returns (dqkv [B*S, 3*H*hs] (overwritten), dR fp32 [H, S_max, hs] (accumulated))."""
     if dqkv is None:
         dqkv = torch.empty(B * S, 3 * H * hs, device=qkv.device, dtype=qkv.dtype)
@@ -29,6 +32,9 @@ def relattn_bwd(dout, out, lse, qkv, R, B, S, H, hs, scale, dqkv=None, dR=None, 
         dR = torch.zeros(R.shape, device=qkv.device, dtype=torch.float32)
     nbytes = L.lib().msq_relattn_bwd_workspace(dt(qkv), B, S, H)
     ws = workspace(nbytes, qkv.device, "attn")
-    call("msq_relattn_bwd", dt(qkv), ptr(dqkv), dqkv.stride(0), ptr(dR), ptr(dout), dout.stride(0), ptr(out), ptr(lse),
-         ptr(qkv), qkv.stride(0), ptr(R), B, S, H, hs, R.shape[1], float(scale), n_meta, ptr(ws), stream())
+    masks, p = drop if drop is not None else (None, 0.0)
+    call("msq_relattn_bwd_dropout", dt(qkv), ptr(dqkv), dqkv.stride(0), ptr(dR), ptr(dout), dout.stride(0), ptr(out),
+         ptr(lse), ptr(qkv), qkv.stride(0), ptr(R), B, S, H, hs, R.shape[1], float(scale), n_meta,
+         ptr(masks[0]) if masks is not None else None, ptr(masks[1]) if masks is not None else None, float(p),
+         ptr(ws), stream())
     return dqkv, dR

@@ -7,7 +7,18 @@ struct AttnArgs {
     float scale;
     const void* qkv; int64_t ldq;  // [B*S, ldq]: q | k | v, head h at col h*hs
     const void* R;                 // [H, S_max, hs]
+    // attention-probability dropout (model_transformer.py:80); null = none.
+    // keep bit of (b,h,i,j): rowmask[((b*H+h)*S+i)*mask_ld + j/32] >> (j%32),
+    // the same bit transposed in colmask (dropout.hip); kept p scaled by keep_scale
+    const uint32_t* rowmask = nullptr;
+    const uint32_t* colmask = nullptr;
+    int64_t mask_ld = 0;
+    float keep_scale = 1.f;
 };
+
+__device__ __forceinline__ float keep_bit(const AttnArgs& a, int64_t bh, int64_t i, int64_t j) {
+    return (a.rowmask[(bh * a.S + i) * a.mask_ld + (j >> 5)] >> (j & 31)) & 1u ? a.keep_scale : 0.f;
+}
 
 // exact fp32 path (attn_exact.hip)
 size_t exact_bwd_workspace(int64_t B, int64_t S, int64_t H);

@@ -23,7 +23,8 @@ constexpr int NT = 512;
 constexpr int KB = 128, QT = 32, NCH = 6, SCR = 36;
 constexpr int O_Q = 0, O_O = 2 * QT * 256, O_L = 4 * QT * 256, O_R = O_L + 2 * 2 * 64 * 4;
 constexpr int O_S = O_R + NCH * 32 * 256, O_M = O_S + 8 * 2 * 16 * SCR * 4;
-constexpr int LDS_BYTES = O_M + 64 * 4;
+constexpr int O_D = O_M + 64 * 4;  // dropout keep words of the block's 128 keys, 2 tiles
+constexpr int LDS_BYTES = O_D + 2 * KB * 4;
 constexpr uint32_t OOB = 0xFFFF0000u;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
@@ -47,6 +48,10 @@ __device__ __forceinline__ void bar() {
 // dual image (row reads and transposed quads reads, cdna_hip_programming.md T10 (b))
 __device__ __forceinline__ int sw_dual(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
+// DROP: attention-probability dropout (model_transformer.py:80); the keep word
+// (key, query tile) of colmask is staged with the tile: dV uses P keep/(1-p),
+// dS = P (dP keep/(1-p) - D) scale
+template <bool DROP>
 __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const float* __restrict__ lse,
                                                               const float* __restrict__ Dv,
                                                               const bf16* __restrict__ dout, int64_t ldo,
@@ -128,6 +133,17 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const 
             dma4(w == 0 ? rl : rd, smem + O_L + (buf * 2 + w) * 256, okl ? (uint32_t)((i0 + lane) * 4) : OOB);
         }
     };
+    const int64_t mld = a.mask_ld;
+    const __amdgpu_buffer_rsrc_t rm =
+        make_rsrc(DROP ? (const void*)(a.colmask + (int64_t)(b * H + h) * S * mld) : (const void*)a.R,
+                  DROP ? (uint32_t)(S * mld * 4) : 0u);
+    auto stage_m = [&](int t) {  // keep words colmask[b,h,j][i0/32] of the block's keys (waves 2-3)
+        if (DROP && w >= 2 && w < 4) {
+            const int i0 = it0 + QT * t, key = j0 + 64 * (w - 2) + lane;
+            dma4(rm, smem + O_D + (t & 1) * KB * 4 + (w - 2) * 256,
+                 key < S ? (uint32_t)((key * mld + i0 / 32) * 4) : OOB);
+        }
+    };
     auto stage_r = [&](int c) {  // R chunk c into ring slot c % NCH
         const int r0 = rw0 + 128 - 32 * c, rg = r0 + lrow;
         dma16(rr, sR + (c % NCH) * 32 * 256 + w * 1024,
@@ -149,6 +165,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const 
 
     // prologue: tile 0 and the 5 R chunks of its window
     stage_q(0);
+    stage_m(0);
 #pragma unroll
     for (int c = 0; c < NCH - 1; ++c) stage_r(c);
 
@@ -173,6 +190,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const 
         if (t + 1 < nqt) {
             stage_q(t + 1);
             stage_r(t + NCH - 1);
+            stage_m(t + 1);
         }
         const char* cQ = smem + O_Q + buf * QT * 256;
         const char* cO = smem + O_O + buf * QT * 256;
@@ -184,6 +202,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const 
         bf16x8 pa, da;
         // whole sub-tile below the diagonal and inside the sequence: no mask
         const bool unmasked = (i0 >= jw0 + 15) && (i0 + QT <= S);
+        const uint32_t kw = DROP ? ((const uint32_t*)(smem + O_D + buf * KB * 4))[16 * w + il] >> (4 * g) : 0u;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             f32x4 sacc = zero4(), dpacc = zero4(), qa = zero4(), qb2 = zero4();
@@ -220,16 +239,18 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const 
                 float x = sacc[r] + sc[ir * SCR + il - ir + 15];
                 const float l2 = cL[16 * s + ir] * LOG2E, dd = cD[16 * s + ir];
                 float p, ds;
+                const float kb = DROP ? ((kw >> (16 * s + r)) & 1u ? a.keep_scale : 0.f) : 1.f;
                 if (unmasked) {
                     p = __builtin_amdgcn_exp2f(fmaf(x, c2, -l2));
-                    ds = p * (dpacc[r] - dd) * a.scale;
+                    ds = p * (DROP ? fmaf(dpacc[r], kb, -dd) : dpacc[r] - dd) * a.scale;
                 } else {
                     const bool ok = (i < S) && (jk < S) && (jk <= i || jk < nm);
                     if (ok && jk >= i + 2) x += mbd[i * 8 + jk];
                     p = ok ? __builtin_amdgcn_exp2f(fmaf(x, c2, -l2)) : 0.f;
-                    ds = ok ? p * (dpacc[r] - dd) * a.scale : 0.f;
+                    ds = ok ? p * (DROP ? fmaf(dpacc[r], kb, -dd) : dpacc[r] - dd) * a.scale : 0.f;
                     if (ok && jk > i) meta_ds[(((int64_t)b * H + h) * 8 + i) * 8 + jk] = ds;
                 }
+                if (DROP) p *= kb;
                 pa[4 * s + r] = (bf16)p;
                 da[4 * s + r] = (bf16)ds;
             }
@@ -266,13 +287,20 @@ int flash_bwd_kv3(const AttnArgs& a, const float* lse, const float* Dv, const bf
                   int64_t ldd, bf16* dqr, int64_t ldr, float* meta_ds, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)flash_bwd_kv3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)flash_bwd_kv3_kernel<false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)flash_bwd_kv3_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   LDS_BYTES);
         attr = true;
     }
     if (a.S * a.ldq * 2 >= (int64_t)OOB || a.S * ldo * 2 >= (int64_t)OOB || a.n_meta > 8) return -1;
+    if (a.colmask && a.S * a.mask_ld * 4 >= (int64_t)OOB) return -1;
     const dim3 grid((unsigned)((a.S + KB - 1) / KB), (unsigned)a.H, (unsigned)a.B);
-    hipLaunchKernelGGL(flash_bwd_kv3_kernel, grid, dim3(NT), LDS_BYTES, s, a, lse, Dv, dout, ldo, dqkv, ldd, dqr, ldr,
-                       meta_ds);
+    if (a.colmask)
+        hipLaunchKernelGGL(flash_bwd_kv3_kernel<true>, grid, dim3(NT), LDS_BYTES, s, a, lse, Dv, dout, ldo, dqkv, ldd,
+                           dqr, ldr, meta_ds);
+    else
+        hipLaunchKernelGGL(flash_bwd_kv3_kernel<false>, grid, dim3(NT), LDS_BYTES, s, a, lse, Dv, dout, ldo, dqkv, ldd,
+                           dqr, ldr, meta_ds);
     return 0;
 }

@@ -71,6 +71,10 @@ __global__ __launch_bounds__(NTH) void exact_fwd_kernel(AttnArgs a, float* out, 
     if (threadIdx.x == 0) lse[(b * a.H + h) * a.S + i] = mx + logf(sum);
     __syncthreads();
     const float inv = 1.f / sum;
+    if (a.rowmask) {  // dropout: O = sum_j (p_j keep_j / (1-p)) v_j / sum
+        for (int64_t j = threadIdx.x; j < a.S; j += NTH) srow[j] *= keep_bit(a, b * a.H + h, i, j);
+        __syncthreads();
+    }
     for (int d = threadIdx.x; d < a.hs; d += NTH) {
         float o = 0.f;
         for (int64_t j = 0; j < a.S; ++j) o = fmaf(srow[j], qrow(a, b, h, j, 2)[d], o);
@@ -93,7 +97,10 @@ __global__ __launch_bounds__(NTH) void exact_bwd_row_kernel(AttnArgs a, const fl
     for (int64_t j = threadIdx.x; j < a.S; j += NTH) {
         const float s = score(a, b, h, i, j);
         const float p = s == -INFINITY ? 0.f : expf(s - L);
-        const float dp = dotf(dO, qrow(a, b, h, j, 2), (int)a.hs);
+        float dp = dotf(dO, qrow(a, b, h, j, 2), (int)a.hs);
+        // dropout: P' = P keep/(1-p) feeds dV; dP = dP' keep/(1-p); D = sum P' dP'
+        const float kb = a.rowmask ? keep_bit(a, b * a.H + h, i, j) : 1.f;
+        dp *= kb;
         sp[j] = p;
         sd[j] = dp;
         dsum += p * dp;
@@ -103,7 +110,7 @@ __global__ __launch_bounds__(NTH) void exact_bwd_row_kernel(AttnArgs a, const fl
     for (int64_t j = threadIdx.x; j < a.S; j += NTH) {
         const float ds = sp[j] * (sd[j] - D) * a.scale;
         sd[j] = ds;
-        P[rowoff + j] = sp[j];
+        P[rowoff + j] = a.rowmask ? sp[j] * keep_bit(a, b * a.H + h, i, j) : sp[j];
         dS[rowoff + j] = ds;
     }
     __syncthreads();
@@ -204,28 +211,65 @@ static AttnArgs mk(int64_t B, int64_t S, int64_t H, int64_t hs, int64_t S_max, i
     return a;
 }
 
+static void set_drop(AttnArgs& a, const uint32_t* rowmask, const uint32_t* colmask, float p) {
+    a.rowmask = rowmask;
+    a.colmask = colmask;
+    a.mask_ld = msq_dropout_mask_ld(a.S);
+    a.keep_scale = 1.f / (1.f - p);
+}
+
 extern "C" size_t msq_relattn_bwd_workspace(int dtype, int64_t B, int64_t S, int64_t H) {
     return dtype == MSQ_F32 ? exact_bwd_workspace(B, S, H) : flash_bwd_workspace(B, S, H);
+}
+
+static int relattn_fwd(int dtype, void* out, int64_t ld_out, float* lse, const AttnArgs& a, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == MSQ_F32) {
+        exact_fwd(a, (float*)out, ld_out, lse, s);
+    } else {
+        MSQ_CHECK_ARG(a.hs == 128 && a.ldq % 8 == 0 && ld_out % 4 == 0, "msq_relattn_fwd: bf16 path needs hs == 128");
+        // MSQ_ATTN_FWD=1|2|3 selects a kernel generation for A/B runs (default 3)
+        const char* v = getenv("MSQ_ATTN_FWD");
+        const int ver = a.rowmask ? 3 : (v ? atoi(v) : 3);
+        int rc = -1;
+        if (ver >= 3) rc = flash_fwd3(a, (bf16*)out, ld_out, lse, s);
+        if (rc && a.rowmask) return msq_set_error(MSQ_ERR_UNSUPPORTED, "msq_relattn_fwd: dropout needs the v3 kernel");
+        if (rc && ver >= 2) rc = flash_fwd2(a, (bf16*)out, ld_out, lse, s);
+        if (rc) flash_fwd(a, (bf16*)out, ld_out, lse, s);
+    }
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
 }
 
 extern "C" int msq_relattn_fwd(int dtype, void* out, int64_t ld_out, float* lse, const void* qkv, int64_t ld_qkv,
                                const void* R, int64_t B, int64_t S, int64_t H, int64_t hs, int64_t S_max, float scale,
                                int64_t n_meta, void* stream) {
+    return msq_relattn_fwd_dropout(dtype, out, ld_out, lse, qkv, ld_qkv, R, B, S, H, hs, S_max, scale, n_meta,
+                                   nullptr, nullptr, 0.f, stream);
+}
+
+extern "C" int msq_relattn_fwd_dropout(int dtype, void* out, int64_t ld_out, float* lse, const void* qkv,
+                                       int64_t ld_qkv, const void* R, int64_t B, int64_t S, int64_t H, int64_t hs,
+                                       int64_t S_max, float scale, int64_t n_meta, const uint32_t* rowmask,
+                                       const uint32_t* colmask, float p, void* stream) {
     MSQ_CHECK_ARG(B > 0 && S > 0 && H > 0 && hs > 0 && S <= S_max, "msq_relattn_fwd: bad sizes (S <= S_max)");
     MSQ_CHECK_ARG(ld_qkv >= 3 * H * hs && ld_out >= H * hs, "msq_relattn_fwd: leading dims too small");
-    const AttnArgs a = mk(B, S, H, hs, S_max, n_meta, scale, qkv, ld_qkv, R);
+    MSQ_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || (rowmask && colmask)), "msq_relattn_fwd: dropout needs masks");
+    AttnArgs a = mk(B, S, H, hs, S_max, n_meta, scale, qkv, ld_qkv, R);
+    if (p > 0.f) set_drop(a, rowmask, colmask, p);
+    return relattn_fwd(dtype, out, ld_out, lse, a, stream);
+}
+
+static int relattn_bwd(int dtype, void* dqkv, int64_t ld_dqkv, float* dR, const void* dout, int64_t ld_dout,
+                       const void* out, const float* lse, const AttnArgs& a, void* workspace, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     if (dtype == MSQ_F32) {
-        exact_fwd(a, (float*)out, ld_out, lse, s);
+        exact_bwd(a, lse, (const float*)dout, ld_dout, (float*)dqkv, ld_dqkv, dR, workspace, s);
     } else {
-        MSQ_CHECK_ARG(hs == 128 && ld_qkv % 8 == 0 && ld_out % 4 == 0, "msq_relattn_fwd: bf16 path needs hs == 128");
-        // MSQ_ATTN_FWD=1|2|3 selects a kernel generation for A/B runs (default 3)
-        const char* v = getenv("MSQ_ATTN_FWD");
-        const int ver = v ? atoi(v) : 3;
-        int rc = -1;
-        if (ver >= 3) rc = flash_fwd3(a, (bf16*)out, ld_out, lse, s);
-        if (rc && ver >= 2) rc = flash_fwd2(a, (bf16*)out, ld_out, lse, s);
-        if (rc) flash_fwd(a, (bf16*)out, ld_out, lse, s);
+        MSQ_CHECK_ARG(a.hs == 128 && a.ldq % 8 == 0 && ld_dout % 8 == 0 && ld_dqkv % 8 == 0,
+                      "msq_relattn_bwd: bf16 path needs hs == 128, ld %% 8 == 0");
+        int rc = flash_bwd(a, lse, (const bf16*)dout, ld_dout, (const bf16*)out, (bf16*)dqkv, ld_dqkv, dR, workspace, s);
+        if (rc) return rc;
     }
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
@@ -235,18 +279,19 @@ extern "C" int msq_relattn_bwd(int dtype, void* dqkv, int64_t ld_dqkv, float* dR
                                const void* out, const float* lse, const void* qkv, int64_t ld_qkv, const void* R,
                                int64_t B, int64_t S, int64_t H, int64_t hs, int64_t S_max, float scale, int64_t n_meta,
                                void* workspace, void* stream) {
+    return msq_relattn_bwd_dropout(dtype, dqkv, ld_dqkv, dR, dout, ld_dout, out, lse, qkv, ld_qkv, R, B, S, H, hs,
+                                   S_max, scale, n_meta, nullptr, nullptr, 0.f, workspace, stream);
+}
+
+extern "C" int msq_relattn_bwd_dropout(int dtype, void* dqkv, int64_t ld_dqkv, float* dR, const void* dout,
+                                       int64_t ld_dout, const void* out, const float* lse, const void* qkv,
+                                       int64_t ld_qkv, const void* R, int64_t B, int64_t S, int64_t H, int64_t hs,
+                                       int64_t S_max, float scale, int64_t n_meta, const uint32_t* rowmask,
+                                       const uint32_t* colmask, float p, void* workspace, void* stream) {
     MSQ_CHECK_ARG(B > 0 && S > 0 && H > 0 && hs > 0 && S <= S_max && workspace && n_meta <= 8,
                   "msq_relattn_bwd: bad args");
-    const AttnArgs a = mk(B, S, H, hs, S_max, n_meta, scale, qkv, ld_qkv, R);
-    hipStream_t s = (hipStream_t)stream;
-    if (dtype == MSQ_F32) {
-        exact_bwd(a, lse, (const float*)dout, ld_dout, (float*)dqkv, ld_dqkv, dR, workspace, s);
-    } else {
-        MSQ_CHECK_ARG(hs == 128 && ld_qkv % 8 == 0 && ld_dout % 8 == 0 && ld_dqkv % 8 == 0,
-                      "msq_relattn_bwd: bf16 path needs hs == 128, ld %% 8 == 0");
-        int rc = flash_bwd(a, lse, (const bf16*)dout, ld_dout, (const bf16*)out, (bf16*)dqkv, ld_dqkv, dR, workspace, s);
-        if (rc) return rc;
-    }
-    MSQ_LAUNCH_CHECK();
-    return MSQ_OK;
+    MSQ_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || (rowmask && colmask)), "msq_relattn_bwd: dropout needs masks");
+    AttnArgs a = mk(B, S, H, hs, S_max, n_meta, scale, qkv, ld_qkv, R);
+    if (p > 0.f) set_drop(a, rowmask, colmask, p);
+    return relattn_bwd(dtype, dqkv, ld_dqkv, dR, dout, ld_dout, out, lse, a, workspace, stream);
 }

@@ -511,7 +511,9 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     hipLaunchKernelGGL(flash_bwd_pre_kernel, dim3((unsigned)((B * S * H + 3) / 4)), dim3(256), 0, s, a, dout, ldo, out, Dv);
     // MSQ_ATTN_BWD=1 selects the first-generation key/value pass (A/B runs)
     const char* bv = getenv("MSQ_ATTN_BWD");
-    if ((bv && atoi(bv) == 1) || flash_bwd_kv3(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, ldr, meta_ds, s)) {
+    const bool v1 = bv && atoi(bv) == 1 && !a.rowmask;
+    if (v1 || flash_bwd_kv3(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, ldr, meta_ds, s)) {
+        if (a.rowmask) return msq_set_error(MSQ_ERR_UNSUPPORTED, "flash_bwd: dropout needs the v3 kernel");
         const unsigned nkb = (unsigned)((S + A_KB - 1) / A_KB);
         hipLaunchKernelGGL(flash_bwd_a_kernel, dim3(nkb, (unsigned)H, (unsigned)B), dim3(NT), 0, s, a, lse, Dv, dout,
                            ldo, dqkv, ldd, dqr, ldr, meta_ds);

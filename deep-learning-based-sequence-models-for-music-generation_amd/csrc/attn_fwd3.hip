@@ -25,7 +25,8 @@ constexpr int NT = 512;
 constexpr int QB = 256, KB = 32, NCH = 10, RING = NCH * KB, SCR = 52;
 constexpr int O_K = 0, O_V = 2 * KB * 256, O_R = 4 * KB * 256, O_S = O_R + RING * 256;
 constexpr int O_M = O_S + 8 * 16 * SCR * 4;
-constexpr int LDS_BYTES = O_M + 64 * 4;
+constexpr int O_D = O_M + 64 * 4;  // dropout keep words of the block's 256 queries, 2 tiles
+constexpr int LDS_BYTES = O_D + 2 * QB * 4;
 constexpr uint32_t OOB = 0xFFFF0000u;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
@@ -61,7 +62,10 @@ __device__ __forceinline__ void bar() {
 
 // LAB: ablation switches for tools/lab (0 in the library):
 // 1 no K.Q^T MFMA, 2 no QR MFMA, 4 no skew / softmax, 8 no PV MFMA, 16 no DMA in the loop
-template <int LAB = 0>
+// DROP: attention-probability dropout (model_transformer.py:80): the keep word
+// of (query, key tile) is staged by LDS-DMA with the tile; P.V uses p * keep,
+// the softmax normaliser the undropped p, the output is scaled by 1/(1-p)
+template <int LAB = 0, bool DROP = false>
 __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __restrict__ out, int64_t ldo,
                                                            float* __restrict__ lse) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -116,6 +120,19 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
     const float c2 = a.scale * LOG2E;
 
     const int nkt = (qhi - 1) / KB + 1;
+    // keep words rowmask[b,h,i][kt]: waves 0-3 stage the block's 256 queries
+    const int64_t mld = a.mask_ld;
+    const __amdgpu_buffer_rsrc_t rm =
+        make_rsrc(DROP ? (const void*)(a.rowmask + (int64_t)(b * H + h) * S * mld) : (const void*)a.R,
+                  DROP ? (uint32_t)(S * mld * 4) : 0u);
+    auto stage_m = [&](int kt, int buf) {
+        if (DROP && w < 4) {
+            const int iq = i0 + 64 * w + lane;
+            const uint32_t vo = (iq >= 0 && iq < S) ? (uint32_t)((iq * mld + kt) * 4) : OOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, (lds_char*)(smem + O_D + buf * QB * 4 + w * 256), 4, vo, 0,
+                                                     0, 0);
+        }
+    };
     const int rb0 = S - qhi;  // R row of block-window row 0 at tile 0; chunk c = rows rb0 + 32 c ..
 
     // per-lane DMA constants: row tid/16 of a 32-row tile, chunk slot lane%16
@@ -136,6 +153,7 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
     }
 
     // prologue: tile 0 and the 9 R chunks of its window
+    stage_m(0, 0);
     dma32(rq, smem + O_K, offK, lrow, 0, 0, S, w);
     dma32(rq, smem + O_V, offV, lrow, 0, 0, S, w);
 #pragma unroll
@@ -156,6 +174,7 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
             dma32(rq, smem + O_K + (cur ^ 1) * KB * 256, offK, lrow, (uint32_t)j1 * ldq2, 0, S - j1, w);
             dma32(rq, smem + O_V + (cur ^ 1) * KB * 256, offV, lrow, (uint32_t)j1 * ldq2, 0, S - j1, w);
             dma32(rr, sR + (c % NCH) * KB * 256, offR, lrow, (uint32_t)(r0 * HS * 2), -r0, S - r0, w);
+            stage_m(kt + 1, cur ^ 1);
         }
         if (live) {
             const char* cK = smem + O_K + cur * KB * 256;
@@ -258,13 +277,15 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
                 }
                 m_run[q2] = m_new;
                 float ps = 0.f;
+                uint32_t kw = 0;
+                if (DROP) kw = ((const uint32_t*)(smem + O_D + cur * QB * 4))[32 * w + 16 * q2 + il] >> (4 * g);
 #pragma unroll
                 for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const float p = __builtin_amdgcn_exp2f(fmaf(sv[nt][r], c2, -m_new));
                         ps += p;
-                        pf[q2][nt * 4 + r] = (bf16)p;
+                        pf[q2][nt * 4 + r] = DROP ? ((kw >> (nt * 16 + r)) & 1u ? (bf16)p : (bf16)0.f) : (bf16)p;
                     }
                 l_part[q2] += ps;
             }
@@ -289,7 +310,7 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
         float l = l_part[q2] + __shfl_xor(l_part[q2], 16, 64);
         l += __shfl_xor(l, 32, 64);
         if (iq >= 0 && iq < S) {
-            const float inv = 1.f / l;
+            const float inv = (DROP ? a.keep_scale : 1.f) / l;
             bf16* op = out + ((int64_t)b * S + iq) * ldo + h * HS;
 #pragma unroll
             for (int n = 0; n < 8; ++n) store4(op + n * 16 + 4 * g, oacc[q2][n] * inv);
@@ -303,12 +324,16 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
 int flash_fwd3(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)flash_fwd3_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)flash_fwd3_kernel<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)flash_fwd3_kernel<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   LDS_BYTES);
         attr = true;
     }
+    if (a.rowmask && a.S * a.mask_ld * 4 >= (int64_t)OOB) return -1;
     if (a.S * a.ldq * 2 >= (int64_t)OOB || a.S * HS * 2 >= (int64_t)OOB || a.n_meta > 8) return -1;
     const dim3 grid((unsigned)((a.S + QB - 1) / QB), (unsigned)a.H, (unsigned)a.B);
-    hipLaunchKernelGGL(flash_fwd3_kernel<0>, grid, dim3(NT), LDS_BYTES, s, a, out, ldo, lse);
+    if (a.rowmask) hipLaunchKernelGGL((flash_fwd3_kernel<0, true>), grid, dim3(NT), LDS_BYTES, s, a, out, ldo, lse);
+    else hipLaunchKernelGGL((flash_fwd3_kernel<0, false>), grid, dim3(NT), LDS_BYTES, s, a, out, ldo, lse);
     return 0;
 }

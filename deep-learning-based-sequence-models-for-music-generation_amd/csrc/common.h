@@ -68,3 +68,31 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
     const int q = nblk / 8, r = nblk % 8, xcd = bid % 8, loc = bid / 8;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
+
+// ---- dropout (nn.Dropout, model_transformer.py:51,80,101) ----
+// Counter-based keep mask: element (row, col) of dropout site `site` under the
+// step seed `seed` is kept iff drop_bits(drop_row(drop_base(seed, site), row),
+// col) >= thr, thr = round(p * 2^32); kept values are scaled by 1/(1-p).
+// oracle/dropout.py restates these four functions bit-exactly.
+__host__ __device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x21f0aaadu;
+    x ^= x >> 15;
+    x *= 0x735a2d97u;
+    x ^= x >> 15;
+    return x;
+}
+__host__ __device__ __forceinline__ uint32_t drop_base(uint32_t seed, uint32_t site) {
+    return drop_mix(seed ^ drop_mix(site + 0x9e3779b9u));
+}
+__host__ __device__ __forceinline__ uint32_t drop_row(uint32_t base, uint32_t row) {
+    return drop_mix(base + row * 0x9e3779b9u);
+}
+__host__ __device__ __forceinline__ uint32_t drop_bits(uint32_t rowkey, uint32_t col) {
+    return drop_mix(rowkey ^ (col * 0x85ebca6bu));
+}
+// host: keep threshold for drop probability p
+static inline uint32_t drop_threshold(float p) {
+    const double t = (double)p * 4294967296.0;
+    return t <= 0.0 ? 0u : (t >= 4294967295.0 ? 0xffffffffu : (uint32_t)(t + 0.5));
+}

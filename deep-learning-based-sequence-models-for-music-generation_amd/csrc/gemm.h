@@ -20,7 +20,18 @@ struct GemmArgs {
     // 2 = K is nseg segments of seg rows, tile rows m = r need k%seg >= seg-1-r (dR)
     int tri;
     int64_t seg;
+    // MSQ_EPI_BIAS_DROP_RESID: drop_base = drop_base(seed, site), keep iff bits >= drop_thr
+    uint32_t drop_base, drop_thr;
+    float drop_scale;
 };
+
+// dropout(v + bias) of one lane's 4 outputs C[m][n..n+3] (nn.Dropout, common.h hash)
+__device__ __forceinline__ f32x4 epi_drop(const GemmArgs& g, int64_t m, int64_t n, f32x4 v) {
+    const uint32_t rk = drop_row(g.drop_base, (uint32_t)m);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = drop_bits(rk, (uint32_t)(n + t)) >= g.drop_thr ? v[t] * g.drop_scale : 0.f;
+    return v;
+}
 
 template <typename TC>
 __device__ __forceinline__ void epi_store(TC* p, f32x4 v, int nv) {
@@ -45,8 +56,10 @@ __device__ __forceinline__ f32x4 epi_load(const T* p, int nv) {
 template <int EPI, typename TC, typename TX>
 __device__ __forceinline__ void epi_apply(const GemmArgs& g, TC* C, const TX* X, int64_t m, int64_t n, f32x4 v) {
     const int nv = g.vec ? (int)min<int64_t>(4, g.N - n) : -(int)min<int64_t>(4, g.N - n);
-    if ((EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID) && g.bias)
+    if ((EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID ||
+         EPI == MSQ_EPI_BIAS_DROP_RESID) && g.bias)
         v += epi_load(g.bias + n, nv);
+    if (EPI == MSQ_EPI_BIAS_DROP_RESID) v = epi_drop(g, m, n, v) + epi_load(X + m * g.ldx + n, nv);
     if (EPI == MSQ_EPI_BIAS_RELU) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);

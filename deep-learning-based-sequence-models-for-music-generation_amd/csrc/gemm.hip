@@ -213,8 +213,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
             if (n >= g.N) continue;
             const int nv = g.vec ? (int)min<int64_t>(4, g.N - n) : -(int)min<int64_t>(4, g.N - n);
             f32x4 v = acc[i][j];
-            if ((EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID) && g.bias)
+            if ((EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID ||
+                 EPI == MSQ_EPI_BIAS_DROP_RESID) && g.bias)
                 v += epi_load(g.bias + n, nv);
+            if (EPI == MSQ_EPI_BIAS_DROP_RESID) v = epi_drop(g, m, n, v) + epi_load(X + m * g.ldx + n, nv);
             if (EPI == MSQ_EPI_BIAS_RELU) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);
@@ -287,7 +289,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g, int ta, int t
             const int64_t n = n0 + tx * 4 + j;
             if (n >= g.N) continue;
             float v = acc[i][j];
-            if ((EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID) && g.bias) v += g.bias[n];
+            if ((EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID ||
+                 EPI == MSQ_EPI_BIAS_DROP_RESID) && g.bias)
+                v += g.bias[n];
+            if (EPI == MSQ_EPI_BIAS_DROP_RESID)
+                v = (drop_bits(drop_row(g.drop_base, (uint32_t)m), (uint32_t)n) >= g.drop_thr ? v * g.drop_scale : 0.f) +
+                    (float)X[m * g.ldx + n];
             if (EPI == MSQ_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
             if (EPI == MSQ_EPI_BIAS_RESID) v += (float)X[m * g.ldx + n];
             if (EPI == MSQ_EPI_RELU_MASK) v = ((float)X[m * g.ldx + n] > 0.f) ? v : 0.f;
@@ -331,6 +338,7 @@ int dispatch_epi(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hipS
         case MSQ_EPI_RELU_MASK:
             return aux_dtype == MSQ_BF16 ? D(MSQ_EPI_RELU_MASK, bf16) : D(MSQ_EPI_RELU_MASK, float);
         case MSQ_EPI_ACCUM: return D(MSQ_EPI_ACCUM, float);
+        case MSQ_EPI_BIAS_DROP_RESID: return D(MSQ_EPI_BIAS_DROP_RESID, float);
     }
 #undef D
     return -1;
@@ -368,9 +376,21 @@ extern "C" int msq_gemm(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t
                         int64_t strideA, const void* B, int64_t ldb, int64_t strideB, void* C, int c_dtype,
                         int64_t ldc, int64_t strideC, int64_t batch, int epilogue, const float* bias,
                         const void* aux, int aux_dtype, int64_t ld_aux, int64_t stride_aux, void* stream) {
+    MSQ_CHECK_ARG(epilogue != MSQ_EPI_BIAS_DROP_RESID, "msq_gemm: the dropout epilogue needs msq_gemm_dropout");
+    return msq_gemm_dropout(dtype, ta, tb, M, N, K, A, lda, strideA, B, ldb, strideB, C, c_dtype, ldc, strideC, batch,
+                            epilogue, bias, aux, aux_dtype, ld_aux, stride_aux, 0u, 0u, 0.f, stream);
+}
+
+extern "C" int msq_gemm_dropout(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A,
+                                int64_t lda, int64_t strideA, const void* B, int64_t ldb, int64_t strideB, void* C,
+                                int c_dtype, int64_t ldc, int64_t strideC, int64_t batch, int epilogue,
+                                const float* bias, const void* aux, int aux_dtype, int64_t ld_aux, int64_t stride_aux,
+                                uint32_t seed, uint32_t site, float p, void* stream) {
     MSQ_CHECK_ARG(dtype == MSQ_BF16 || dtype == MSQ_F32, "msq_gemm: bad dtype %d", dtype);
     MSQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && batch > 0, "msq_gemm: empty problem");
-    MSQ_CHECK_ARG(epilogue >= MSQ_EPI_NONE && epilogue <= MSQ_EPI_ACCUM, "msq_gemm: bad epilogue");
+    MSQ_CHECK_ARG(epilogue >= MSQ_EPI_NONE && epilogue <= MSQ_EPI_BIAS_DROP_RESID, "msq_gemm: bad epilogue");
+    MSQ_CHECK_ARG(p >= 0.f && p < 1.f, "msq_gemm_dropout: p must be in [0, 1)");
+    MSQ_CHECK_ARG(aux || epilogue != MSQ_EPI_BIAS_DROP_RESID, "msq_gemm: epilogue needs aux");
     MSQ_CHECK_ARG(!(epilogue == MSQ_EPI_ACCUM && c_dtype != MSQ_F32), "msq_gemm: ACCUM needs fp32 C");
     MSQ_CHECK_ARG(bias || (epilogue != MSQ_EPI_BIAS && epilogue != MSQ_EPI_BIAS_RELU),
                   "msq_gemm: epilogue needs bias (BIAS_RESID accepts NULL)");
@@ -388,6 +408,9 @@ extern "C" int msq_gemm(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t
     g.B = B; g.ldb = ldb; g.sB = strideB;
     g.C = C; g.ldc = ldc; g.sC = strideC;
     g.bias = bias; g.aux = aux; g.ldx = ld_aux; g.sX = stride_aux;
+    g.drop_base = drop_base(seed, site);
+    g.drop_thr = drop_threshold(p);
+    g.drop_scale = 1.f / (1.f - p);
     g.tiles_m = (int)((M + BM - 1) / BM);
     g.tiles_n = (int)((N + BN - 1) / BN);
     g.batch = (int)batch;

@@ -345,6 +345,7 @@ void dispatch_epi(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hip
             else dispatch_t<MSQ_EPI_RELU_MASK, TC, float>(g, ta, tb, s);
             break;
         case MSQ_EPI_ACCUM: dispatch_t<MSQ_EPI_ACCUM, TC, float>(g, ta, tb, s); break;
+        case MSQ_EPI_BIAS_DROP_RESID: dispatch_t<MSQ_EPI_BIAS_DROP_RESID, TC, float>(g, ta, tb, s); break;
     }
 }
 

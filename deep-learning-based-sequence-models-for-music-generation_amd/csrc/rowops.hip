@@ -107,13 +107,20 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(TY* __restrict__ y, float* 
 
 constexpr int LN_BWD_BLOCKS = 512;
 
+// dropout keep mask applied to the copy (the gradient into the dropped branch)
+struct CopyDrop {
+    uint32_t base, thr;
+    float scale;
+    int on;
+};
+
 // dx_acc += rstd*(dyg - mean(dyg) - xhat*mean(dyg*xhat)); per-block dgamma/dbeta partials
 template <typename TD, typename TO, int MAXC>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO* __restrict__ dcopy,
                                                      float* __restrict__ part, const TD* __restrict__ dy,
                                                      const float* __restrict__ x, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const float* __restrict__ gamma,
-                                                     int64_t rows, int d, int64_t seg, int64_t skip) {
+                                                     int64_t rows, int d, int64_t seg, int64_t skip, CopyDrop cd) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     f32x4 pg[MAXC], pb[MAXC];
 #pragma unroll
@@ -153,7 +160,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
 #pragma unroll
                 for (int t = 0; t < 4; ++t) o[t] += rs * (g[c][t] - m1 - xh[c][t] * m2);
                 *(f32x4*)dp = o;
-                if (dcopy) store4(dcopy + xrow * d + col, o);
+                if (dcopy) {
+                    if (cd.on) {  // d(dropped branch) = g * keep / (1-p) at (row xrow, col)
+                        const uint32_t rk = drop_row(cd.base, (uint32_t)xrow);
+#pragma unroll
+                        for (int t = 0; t < 4; ++t)
+                            o[t] = drop_bits(rk, (uint32_t)(col + t)) >= cd.thr ? o[t] * cd.scale : 0.f;
+                    }
+                    store4(dcopy + xrow * d + col, o);
+                }
             }
         }
     }
@@ -234,28 +249,39 @@ extern "C" int msq_layernorm_fwd(void* y, int y_dtype, float* mean, float* rstd,
 template <typename TD, typename TO>
 static void ln_bwd_launch(float* dxa, TO* dcopy, float* part, const TD* dy, const float* x, const float* mean,
                           const float* rstd, const float* gamma, int64_t rows, int d, int64_t seg, int64_t skip,
-                          hipStream_t s) {
+                          CopyDrop cd, hipStream_t s) {
     const dim3 grid(LN_BWD_BLOCKS);
-    if (d <= 256) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 1>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip);
-    else if (d <= 1024) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip);
-    else hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 8>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip);
+    if (d <= 256) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 1>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
+    else if (d <= 1024) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
+    else hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 8>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
 }
 
 extern "C" int msq_layernorm_bwd(float* dx_acc, void* dx_copy, int copy_dtype, float* dgamma, float* dbeta,
                                  const void* dy, int dy_dtype, const float* x, const float* mean, const float* rstd,
                                  const float* gamma, int64_t rows, int64_t d, int64_t seg_len, int64_t seg_skip,
                                  void* workspace, void* stream) {
+    return msq_layernorm_bwd_dropout(dx_acc, dx_copy, copy_dtype, dgamma, dbeta, dy, dy_dtype, x, mean, rstd, gamma,
+                                     rows, d, seg_len, seg_skip, 0u, 0u, 0.f, workspace, stream);
+}
+
+extern "C" int msq_layernorm_bwd_dropout(float* dx_acc, void* dx_copy, int copy_dtype, float* dgamma, float* dbeta,
+                                         const void* dy, int dy_dtype, const float* x, const float* mean,
+                                         const float* rstd, const float* gamma, int64_t rows, int64_t d,
+                                         int64_t seg_len, int64_t seg_skip, uint32_t seed, uint32_t site, float p,
+                                         void* workspace, void* stream) {
     MSQ_CHECK_ARG(d % 4 == 0 && d <= 2048 && rows > 0 && workspace, "msq_layernorm_bwd: bad args");
+    MSQ_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || dx_copy), "msq_layernorm_bwd: dropout needs dx_copy");
+    CopyDrop cd{drop_base(seed, site), drop_threshold(p), 1.f / (1.f - p), p > 0.f ? 1 : 0};
     MSQ_CHECK_ARG(seg_skip == 0 || seg_len > 0, "msq_layernorm_bwd: seg_len must be > 0 with seg_skip");
     hipStream_t s = (hipStream_t)stream;
     float* part = (float*)workspace;
     const int di = (int)d;
     if (dy_dtype == MSQ_BF16) {
-        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, s);
-        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, s);
+        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, s);
+        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, s);
     } else {
-        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, s);
-        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, s);
+        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, s);
+        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, s);
     }
     hipLaunchKernelGGL(ln_reduce_kernel, dim3((unsigned)((2 * d + 63) / 64)), dim3(256), 0, s, dgamma, dbeta, part,
                        LN_BWD_BLOCKS, di);

@@ -179,7 +179,8 @@ class MambaEngine:
         c = self.cfg
         return A.B, A.L, c.d_inner, c.nheads
 
-    def forward(self, idx, meta, save=True):
+    def forward(self, idx, meta, save=True, train=False):
+        # models/mamba/mamba.py has no dropout: train mode changes nothing
         cfg, P, W = self.cfg, self.P, self.W
         if not idx.is_cuda:
             raise RuntimeError("the MI355X engine runs on the GPU only (no CPU fallback)")

@@ -19,8 +19,10 @@ def _mat(t, trans):
     return r, c, ld, 0, 1
 
 
-def gemm(A, B, *, ta=False, tb=False, out=None, out_dtype=None, epilogue=L.EPI_NONE, bias=None, aux=None):
-    """C = op(A) . op(B).  ta: A stored [K,M]; tb: B stored [K,N] (else [N,K])."""
+def gemm(A, B, *, ta=False, tb=False, out=None, out_dtype=None, epilogue=L.EPI_NONE, bias=None, aux=None,
+         drop=None):
+    """C = op(A) . op(B).  ta: A stored [K,M]; tb: B stored [K,N] (else [N,K]).
+    drop=(seed, site, p): epilogue BIAS_RESID becomes aux + dropout(acc + bias)."""
     ar, ac, lda, sA, ba = _mat(A, ta)
     br, bc, ldb, sB, bb = _mat(B, tb)
     M, K = (ac, ar) if ta else (ar, ac)
@@ -38,6 +40,12 @@ def gemm(A, B, *, ta=False, tb=False, out=None, out_dtype=None, epilogue=L.EPI_N
     if aux is not None:
         _, _, ldx, sX, _ = _mat(aux, False)
         axd = dt(aux)
+    if drop is not None and drop[2] > 0:
+        assert epilogue == L.EPI_BIAS_RESID, "dropout is fused into the bias+residual epilogue only"
+        call("msq_gemm_dropout", dt(A), int(ta), int(tb), M, N, K, ptr(A), lda, sA, ptr(B), ldb, sB, ptr(out),
+             dt(out), ldc, sC, batch, L.EPI_BIAS_DROP_RESID, ptr(bias), ptr(aux), axd, ldx, sX, int(drop[0]),
+             int(drop[1]), float(drop[2]), stream())
+        return out
     call("msq_gemm", dt(A), int(ta), int(tb), M, N, K, ptr(A), lda, sA, ptr(B), ldb, sB, ptr(out), dt(out), ldc,
          sC, batch, epilogue, ptr(bias), ptr(aux), axd, ldx, sX, stream())
     return out
@@ -70,14 +78,16 @@ def workspace(nbytes, device, tag="ws"):
     return buf
 
 
-def layernorm_bwd(dx_acc, dy, x, mean, rstd, gamma, dgamma, dbeta, dx_copy=None, seg=(0, 0)):
-    """dx_acc[map(r)] += LN'(dy[r]); dgamma/dbeta += ...; optional copy of the updated rows."""
+def layernorm_bwd(dx_acc, dy, x, mean, rstd, gamma, dgamma, dbeta, dx_copy=None, seg=(0, 0), drop=None):
+    """dx_acc[map(r)] += LN'(dy[r]); dgamma/dbeta += ...; optional copy of the updated rows
+    (drop=(seed, site, p): the copy is masked by that site's dropout keep mask and scaled)."""
     d = x.shape[-1]
     rows = mean.numel()
     ws = workspace(L.lib().msq_layernorm_bwd_workspace(rows, d), x.device, "ln")
-    call("msq_layernorm_bwd", ptr(dx_acc), ptr(dx_copy), dt(dx_copy) if dx_copy is not None else L.F32,
+    seed, site, p = drop if drop is not None else (0, 0, 0.0)
+    call("msq_layernorm_bwd_dropout", ptr(dx_acc), ptr(dx_copy), dt(dx_copy) if dx_copy is not None else L.F32,
          ptr(dgamma), ptr(dbeta), ptr(dy), dt(dy), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), rows, d, seg[0], seg[1],
-         ptr(ws), stream())
+         int(seed), int(site), float(p), ptr(ws), stream())
 
 
 def colsum(x2d, out, accumulate=False):
@@ -108,3 +118,12 @@ def cast(dst, src):
 def adam_step(p, g, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, shadow=None, grad_scale=1.0):
     call("msq_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow), p.numel(), float(lr), float(beta1),
          float(beta2), float(eps), int(step), float(grad_scale), stream())
+
+
+def dropout_attn_mask(B, H, S, seed, site0, p, device, out=None):
+    """(rowmask, colmask) keep bits of one layer's attention dropout (msq_dropout_attn_mask)."""
+    ld = L.lib().msq_dropout_mask_ld(S)
+    if out is None:
+        out = torch.zeros(2, B * H * S * ld, device=device, dtype=torch.int32)
+    call("msq_dropout_attn_mask", ptr(out[0]), ptr(out[1]), B, H, S, int(seed), int(site0), float(p), stream())
+    return out

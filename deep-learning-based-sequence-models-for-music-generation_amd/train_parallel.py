@@ -48,7 +48,7 @@ class TrainStep:
     def __call__(self, src, trg, meta):
         eng, cfg = self.eng, self.eng.cfg
         B, T = src.shape
-        eng.forward(src, meta)
+        eng.forward(src, meta, train=self.model.training)
         A = eng.acts(B, T)
         dl = eng.dlogits_buffer(B, T)
         loss, _ = ce_forward_backward(src, A.logits.view(B, T, cfg.v_pad), trg, cfg.vocab_size, self.grammar,

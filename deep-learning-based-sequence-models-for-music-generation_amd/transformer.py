@@ -25,6 +25,10 @@ from . import ops
 from .attention import relattn_fwd, relattn_bwd
 from .config import N_META, VOCAB_SIZE, METADATA_VOCAB_SIZE, BLOCK_LEN
 
+# dropout sites of the counter-based keep masks (csrc/common.h; oracle/dropout.py):
+# attention probabilities of layer l / batch b / head h, proj output, FFN output
+DROP_ATTN, DROP_PROJ, DROP_FFN = 1 << 28, 2 << 28, 3 << 28
+
 
 @dataclass
 class TransformerConfig:
@@ -164,6 +168,15 @@ class _Acts:
         self.logits = e(B * T, cfg.v_pad)
         self.gen = 0
         self._bwd = None
+        self.drop = None      # (seed, p) of the last training forward
+        self._masks = None    # [L, 2, n] attention keep bits (row / col layouts)
+
+    def masks(self, cfg, device):
+        if self._masks is None:
+            ld = L.lib().msq_dropout_mask_ld(self.S)
+            n = self.B * cfg.n_heads * self.S * ld
+            self._masks = torch.zeros(cfg.n_layer if self.save else 1, 2, n, device=device, dtype=torch.int32)
+        return self._masks
 
     def bwd(self, cfg, device, act):
         if self._bwd is None:
@@ -171,7 +184,8 @@ class _Acts:
             M = self.M
             f32 = torch.float32
             e = lambda *s, dt=act: torch.empty(*s, device=device, dtype=dt)  # noqa: E731
-            self._bwd = dict(gres=e(M, d, dt=f32), gb=e(M, d) if act != f32 else None, dtmp=e(M, d),
+            need_copy = act != f32 or cfg.dropout > 0  # fp32 + dropout: masked fp32 copy
+            self._bwd = dict(gres=e(M, d, dt=f32), gb=e(M, d) if need_copy else None, dtmp=e(M, d),
                              dh=e(M, 4 * d), dqkv=e(M, 3 * d), df=e(self.B * self.T, d),
                              dlogits=torch.zeros(self.B * self.T, cfg.v_pad, device=device, dtype=act))
         return self._bwd
@@ -181,8 +195,8 @@ class TransformerEngine:
     """Explicit forward / backward over the libmidiseq kernels."""
 
     def __init__(self, cfg: TransformerConfig, flat: torch.Tensor):
-        if cfg.dropout not in (0, 0.0):
-            raise NotImplementedError("dropout > 0 is not implemented in this engine yet (use dropout=0)")
+        if not 0.0 <= cfg.dropout < 1.0:
+            raise ValueError(f"dropout must be in [0, 1), got {cfg.dropout}")
         self.cfg = cfg
         self.layout = ParamLayout(cfg)
         self.act = torch.bfloat16 if cfg.precision == "bf16" else torch.float32
@@ -220,9 +234,12 @@ class TransformerEngine:
         return self._acts[key]
 
     # ------------------------------------------------------------- forward
-    def forward(self, idx, meta, save=True):
+    def forward(self, idx, meta, save=True, train=False, seed=None):
         """save=False (inference): one layer's activation buffers are reused
-        and nothing is kept for a backward pass."""
+        and nothing is kept for a backward pass. train=True (nn.Module.train()
+        mode, save=True only) applies nn.Dropout(cfg.dropout) at the reference's
+        three sites (model_transformer.py:51,80,101) with keep masks drawn from
+        `seed` (default: one draw of torch's CPU generator per step)."""
         cfg, P, W = self.cfg, self.P, self.W
         if not idx.is_cuda:
             raise RuntimeError("the MI355X engine runs on the GPU only (no CPU fallback)")
@@ -238,18 +255,32 @@ class TransformerEngine:
         meta = meta.contiguous()
         if save:
             self._idx, self._meta = idx, meta
+        p = float(cfg.dropout) if (train and save) else 0.0
+        if p > 0:
+            if seed is None:
+                seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+            A.drop = (int(seed) & 0xFFFFFFFF, p)
+            masks = A.masks(cfg, self.device)
+        else:
+            A.drop = None
         ops.embed_fwd(A.x[0].view(B, S, d), P["tok_emb"], P["meta_emb"], idx, meta)
         for l in range(cfg.n_layer):
             k = l if save else 0
             x, xo = (A.x[l], A.x[l + 1]) if save else (A.x[l % 2], A.x[(l + 1) % 2])
             ops.layernorm_fwd(x, P[f"{l}.ln1_w"], P[f"{l}.ln1_b"], out=A.a[k], mean=A.st1[k, 0], rstd=A.st1[k, 1])
             ops.gemm(A.a[k], W[f"{l}.wqkv"], out=A.qkv[k])
-            relattn_fwd(A.qkv[k], W[f"{l}.R"], B, S, H, hs, scale, out=A.o[k], lse=A.lse[k])
-            ops.gemm(A.o[k], W[f"{l}.wproj"], out=A.xm[k], epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.bproj"], aux=x)
+            adrop = pdrop = fdrop = None
+            if p > 0:
+                ops.dropout_attn_mask(B, H, S, seed, DROP_ATTN + l * 65536, p, self.device, out=masks[k])
+                adrop, pdrop, fdrop = (masks[k], p), (seed, DROP_PROJ + l, p), (seed, DROP_FFN + l, p)
+            relattn_fwd(A.qkv[k], W[f"{l}.R"], B, S, H, hs, scale, out=A.o[k], lse=A.lse[k], drop=adrop)
+            ops.gemm(A.o[k], W[f"{l}.wproj"], out=A.xm[k], epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.bproj"], aux=x,
+                     drop=pdrop)
             ops.layernorm_fwd(A.xm[k], P[f"{l}.ln2_w"], P[f"{l}.ln2_b"], out=A.c[k], mean=A.st2[k, 0],
                               rstd=A.st2[k, 1])
             ops.gemm(A.c[k], W[f"{l}.w1"], out=A.h[k], epilogue=L.EPI_BIAS_RELU, bias=P[f"{l}.b1"])
-            ops.gemm(A.h[k], W[f"{l}.w2"], out=xo, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.b2"], aux=A.xm[k])
+            ops.gemm(A.h[k], W[f"{l}.w2"], out=xo, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.b2"], aux=A.xm[k],
+                     drop=fdrop)
         x_last = A.x[cfg.n_layer] if save else A.x[cfg.n_layer % 2]
         ops.layernorm_fwd(x_last, P["lnf_w"], P["lnf_b"], out=A.f, mean=A.stf[0], rstd=A.stf[1],
                           seg=(T, N_META))
@@ -280,31 +311,37 @@ class TransformerEngine:
         gb = Bw["gb"] if Bw["gb"] is not None else gres
         if Bw["gb"] is not None:
             gb.zero_()
+        # dropout: gb is the gradient INTO the dropped branch (gres masked by the
+        # keep mask of the site whose output was added to the residual there);
+        # the bias gradients then sum gb instead of gres
+        seed, p = A.drop if A.drop is not None else (0, 0.0)
+        dsite = (lambda site: (seed, site, p)) if p > 0 else (lambda site: None)  # noqa: E731
+        gbias = gb if p > 0 else gres
         ops.layernorm_bwd(gres, Bw["df"], A.x[cfg.n_layer], A.stf[0], A.stf[1], P["lnf_w"], G["lnf_w"], G["lnf_b"],
-                          dx_copy=Bw["gb"], seg=(T, N_META))
+                          dx_copy=Bw["gb"], seg=(T, N_META), drop=dsite(DROP_FFN + cfg.n_layer - 1))
         hook = getattr(self, "layer_grad_ready", None)
         if hook is not None:
             hook("head")
         for l in reversed(range(cfg.n_layer)):
             # FFN (model_transformer.py:92-105,120)
             ops.gemm(gb, A.h[l], ta=True, tb=True, out=G[f"{l}.w2"], epilogue=L.EPI_ACCUM)
-            ops.colsum(gres, G[f"{l}.b2"], accumulate=True)
+            ops.colsum(gbias, G[f"{l}.b2"], accumulate=True)
             ops.gemm(gb, W[f"{l}.w2"], tb=True, out=Bw["dh"], epilogue=L.EPI_RELU_MASK, aux=A.h[l])
             ops.gemm(Bw["dh"], A.c[l], ta=True, tb=True, out=G[f"{l}.w1"], epilogue=L.EPI_ACCUM)
             ops.colsum(Bw["dh"], G[f"{l}.b1"], accumulate=True)
             ops.gemm(Bw["dh"], W[f"{l}.w1"], tb=True, out=Bw["dtmp"])
             ops.layernorm_bwd(gres, Bw["dtmp"], A.xm[l], A.st2[l, 0], A.st2[l, 1], P[f"{l}.ln2_w"], G[f"{l}.ln2_w"],
-                              G[f"{l}.ln2_b"], dx_copy=Bw["gb"])
+                              G[f"{l}.ln2_b"], dx_copy=Bw["gb"], drop=dsite(DROP_PROJ + l))
             # attention (model_transformer.py:41-90,119)
             ops.gemm(gb, A.o[l], ta=True, tb=True, out=G[f"{l}.wproj"], epilogue=L.EPI_ACCUM)
-            ops.colsum(gres, G[f"{l}.bproj"], accumulate=True)
+            ops.colsum(gbias, G[f"{l}.bproj"], accumulate=True)
             ops.gemm(gb, W[f"{l}.wproj"], tb=True, out=Bw["dtmp"])
             relattn_bwd(Bw["dtmp"], A.o[l], A.lse[l], A.qkv[l], W[f"{l}.R"], B, S, H, hs, scale, dqkv=Bw["dqkv"],
-                        dR=G[f"{l}.R"])
+                        dR=G[f"{l}.R"], drop=(A._masks[l], p) if p > 0 else None)
             ops.gemm(Bw["dqkv"], A.a[l], ta=True, tb=True, out=G[f"{l}.wqkv"], epilogue=L.EPI_ACCUM)
             ops.gemm(Bw["dqkv"], W[f"{l}.wqkv"], tb=True, out=Bw["dtmp"])
             ops.layernorm_bwd(gres, Bw["dtmp"], A.x[l], A.st1[l, 0], A.st1[l, 1], P[f"{l}.ln1_w"], G[f"{l}.ln1_w"],
-                              G[f"{l}.ln1_b"], dx_copy=Bw["gb"])
+                              G[f"{l}.ln1_b"], dx_copy=Bw["gb"], drop=dsite(DROP_FFN + l - 1) if l > 0 else None)
             if hook is not None:
                 hook(l)
         ops.embed_bwd(G["tok_emb"], G["meta_emb"], gres, idx, meta)
@@ -322,8 +359,8 @@ class TransformerEngine:
 
 class _TransformerFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, flat, idx, meta, engine):
-        logits = engine.forward(idx, meta)
+    def forward(ctx, flat, idx, meta, engine, train):
+        logits = engine.forward(idx, meta, train=train)
         A = engine.acts(*idx.shape)
         ctx.engine, ctx.gen, ctx.shape = engine, A.gen, tuple(idx.shape)
         return logits
@@ -343,7 +380,7 @@ class _TransformerFn(torch.autograd.Function):
         dl2 = buf
         grads = torch.zeros_like(eng.flat.data)
         eng.backward(dl2, grads)
-        return grads, None, None, None
+        return grads, None, None, None, None
 
 
 class Transformer(nn.Module):
@@ -411,7 +448,7 @@ class Transformer(nn.Module):
     def forward(self, idx, metadata_idx, targets=None):
         if not (torch.is_grad_enabled() and self.flat.requires_grad):
             return self.engine.forward(idx, metadata_idx, save=False)
-        return _TransformerFn.apply(self.flat, idx, metadata_idx, self.engine)
+        return _TransformerFn.apply(self.flat, idx, metadata_idx, self.engine, self.training)
 
     def get_name(self):
         return "Transformer"

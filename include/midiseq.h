@@ -41,6 +41,8 @@ extern "C" {
 #define MSQ_EPI_BIAS_RESID 3 /* C = acc + bias[n] + aux[m,n]  (aux fp32)   */
 #define MSQ_EPI_RELU_MASK 4  /* C = acc * (aux[m,n] > 0)                   */
 #define MSQ_EPI_ACCUM 5      /* C += acc                     (C fp32)      */
+/* C = aux[m,n] + dropout(acc + bias[n]) (aux fp32): msq_gemm_dropout only   */
+#define MSQ_EPI_BIAS_DROP_RESID 6
 
 const char* msq_last_error(void);
 int msq_version(void);
@@ -71,6 +73,13 @@ int msq_layernorm_bwd(float* dx_acc, void* dx_copy, int copy_dtype, float* dgamm
                       int dy_dtype, const float* x, const float* mean, const float* rstd, const float* gamma,
                       int64_t rows, int64_t d, int64_t seg_len, int64_t seg_skip, void* workspace, void* stream);
 
+/* msq_layernorm_bwd whose dx_copy is the gradient of a dropped branch: the
+ * copy of row map(r) is multiplied by keep(seed, site, map(r), col)/(1-p)
+ * (the mask msq_gemm_dropout drew in the forward); dx_acc stays unmasked.   */
+int msq_layernorm_bwd_dropout(float* dx_acc, void* dx_copy, int copy_dtype, float* dgamma, float* dbeta,
+                              const void* dy, int dy_dtype, const float* x, const float* mean, const float* rstd,
+                              const float* gamma, int64_t rows, int64_t d, int64_t seg_len, int64_t seg_skip,
+                              uint32_t seed, uint32_t site, float p, void* workspace, void* stream);
 /* ---- GEMM (nn.Linear fwd/bwd: model_transformer.py:46,57-59,97-100,147;
  * Mamba2 in_proj/out_proj). C[b] = op(A[b]) . op(B[b]) with
  *   ta = 0: A stored [M,K] (K contiguous)     ta = 1: A stored [K,M]
@@ -84,6 +93,14 @@ int msq_gemm(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, const v
              int64_t strideC, int64_t batch, int epilogue, const float* bias, const void* aux, int aux_dtype,
              int64_t ld_aux, int64_t stride_aux, void* stream);
 
+/* msq_gemm with nn.Dropout(p) on acc + bias before the residual add
+ * (model_transformer.py:51 proj, :101 FFN output): epilogue
+ * MSQ_EPI_BIAS_DROP_RESID; element (m, n) is kept iff
+ * hash(seed, site, row m, col n) >= p*2^32 (csrc/common.h) and scaled by 1/(1-p). */
+int msq_gemm_dropout(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                     int64_t strideA, const void* B, int64_t ldb, int64_t strideB, void* C, int c_dtype, int64_t ldc,
+                     int64_t strideC, int64_t batch, int epilogue, const float* bias, const void* aux, int aux_dtype,
+                     int64_t ld_aux, int64_t stride_aux, uint32_t seed, uint32_t site, float p, void* stream);
 /* column sums (bias gradients): out[c] (+)= sum_r x[r, c]                      */
 size_t msq_colsum_workspace(int64_t rows, int64_t cols);
 int msq_colsum(float* out, int accumulate, const void* x, int dtype, int64_t rows, int64_t cols, int64_t ld,
@@ -109,12 +126,32 @@ int msq_adam_step(float* p, const float* g, float* m, float* v, void* p_shadow, 
 int msq_relattn_fwd(int dtype, void* out, int64_t ld_out, float* lse, const void* qkv, int64_t ld_qkv,
                     const void* R, int64_t B, int64_t S, int64_t H, int64_t hs, int64_t S_max, float scale,
                     int64_t n_meta, void* stream);
+/* ---- attention-probability dropout (nn.Dropout(p) on the softmax output,
+ * model_transformer.py:62,80; active in train() mode, config.yaml:16 p = 0.01).
+ * Keep bits of one layer, both layouts [B, H, S, msq_dropout_mask_ld(S)] uint32:
+ * rowmask[b,h,i][w] bit t = keep(i, 32w+t), colmask[b,h,j][w] bit t =
+ * keep(32w+t, j); keep(i,j) = hash(seed, site0 + b*H + h, i, j) >= p*2^32
+ * (counter-based, csrc/common.h). Only the causal lower block triangle is
+ * written.                                                                  */
+int64_t msq_dropout_mask_ld(int64_t S);
+int msq_dropout_attn_mask(uint32_t* rowmask, uint32_t* colmask, int64_t B, int64_t H, int64_t S, uint32_t seed,
+                          uint32_t site0, float p, void* stream);
+/* msq_relattn_fwd / _bwd with dropout p on the attention probabilities: the
+ * masks of msq_dropout_attn_mask; kept probabilities are scaled by 1/(1-p);
+ * lse stays the undropped softmax normaliser. p = 0 = the plain entry points. */
+int msq_relattn_fwd_dropout(int dtype, void* out, int64_t ld_out, float* lse, const void* qkv, int64_t ld_qkv,
+                            const void* R, int64_t B, int64_t S, int64_t H, int64_t hs, int64_t S_max, float scale,
+                            int64_t n_meta, const uint32_t* rowmask, const uint32_t* colmask, float p, void* stream);
 size_t msq_relattn_bwd_workspace(int dtype, int64_t B, int64_t S, int64_t H);
 /* dqkv (same layout as qkv) is overwritten; dR (fp32 [H, S_max, hs]) accumulates. */
 int msq_relattn_bwd(int dtype, void* dqkv, int64_t ld_dqkv, float* dR, const void* dout, int64_t ld_dout,
                     const void* out, const float* lse, const void* qkv, int64_t ld_qkv, const void* R, int64_t B,
                     int64_t S, int64_t H, int64_t hs, int64_t S_max, float scale, int64_t n_meta, void* workspace,
                     void* stream);
+int msq_relattn_bwd_dropout(int dtype, void* dqkv, int64_t ld_dqkv, float* dR, const void* dout, int64_t ld_dout,
+                            const void* out, const float* lse, const void* qkv, int64_t ld_qkv, const void* R,
+                            int64_t B, int64_t S, int64_t H, int64_t hs, int64_t S_max, float scale, int64_t n_meta,
+                            const uint32_t* rowmask, const uint32_t* colmask, float p, void* workspace, void* stream);
 
 /* ---- grammar-weighted filtered loss (train.py:79-138; CrossEntropyLoss,
  * train_parallel.py:156,179). logits [B,T,ld] (ld >= V, ld % 4 == 0) in dtype;

@@ -2,8 +2,12 @@
 relative-position Transformer (models/transformer/model_transformer.py:8-165).
 
 Parameters are a dict keyed by the reference's state_dict names; autograd
-provides the backward. Dropout is 0 (the parity fixtures are recorded with
-``cc.config.values.dropout = params.dropout = 0``).
+provides the backward. The golden fixtures are recorded with dropout 0
+(``cc.config.values.dropout = params.dropout = 0``); ``forward(..., drop=(seed,
+p))`` applies nn.Dropout(p) at the reference's three sites (attention
+probabilities :80, proj output :51, FFN output :101) with the keep masks of
+oracle/dropout.py (the build's counter-based stream), so the build's training
+mode can be checked element for element.
 """
 import math
 
@@ -37,12 +41,12 @@ def skew_index(S: int):
     return row, (pc - 1).clamp(min=0), pc == 0
 
 
-def rel_head(x, wq, wk, wv, R, scale):
+def rel_head(x, wq, wk, wv, R, scale, keep=None, keep_scale=1.0):
     """One HeadRelPos (model_transformer.py:64-82): scores (q.k + skew(q.R)) * scale."""
-    return rel_attention(x @ wq.t(), x @ wk.t(), x @ wv.t(), R, scale)
+    return rel_attention(x @ wq.t(), x @ wk.t(), x @ wv.t(), R, scale, keep, keep_scale)
 
 
-def rel_attention(q, k, v, R, scale):
+def rel_attention(q, k, v, R, scale, keep=None, keep_scale=1.0):
     """Attention core of HeadRelPos given q, k, v [B,S,hs] and R [>=S, hs]."""
     S = q.shape[1]
     ac = q @ k.transpose(1, 2)
@@ -51,29 +55,46 @@ def rel_attention(q, k, v, R, scale):
     bd = qr[:, row, col].masked_fill(pad, 0.0)
     s = (ac + bd) * scale
     s = s.masked_fill(~allowed_mask(S), float("-inf"))
-    return torch.softmax(s, dim=-1) @ v
+    w = torch.softmax(s, dim=-1)
+    if keep is not None:  # self.dropout(attn) (model_transformer.py:80)
+        w = w * keep * keep_scale
+    return w @ v
 
 
-def forward(p: dict, idx: torch.Tensor, meta: torch.Tensor, n_layer: int, n_heads: int) -> torch.Tensor:
+def forward(p: dict, idx: torch.Tensor, meta: torch.Tensor, n_layer: int, n_heads: int, drop=None) -> torch.Tensor:
     """Transformer.forward (model_transformer.py:149-165): meta rows first,
-    pre-LN blocks, LN_f, lm_head, keep the last T rows."""
+    pre-LN blocks, LN_f, lm_head, keep the last T rows. drop=(seed, p): train
+    mode with nn.Dropout(p) (masks from oracle/dropout.py)."""
+    from . import dropout as odrop
     B, T = idx.shape
     x = torch.cat([p["metadata_embedding_table.weight"][meta], p["token_embedding_table.weight"][idx]], dim=1)
     C = x.shape[-1]
     scale = C ** -0.5                         # n_embd^-1/2, not head_size (model_transformer.py:65,77)
+    S = x.shape[1]
+    if drop is not None:
+        seed, pd = drop
+        ks = odrop.scale(pd)
+
+        def site(y, s):  # nn.Dropout on a [B, S, C] branch output; rows = flat b*S + i
+            k = torch.from_numpy(odrop.keep(seed, s, B * S, y.shape[-1], pd)).view(B, S, -1)
+            return y * k * ks
     for l in range(n_layer):
         pre = f"blocks.{l}."
         h = F.layer_norm(x, (C,), p[pre + "ln1.weight"], p[pre + "ln1.bias"], 1e-5)
+        keep = torch.from_numpy(odrop.attn_keep(drop[0], l, B, n_heads, S, drop[1])) if drop is not None else None
         heads = []
         for hh in range(n_heads):
             hp = f"{pre}sa.heads.{hh}."
             heads.append(rel_head(h, p[hp + "query.weight"], p[hp + "key.weight"], p[hp + "value.weight"],
-                                  p[hp + "rel_pos_emb"], scale))
+                                  p[hp + "rel_pos_emb"], scale, keep[:, hh] if keep is not None else None,
+                                  odrop.scale(drop[1]) if drop is not None else 1.0))
         att = torch.cat(heads, dim=-1)
-        x = x + F.linear(att, p[pre + "sa.proj.weight"], p[pre + "sa.proj.bias"])
+        y = F.linear(att, p[pre + "sa.proj.weight"], p[pre + "sa.proj.bias"])
+        x = x + (site(y, odrop.PROJ + l) if drop is not None else y)
         h = F.layer_norm(x, (C,), p[pre + "ln2.weight"], p[pre + "ln2.bias"], 1e-5)
         h = torch.relu(F.linear(h, p[pre + "ffwd.net.0.weight"], p[pre + "ffwd.net.0.bias"]))
-        x = x + F.linear(h, p[pre + "ffwd.net.2.weight"], p[pre + "ffwd.net.2.bias"])
+        y = F.linear(h, p[pre + "ffwd.net.2.weight"], p[pre + "ffwd.net.2.bias"])
+        x = x + (site(y, odrop.FFN + l) if drop is not None else y)
     x = F.layer_norm(x, (C,), p["ln_f.weight"], p["ln_f.bias"], 1e-5)
     return F.linear(x, p["lm_head.weight"], p["lm_head.bias"])[:, -T:, :]
 
