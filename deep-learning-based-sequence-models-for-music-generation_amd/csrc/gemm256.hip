@@ -363,11 +363,21 @@ bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dt
     g.ksplit = 1;
     g.kper = (g.K + 63) / 64 * 64;
     if (epi == MSQ_EPI_ACCUM) {
-        // split-K for the weight-gradient products: about one block per CU
-        int64_t ks = (256 + tiles - 1) / tiles;
-        ks = std::min<int64_t>(ks, std::max<int64_t>(1, g.K / 2048));
-        if (ks > 1) {
-            g.kper = ((g.K + ks - 1) / ks + 63) / 64 * 64;
+        // split-K for the weight-gradient products (fp32 atomics): pick the
+        // split that minimises  waves(ks) x (k-steps per block + C), one block
+        // per CU, C ~ prologue + atomic epilogue in k-step units. E.g. lm_head
+        // dW (280 tiles, K = 65536): ks = 8 -> 9 waves of 136, vs ks = 1 -> 2
+        // waves of 1032 (the second one 24/256 full).
+        const int64_t ksteps = (g.K + 63) / 64;
+        const int64_t C = 8;
+        int64_t best = 1, best_cost = INT64_MAX;
+        for (int64_t ks = 1; ks <= 32 && ksteps / ks >= 16; ++ks) {
+            const int64_t waves = (tiles * ks + 255) / 256;
+            const int64_t cost = waves * ((ksteps + ks - 1) / ks + C);
+            if (cost < best_cost) best = ks, best_cost = cost;
+        }
+        if (best > 1) {
+            g.kper = ((g.K + best - 1) / best + 63) / 64 * 64;
             g.ksplit = (int)((g.K + g.kper - 1) / g.kper);
         }
     }

@@ -16,7 +16,7 @@ from midiseq import ops  # noqa: E402
 from midiseq import _lib as L  # noqa: E402
 
 
-def timeit(fn, iters=10, warm=3):
+def timeit(fn, iters=30, warm=5):
     for _ in range(warm):
         fn()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -43,7 +43,10 @@ def main():
         ("w2   dW  TT accum", d, 4 * d, M, 1, 1, L.EPI_ACCUM),
         ("w1   dW  TT accum", 4 * d, d, M, 1, 1, L.EPI_ACCUM),
         ("proj dW  TT accum", d, d, M, 1, 1, L.EPI_ACCUM),
-        ("lm   dW  TT accum", 17914, d, 32 * 2048, 1, 1, L.EPI_ACCUM),
+        ("lm   dW  TT accum", 17920, d, 32 * 2048, 1, 1, L.EPI_ACCUM),
+        ("qkv  dW  TT accum", 3 * d, d, M, 1, 1, L.EPI_ACCUM),
+        ("proj fwd NT +bias+resid", M, d, d, 0, 0, L.EPI_BIAS_RESID),
+        ("qkv  dX  NN", M, d, 3 * d, 0, 1, L.EPI_NONE),
     ]
     for name, m, n, k, ta, tb, epi in cases:
         pad = lambda r, c: torch.randn(r, (c + 7) // 8 * 8, device=dev).to(bf)[:, :c]  # noqa: E731
@@ -58,11 +61,11 @@ def main():
                   bias=bias if epi in (L.EPI_BIAS, L.EPI_BIAS_RELU, L.EPI_BIAS_RESID) else None, aux=aux)
         fl = 2.0 * m * n * k
         res = {}
-        for tag, env in (("g128", "1"), ("g256", None)):
+        for tag, env in (("g128", "MSQ_GEMM128"), ("g256", None)):
+            os.environ.pop("MSQ_GEMM128", None)
+            os.environ.pop("MSQ_GEMM_NOTAIL", None)
             if env:
-                os.environ["MSQ_GEMM128"] = env
-            else:
-                os.environ.pop("MSQ_GEMM128", None)
+                os.environ[env] = "1"
             out.zero_()
             ms = timeit(lambda: ops.gemm(A, Bm, **kw))
             res[tag] = (ms, fl / ms / 1e9)
@@ -71,6 +74,7 @@ def main():
                 ops.gemm(A, Bm, **kw)
                 got = out.float()
         os.environ.pop("MSQ_GEMM128", None)
+        os.environ.pop("MSQ_GEMM_NOTAIL", None)
         At = A.t() if ta else A
         Bt = Bm if tb else Bm.t()
         ms = timeit(lambda: torch.matmul(At, Bt))
