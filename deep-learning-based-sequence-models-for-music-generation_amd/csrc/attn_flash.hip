@@ -474,12 +474,16 @@ __global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, int64_t ldr, int64_
 int64_t flash_dqr_ld(int64_t S) { return (S + 7) / 8 * 8; }
 
 // workspace: dQR bf16 [H][B][S][ldr] | D f32 [B][H][S] | meta_ds f32 [B][H][8][8] | dq_ac f32 [B*S][H*HS]
+//            | dR split-K partials f32 [ksplit][H][S][HS]
 static size_t align256(size_t x) { return (x + 255) / 256 * 256; }
+static size_t dr_ws_bytes(int64_t B, int64_t S, int64_t H) {
+    return splitk_ws_bytes(S, HS, H, gemm_bf16_tri_ksplit(2, S, HS, B * S, S, H));
+}
 
 size_t flash_bwd_workspace(int64_t B, int64_t S, int64_t H) {
     const int64_t ldr = flash_dqr_ld(S);
     return align256((size_t)H * B * S * ldr * 2) + align256((size_t)B * H * S * 4) + align256((size_t)B * H * 64 * 4) +
-           align256((size_t)B * S * H * HS * 4);
+           align256((size_t)B * S * H * HS * 4) + align256(dr_ws_bytes(B, S, H));
 }
 
 int flash_fwd(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s) {
@@ -504,6 +508,8 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     float* meta_ds = (float*)p;
     p += align256((size_t)B * H * 64 * 4);
     float* dq_ac = (float*)p;
+    p += align256((size_t)B * S * H * HS * 4);
+    float* dr_ws = (float*)p;
 
     hipLaunchKernelGGL(dqr_band_zero_kernel, dim3((unsigned)((H * B * S + 3) / 4)), dim3(256), 0, s, dqr, ldr, S,
                        H * B * S);
@@ -529,7 +535,7 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     // dR[h][r] += sum_{b,i} dQR[h][b,i][r] q_{b,i}   (batched over heads; per batch
     // segment only i >= S-1-r contributes: tri 2, split over segments)
     rc = gemm_bf16_tri(2, S, 1, 1, S, HS, B * S, dqr, ldr, B * S * ldr, a.qkv, a.ldq, HS, dR, MSQ_F32, HS,
-                       a.S_max * HS, H, MSQ_EPI_ACCUM, nullptr, MSQ_F32, 0, 0, s);
+                       a.S_max * HS, H, MSQ_EPI_ACCUM, nullptr, MSQ_F32, 0, 0, s, dr_ws, dr_ws_bytes(B, S, H));
     if (rc) return msq_set_error(MSQ_ERR_ARG, "flash_bwd: dR product");
     hipLaunchKernelGGL(flash_bwd_meta_kernel, dim3(1, (unsigned)H, (unsigned)B), dim3(HS), 0, s, a, meta_ds, dqkv, ldd,
                        dR);

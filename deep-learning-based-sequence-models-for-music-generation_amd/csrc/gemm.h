@@ -23,7 +23,17 @@ struct GemmArgs {
     // MSQ_EPI_BIAS_DROP_RESID: drop_base = drop_base(seed, site), keep iff bits >= drop_thr
     uint32_t drop_base, drop_thr;
     float drop_scale;
+    // split-K partials (ACCUM, ksplit > 1): slice s of batch z at
+    // ws + ((s * batch + z) * M) * N (N % 4 == 0); null = fp32 atomics into C
+    float* ws;
 };
+
+// bytes of the split-K partial workspace an ACCUM product with this split needs
+inline size_t splitk_ws_bytes(int64_t M, int64_t N, int64_t batch, int ksplit) {
+    return ksplit > 1 && N % 4 == 0 ? (size_t)ksplit * batch * M * N * 4 : 0;
+}
+// C[z][m][n] += sum_s ws[s][z][m][n] (gemm.hip)
+void splitk_reduce(const GemmArgs& g, hipStream_t s);
 
 // dropout(v + bias) of one lane's 4 outputs C[m][n..n+3] (nn.Dropout, common.h hash)
 __device__ __forceinline__ f32x4 epi_drop(const GemmArgs& g, int64_t m, int64_t n, f32x4 v) {
@@ -54,7 +64,12 @@ __device__ __forceinline__ f32x4 epi_load(const T* p, int nv) {
 
 // Applies the epilogue to one lane's 4 consecutive outputs C[m][n..n+3].
 template <int EPI, typename TC, typename TX>
-__device__ __forceinline__ void epi_apply(const GemmArgs& g, TC* C, const TX* X, int64_t m, int64_t n, f32x4 v) {
+__device__ __forceinline__ void epi_apply(const GemmArgs& g, TC* C, const TX* X, int64_t m, int64_t n, f32x4 v,
+                                          float* wsp = nullptr) {
+    if (EPI == MSQ_EPI_ACCUM && wsp) {  // split-K partial, reduced by splitk_reduce
+        store4(wsp + m * g.N + n, v);
+        return;
+    }
     const int nv = g.vec ? (int)min<int64_t>(4, g.N - n) : -(int)min<int64_t>(4, g.N - n);
     if ((EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID ||
          EPI == MSQ_EPI_BIAS_DROP_RESID) && g.bias)
@@ -82,9 +97,20 @@ __device__ __forceinline__ void epi_apply(const GemmArgs& g, TC* C, const TX* X,
 
 // 256x256 kernel family: returns false when the problem does not fit its
 // preconditions (the caller then uses the 128x128 kernel).
-bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s);
+bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, size_t ws_bytes,
+                    hipStream_t s);
+// fills tiles / ksplit / kper (and descriptor extents) of the 256 tile; false if it does not apply
+bool gemm256_plan(GemmArgs& g, int ta, int tb, int epi);
 
 // bf16 GEMM with a triangular K range (GemmArgs::tri); same operand conventions as msq_gemm
 int gemm_bf16_tri(int tri, int64_t seg, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                   int64_t sA, const void* B, int64_t ldb, int64_t sB, void* C, int c_dtype, int64_t ldc, int64_t sC,
-                  int64_t batch, int epi, const void* aux, int aux_dtype, int64_t ldx, int64_t sX, hipStream_t s);
+                  int64_t batch, int epi, const void* aux, int aux_dtype, int64_t ldx, int64_t sX, hipStream_t s,
+                  float* ws = nullptr, size_t ws_bytes = 0);
+// K split gemm_bf16_tri uses (its split-K workspace: splitk_ws_bytes(M, N, batch, this))
+int gemm_bf16_tri_ksplit(int tri, int64_t M, int64_t N, int64_t K, int64_t seg, int64_t batch);
+extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                           int64_t strideA, const void* B, int64_t ldb, int64_t strideB, void* C, int c_dtype,
+                           int64_t ldc, int64_t strideC, int64_t batch, int epilogue, const float* bias,
+                           const void* aux, int aux_dtype, int64_t ld_aux, int64_t stride_aux, uint32_t seed,
+                           uint32_t site, float p, void* ws, int64_t ws_bytes, void* stream);

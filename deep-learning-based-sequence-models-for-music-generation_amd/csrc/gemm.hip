@@ -230,6 +230,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
                 for (int t = 0; t < 4; ++t) v[t] = x[t] > 0.f ? v[t] : 0.f;
             }
             TC* cp = C + m * g.ldc + n;
+            if (EPI == MSQ_EPI_ACCUM && g.ksplit > 1 && g.ws) {  // partial, reduced by splitk_reduce
+                store4(g.ws + (((int64_t)kslice * g.batch + bz) * g.M + m) * g.N + n, v);
+                continue;
+            }
             if (EPI == MSQ_EPI_ACCUM && g.ksplit > 1) {
                 const int na = nv < 0 ? -nv : nv;
                 for (int t = 0; t < na; ++t) atomicAdd((float*)cp + t, v[t]);
@@ -344,11 +348,44 @@ int dispatch_epi(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hipS
     return -1;
 }
 
+// C[z][m][n..n+3] += sum_s ws[s][z][m][n..n+3]  (N % 4 == 0; one lane per 4 outputs)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ C, int64_t ldc, int64_t sC,
+                                                            const float* __restrict__ ws, int64_t M, int64_t N,
+                                                            int64_t batch, int ksplit) {
+    const int64_t nq = N / 4, per = M * nq, total = batch * per, slice = batch * M * N;
+    for (int64_t e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+        const int64_t z = e / per, r = e - z * per, m = r / nq, n = (r - m * nq) * 4;
+        const float* w = ws + (z * M + m) * N + n;
+        f32x4 v = load4(w);
+        for (int k = 1; k < ksplit; ++k) v += load4(w + k * slice);
+        float* cp = C + z * sC + m * ldc + n;
+        if (((uintptr_t)cp & 15) == 0) {
+            store4(cp, v + load4(cp));
+        } else {
+            for (int t = 0; t < 4; ++t) cp[t] += v[t];
+        }
+    }
+}
+
 }  // namespace
+
+void splitk_reduce(const GemmArgs& g, hipStream_t s) {
+    const int64_t total = (int64_t)g.batch * g.M * (g.N / 4);
+    const unsigned nb = (unsigned)std::min<int64_t>((total + 255) / 256, 256 * 16);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nb), dim3(256), 0, s, (float*)g.C, g.ldc, g.sC, g.ws, g.M, g.N,
+                       (int64_t)g.batch, g.ksplit);
+}
+
+int gemm_bf16_tri_ksplit(int tri, int64_t M, int64_t N, int64_t K, int64_t seg, int64_t batch) {
+    if (tri != 2) return 1;
+    const int64_t nb = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * batch, nseg = K / seg;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(nseg, (1024 + nb - 1) / nb));
+}
 
 int gemm_bf16_tri(int tri, int64_t seg, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                   int64_t sA, const void* B, int64_t ldb, int64_t sB, void* C, int c_dtype, int64_t ldc, int64_t sC,
-                  int64_t batch, int epi, const void* aux, int aux_dtype, int64_t ldx, int64_t sX, hipStream_t s) {
+                  int64_t batch, int epi, const void* aux, int aux_dtype, int64_t ldx, int64_t sX, hipStream_t s,
+                  float* ws, size_t ws_bytes) {
     GemmArgs g{};
     g.M = M; g.N = N; g.K = K;
     g.A = A; g.lda = lda; g.sA = sA;
@@ -363,12 +400,14 @@ int gemm_bf16_tri(int tri, int64_t seg, int ta, int tb, int64_t M, int64_t N, in
     g.seg = seg;
     g.ksplit = 1;
     g.kper = ((K + BK - 1) / BK) * BK;
-    if (tri == 2) {  // split the segments so that about 1024 blocks (4 per CU) run
-        const int64_t nb = (int64_t)g.tiles_m * g.tiles_n * batch, nseg = K / seg;
-        g.ksplit = (int)std::max<int64_t>(1, std::min<int64_t>(nseg, (1024 + nb - 1) / nb));
-    }
+    // tri 2: split the segments so that about 1024 blocks (4 per CU) run
+    g.ksplit = gemm_bf16_tri_ksplit(tri, M, N, K, seg, batch);
+    if (epi == MSQ_EPI_ACCUM && g.ksplit > 1 && ws && c_dtype == MSQ_F32 &&
+        splitk_ws_bytes(M, N, batch, g.ksplit) && ws_bytes >= splitk_ws_bytes(M, N, batch, g.ksplit))
+        g.ws = ws;
     const int rc = c_dtype == MSQ_BF16 ? dispatch_epi<true, bf16>(g, ta, tb, epi, aux_dtype, s)
                                        : dispatch_epi<true, float>(g, ta, tb, epi, aux_dtype, s);
+    if (!rc && g.ws) splitk_reduce(g, s);
     return rc;
 }
 
@@ -381,11 +420,50 @@ extern "C" int msq_gemm(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t
                             epilogue, bias, aux, aux_dtype, ld_aux, stride_aux, 0u, 0u, 0.f, stream);
 }
 
+namespace {
+// split-K of the 128 tile for an ACCUM product (skinny-output weight gradients)
+void plan128_ksplit(GemmArgs& g, int dtype, int epilogue) {
+    g.ksplit = 1;
+    g.kper = ((g.K + BK - 1) / BK) * BK;
+    if (dtype == MSQ_BF16 && epilogue == MSQ_EPI_ACCUM) {
+        const int64_t nb = (int64_t)g.tiles_m * g.tiles_n * g.batch;
+        int64_t ks = (1024 + nb - 1) / nb;
+        ks = std::min<int64_t>(ks, std::max<int64_t>(1, g.K / 1024));
+        if (ks > 1) {
+            g.kper = ((g.K + ks - 1) / ks + BK - 1) / BK * BK;
+            g.ksplit = (int)((g.K + g.kper - 1) / g.kper);
+        }
+    }
+}
+}  // namespace
+
+extern "C" int64_t msq_gemm_workspace_size(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K,
+                                           int64_t lda, int64_t ldb, int64_t batch, int epilogue) {
+    if (epilogue != MSQ_EPI_ACCUM || dtype != MSQ_BF16 || M <= 0 || N <= 0 || K <= 0 || batch <= 0) return 0;
+    GemmArgs g{};
+    g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.batch = (int)batch;
+    if (!getenv("MSQ_GEMM128") && gemm256_plan(g, ta, tb, epilogue))
+        return (int64_t)splitk_ws_bytes(M, N, batch, g.ksplit);
+    g.tiles_m = (int)((M + BM - 1) / BM);
+    g.tiles_n = (int)((N + BN - 1) / BN);
+    plan128_ksplit(g, dtype, epilogue);
+    return (int64_t)splitk_ws_bytes(M, N, batch, g.ksplit);
+}
+
 extern "C" int msq_gemm_dropout(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A,
                                 int64_t lda, int64_t strideA, const void* B, int64_t ldb, int64_t strideB, void* C,
                                 int c_dtype, int64_t ldc, int64_t strideC, int64_t batch, int epilogue,
                                 const float* bias, const void* aux, int aux_dtype, int64_t ld_aux, int64_t stride_aux,
                                 uint32_t seed, uint32_t site, float p, void* stream) {
+    return msq_gemm_ex(dtype, ta, tb, M, N, K, A, lda, strideA, B, ldb, strideB, C, c_dtype, ldc, strideC, batch,
+                       epilogue, bias, aux, aux_dtype, ld_aux, stride_aux, seed, site, p, nullptr, 0, stream);
+}
+
+extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                           int64_t strideA, const void* B, int64_t ldb, int64_t strideB, void* C, int c_dtype,
+                           int64_t ldc, int64_t strideC, int64_t batch, int epilogue, const float* bias,
+                           const void* aux, int aux_dtype, int64_t ld_aux, int64_t stride_aux, uint32_t seed,
+                           uint32_t site, float p, void* ws, int64_t ws_bytes, void* stream) {
     MSQ_CHECK_ARG(dtype == MSQ_BF16 || dtype == MSQ_F32, "msq_gemm: bad dtype %d", dtype);
     MSQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && batch > 0, "msq_gemm: empty problem");
     MSQ_CHECK_ARG(epilogue >= MSQ_EPI_NONE && epilogue <= MSQ_EPI_BIAS_DROP_RESID, "msq_gemm: bad epilogue");
@@ -422,23 +500,21 @@ extern "C" int msq_gemm_dropout(int dtype, int ta, int tb, int64_t M, int64_t N,
         if (aux) vec = vec && (ld_aux % 4 == 0) && (stride_aux % 4 == 0) && ((uintptr_t)aux % (4 * xsz) == 0);
         g.vec = vec ? 1 : 0;
     }
-    // split-K for skinny-output weight-gradient products (C += acc only)
-    g.ksplit = 1;
-    g.kper = ((K + BK - 1) / BK) * BK;
-    if (dtype == MSQ_BF16 && epilogue == MSQ_EPI_ACCUM) {
-        const int64_t nb = (int64_t)g.tiles_m * g.tiles_n * batch;
-        int64_t ks = (1024 + nb - 1) / nb;
-        ks = std::min<int64_t>(ks, std::max<int64_t>(1, K / 1024));
-        if (ks > 1) {
-            g.kper = ((K + ks - 1) / ks + BK - 1) / BK * BK;
-            g.ksplit = (int)((K + g.kper - 1) / g.kper);
-        }
-    }
+    MSQ_CHECK_ARG(ws_bytes >= 0 && (ws || ws_bytes == 0), "msq_gemm_ex: bad workspace");
+    MSQ_CHECK_ARG(((uintptr_t)ws % 16) == 0, "msq_gemm_ex: workspace must be 16-B aligned");
+    // split-K for skinny-output weight-gradient products (C += acc only): the
+    // partial tiles go to ws when it is large enough, else fp32 atomics into C
+    plan128_ksplit(g, dtype, epilogue);
+    g.ws = (float*)ws;
     hipStream_t s = (hipStream_t)stream;
-    if (dtype == MSQ_BF16 && !getenv("MSQ_GEMM128") && gemm256_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, s)) {
+    if (dtype == MSQ_BF16 && !getenv("MSQ_GEMM128") &&
+        gemm256_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, (size_t)ws_bytes, s)) {
         MSQ_LAUNCH_CHECK();
         return MSQ_OK;
     }
+    if (!(epilogue == MSQ_EPI_ACCUM && g.ksplit > 1 && splitk_ws_bytes(M, N, batch, g.ksplit) &&
+          (size_t)ws_bytes >= splitk_ws_bytes(M, N, batch, g.ksplit)))
+        g.ws = nullptr;
     int rc;
     if (dtype == MSQ_BF16)
         rc = c_dtype == MSQ_BF16 ? dispatch_epi<true, bf16>(g, ta, tb, epilogue, aux_dtype, s)
@@ -447,6 +523,7 @@ extern "C" int msq_gemm_dropout(int dtype, int ta, int tb, int64_t M, int64_t N,
         rc = c_dtype == MSQ_BF16 ? dispatch_epi<false, bf16>(g, ta, tb, epilogue, aux_dtype, s)
                                  : dispatch_epi<false, float>(g, ta, tb, epilogue, aux_dtype, s);
     if (rc) return msq_set_error(MSQ_ERR_ARG, "msq_gemm: unsupported combination");
+    if (g.ws) splitk_reduce(g, s);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }

@@ -296,6 +296,8 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(GemmArgs g) {
     // epilogue: lane holds C[m][n..n+3]
     TC* C = (TC*)g.C + bz * g.sC;
     const TX* X = (const TX*)g.aux + (g.aux ? bz * g.sX : 0);
+    float* wsp = (EPI == MSQ_EPI_ACCUM && g.ksplit > 1 && g.ws) ? g.ws + ((int64_t)kslice * g.batch + bz) * g.M * g.N
+                                                                 : nullptr;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -308,7 +310,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(GemmArgs g) {
                 for (int j = 0; j < 2; ++j) {
                     const int64_t n = n0 + b * 128 + wc * 32 + j * 16 + 4 * (lane >> 4);
                     if (n >= g.N) continue;
-                    epi_apply<EPI, TC, TX>(g, C, X, m, n, acc[a][b][i][j]);
+                    epi_apply<EPI, TC, TX>(g, C, X, m, n, acc[a][b][i][j], wsp);
                 }
         }
 }
@@ -351,7 +353,9 @@ void dispatch_epi(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hip
 
 }  // namespace
 
-bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s) {
+// ksplit / kper / tiles of the 256 tile for this problem, or false when its
+// preconditions fail (the caller then uses the 128x128 kernel)
+bool gemm256_plan(GemmArgs& g, int ta, int tb, int epi) {
     // preconditions: chunks of 8 never straddle an edge; extents fit a descriptor
     if ((ta ? g.M : g.K) % 8 || (tb ? g.N : g.K) % 8) return false;
     const int64_t aext = ((ta ? g.K : g.M) - 1) * g.lda + (ta ? g.M : g.K);
@@ -363,9 +367,9 @@ bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dt
     g.ksplit = 1;
     g.kper = (g.K + 63) / 64 * 64;
     if (epi == MSQ_EPI_ACCUM) {
-        // split-K for the weight-gradient products (fp32 atomics): pick the
-        // split that minimises  waves(ks) x (k-steps per block + C), one block
-        // per CU, C ~ prologue + atomic epilogue in k-step units. E.g. lm_head
+        // split-K for the weight-gradient products: pick the split that
+        // minimises  waves(ks) x (k-steps per block + C), one block per CU,
+        // C ~ prologue + partial-tile epilogue in k-step units. E.g. lm_head
         // dW (280 tiles, K = 65536): ks = 8 -> 9 waves of 136, vs ks = 1 -> 2
         // waves of 1032 (the second one 24/256 full).
         const int64_t ksteps = (g.K + 63) / 64;
@@ -385,7 +389,17 @@ bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dt
     if (tiles * g.ksplit < 128) return false;
     g.a_ext = (uint32_t)(aext * 2);
     g.b_ext = (uint32_t)(bext * 2);
+    return true;
+}
+
+bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, size_t ws_bytes,
+                    hipStream_t s) {
+    if (!gemm256_plan(g, ta, tb, epi)) return false;
+    if (!g.ws || ws_bytes < splitk_ws_bytes(g.M, g.N, g.batch, g.ksplit) ||
+        !splitk_ws_bytes(g.M, g.N, g.batch, g.ksplit))
+        g.ws = nullptr;
     if (c_dtype == MSQ_BF16) dispatch_epi<bf16>(g, ta, tb, epi, aux_dtype, s);
     else dispatch_epi<float>(g, ta, tb, epi, aux_dtype, s);
+    if (epi == MSQ_EPI_ACCUM && g.ws) splitk_reduce(g, s);
     return true;
 }

@@ -46,9 +46,30 @@ def gemm(A, B, *, ta=False, tb=False, out=None, out_dtype=None, epilogue=L.EPI_N
              dt(out), ldc, sC, batch, L.EPI_BIAS_DROP_RESID, ptr(bias), ptr(aux), axd, ldx, sX, int(drop[0]),
              int(drop[1]), float(drop[2]), stream())
         return out
+    if epilogue == L.EPI_ACCUM:
+        nws = L.lib().msq_gemm_workspace_size(dt(A), int(ta), int(tb), M, N, K, lda, ldb, batch, epilogue)
+        ws = _splitk_ws(A.device, nws) if nws > 0 else None
+        call("msq_gemm_ex", dt(A), int(ta), int(tb), M, N, K, ptr(A), lda, sA, ptr(B), ldb, sB, ptr(out), dt(out),
+             ldc, sC, batch, epilogue, ptr(bias), ptr(aux), axd, ldx, sX, 0, 0, 0.0, ptr(ws), nws if ws is not None
+             else 0, stream())
+        return out
     call("msq_gemm", dt(A), int(ta), int(tb), M, N, K, ptr(A), lda, sA, ptr(B), ldb, sB, ptr(out), dt(out), ldc,
          sC, batch, epilogue, ptr(bias), ptr(aux), axd, ldx, sX, stream())
     return out
+
+
+_WS = {}
+
+
+def _splitk_ws(device, nbytes):
+    """Split-K partial workspace of the weight-gradient GEMMs, one per
+    (device, stream): kept and grown, owned by torch's caching allocator."""
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(nbytes, 64 << 20), device=device, dtype=torch.uint8)
+        _WS[key] = ws
+    return ws
 
 
 def layernorm_fwd(x, gamma, beta, eps=1e-5, out_dtype=torch.float32, out=None, mean=None, rstd=None, seg=(0, 0)):

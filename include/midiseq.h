@@ -101,6 +101,19 @@ int msq_gemm_dropout(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K,
                      int64_t strideA, const void* B, int64_t ldb, int64_t strideB, void* C, int c_dtype, int64_t ldc,
                      int64_t strideC, int64_t batch, int epilogue, const float* bias, const void* aux, int aux_dtype,
                      int64_t ld_aux, int64_t stride_aux, uint32_t seed, uint32_t site, float p, void* stream);
+/* msq_gemm_dropout with a caller-owned split-K workspace. An ACCUM product
+ * whose K is split over workgroups (the weight gradients: the dW of
+ * nn.Linear in the DDP backward, train_parallel.py:166) writes each slice's
+ * fp32 partial tile to ws and one reduction adds them into C, instead of
+ * fp32 atomics; ws_bytes below msq_gemm_workspace_size(...) (or ws = NULL)
+ * falls back to the atomics. Other epilogues ignore ws.                      */
+int64_t msq_gemm_workspace_size(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, int64_t lda,
+                                int64_t ldb, int64_t batch, int epilogue);
+int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                int64_t strideA, const void* B, int64_t ldb, int64_t strideB, void* C, int c_dtype, int64_t ldc,
+                int64_t strideC, int64_t batch, int epilogue, const float* bias, const void* aux, int aux_dtype,
+                int64_t ld_aux, int64_t stride_aux, uint32_t seed, uint32_t site, float p, void* ws,
+                int64_t ws_bytes, void* stream);
 /* column sums (bias gradients): out[c] (+)= sum_r x[r, c]                      */
 size_t msq_colsum_workspace(int64_t rows, int64_t cols);
 int msq_colsum(float* out, int accumulate, const void* x, int dtype, int64_t rows, int64_t cols, int64_t ld,
