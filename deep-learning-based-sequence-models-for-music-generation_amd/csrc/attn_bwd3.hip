@@ -56,8 +56,8 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const 
                                                               const float* __restrict__ Dv,
                                                               const bf16* __restrict__ dout, int64_t ldo,
                                                               bf16* __restrict__ dqkv, int64_t ldd,
-                                                              bf16* __restrict__ dqr, int64_t ldr,
-                                                              float* __restrict__ meta_ds) {
+                                                              bf16* __restrict__ dqr, bf16* __restrict__ dsj,
+                                                              int64_t ldr, float* __restrict__ meta_ds) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sR = smem + O_R;
     const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, il = lane & 15;
@@ -77,6 +77,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const 
     const __amdgpu_buffer_rsrc_t rl = make_rsrc(Lp, (uint32_t)(S * 4));
     const __amdgpu_buffer_rsrc_t rd = make_rsrc(Dp, (uint32_t)(S * 4));
     bf16* qr_rows = dqr + ((int64_t)h * a.B + b) * S * ldr;
+    bf16* sj_rows = dsj + ((int64_t)h * a.B + b) * S * ldr;
     float* scw = (float*)(smem + O_S) + w * 2 * 16 * SCR;
     float* mbd = (float*)(smem + O_M);
     const int nm = (int)min<int64_t>(a.n_meta, S);
@@ -174,11 +175,16 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const 
     // waits for fresh stores
     bf16x8 ds_prev = (bf16x8){};
     int i0_prev = -1;
+    // dS twice: r-indexed (dQR, j <= i only) for the R products and j-indexed
+    // (dSj, 0 for j > i) for dq's K product (attn_dq.hip)
     auto store_ds = [&](const bf16x8& v, int ip) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const int i = ip + 16 * (e >> 2) + 4 * g + (e & 3);
-            if (i < S && jk <= i) qr_rows[(int64_t)i * ldr + (S - 1 - i + jk)] = v[e];
+            if (i < S && jk < S) {
+                if (jk <= i) qr_rows[(int64_t)i * ldr + (S - 1 - i + jk)] = v[e];
+                sj_rows[(int64_t)i * ldr + jk] = jk <= i ? v[e] : (bf16)0.f;
+            }
         }
     };
 
@@ -284,7 +290,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const 
 }  // namespace
 
 int flash_bwd_kv3(const AttnArgs& a, const float* lse, const float* Dv, const bf16* dout, int64_t ldo, bf16* dqkv,
-                  int64_t ldd, bf16* dqr, int64_t ldr, float* meta_ds, hipStream_t s) {
+                  int64_t ldd, bf16* dqr, bf16* dsj, int64_t ldr, float* meta_ds, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)flash_bwd_kv3_kernel<false>,
@@ -298,9 +304,9 @@ int flash_bwd_kv3(const AttnArgs& a, const float* lse, const float* Dv, const bf
     const dim3 grid((unsigned)((a.S + KB - 1) / KB), (unsigned)a.H, (unsigned)a.B);
     if (a.colmask)
         hipLaunchKernelGGL(flash_bwd_kv3_kernel<true>, grid, dim3(NT), LDS_BYTES, s, a, lse, Dv, dout, ldo, dqkv, ldd,
-                           dqr, ldr, meta_ds);
+                           dqr, dsj, ldr, meta_ds);
     else
         hipLaunchKernelGGL(flash_bwd_kv3_kernel<false>, grid, dim3(NT), LDS_BYTES, s, a, lse, Dv, dout, ldo, dqkv, ldd,
-                           dqr, ldr, meta_ds);
+                           dqr, dsj, ldr, meta_ds);
     return 0;
 }

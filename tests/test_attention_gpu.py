@@ -45,6 +45,7 @@ def _rel(a, b):
     (torch.bfloat16, 2, 134, 2, 128),
     (torch.bfloat16, 1, 262, 1, 128),
     (torch.bfloat16, 1, 7, 1, 128),
+    (torch.bfloat16, 2, 1030, 2, 128),
 ])
 def test_relattn_fwd_bwd(dtype, B, S, H, hs):
     S_max = S + 5

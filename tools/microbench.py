@@ -68,19 +68,10 @@ def main():
     dout = torch.randn(M, d, device=dev).to(bf)
     dqkv = torch.empty_like(qkv)
     dR = torch.zeros(H, S, 128, device=dev)
-    res = {}
-    for ver in ("1", "3"):
-        os.environ["MSQ_ATTN_BWD"] = ver
-        dR.zero_()
-        ms = timeit(lambda: attention.relattn_bwd(dout, out, lse, qkv, R, B, S, H, 128, scale, dqkv=dqkv, dR=dR),
-                    iters=3, warm=1)
-        rows.append((f"attn bwd v{ver}", ms, 2 * flops_att / ms / 1e9))
-        dR.zero_()
-        attention.relattn_bwd(dout, out, lse, qkv, R, B, S, H, 128, scale, dqkv=dqkv, dR=dR)
-        res[ver] = (dqkv.clone(), dR.clone())
-    del os.environ["MSQ_ATTN_BWD"]
-    print("bwd v3 vs v1: dqkv max diff", (res["3"][0].float() - res["1"][0].float()).abs().max().item(),
-          "dR rel", ((res["3"][1] - res["1"][1]).norm() / res["1"][1].norm()).item(), flush=True)
+    dR.zero_()
+    ms = timeit(lambda: attention.relattn_bwd(dout, out, lse, qkv, R, B, S, H, 128, scale, dqkv=dqkv, dR=dR),
+                iters=3, warm=1)
+    rows.append(("attn bwd", ms, 2 * flops_att / ms / 1e9))
     for n, ms, tf in rows:
         print(f"{n:32s} {ms:9.3f} ms  {tf:8.1f} TFLOP/s")
 
