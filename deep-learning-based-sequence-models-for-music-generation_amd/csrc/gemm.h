@@ -26,6 +26,8 @@ struct GemmArgs {
     // split-K partials (ACCUM, ksplit > 1): slice s of batch z at
     // ws + ((s * batch + z) * M) * N (N % 4 == 0); null = fp32 atomics into C
     float* ws;
+    // global row of local row 0 (the dropout hash is keyed by the global row)
+    int64_t m_off;
 };
 
 // bytes of the split-K partial workspace an ACCUM product with this split needs
@@ -37,7 +39,7 @@ void splitk_reduce(const GemmArgs& g, hipStream_t s);
 
 // dropout(v + bias) of one lane's 4 outputs C[m][n..n+3] (nn.Dropout, common.h hash)
 __device__ __forceinline__ f32x4 epi_drop(const GemmArgs& g, int64_t m, int64_t n, f32x4 v) {
-    const uint32_t rk = drop_row(g.drop_base, (uint32_t)m);
+    const uint32_t rk = drop_row(g.drop_base, (uint32_t)(m + g.m_off));
 #pragma unroll
     for (int t = 0; t < 4; ++t) v[t] = drop_bits(rk, (uint32_t)(n + t)) >= g.drop_thr ? v[t] * g.drop_scale : 0.f;
     return v;

@@ -130,8 +130,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
     const int per_group = GROUP * g.tiles_n;
     const int grp = bid / per_group, first_m = grp * GROUP;
     const int gsz = min(g.tiles_m - first_m, GROUP);
-    const int tm = first_m + (bid % per_group) % gsz;
+    int tm = first_m + (bid % per_group) % gsz;
     const int tn = (bid % per_group) / gsz;
+    if (g.tri == 2) tm = g.tiles_m - 1 - tm;  // dR: K range grows with m, start the long tiles first
     const int m0 = tm * BM, n0 = tn * BN;
 
     const bf16* A = (const bf16*)g.A + bz * g.sA;
@@ -297,7 +298,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g, int ta, int t
                  EPI == MSQ_EPI_BIAS_DROP_RESID) && g.bias)
                 v += g.bias[n];
             if (EPI == MSQ_EPI_BIAS_DROP_RESID)
-                v = (drop_bits(drop_row(g.drop_base, (uint32_t)m), (uint32_t)n) >= g.drop_thr ? v * g.drop_scale : 0.f) +
+                v = (drop_bits(drop_row(g.drop_base, (uint32_t)(m + g.m_off)), (uint32_t)n) >= g.drop_thr ? v * g.drop_scale : 0.f) +
                     (float)X[m * g.ldx + n];
             if (EPI == MSQ_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
             if (EPI == MSQ_EPI_BIAS_RESID) v += (float)X[m * g.ldx + n];
@@ -379,7 +380,9 @@ void splitk_reduce(const GemmArgs& g, hipStream_t s) {
 int gemm_bf16_tri_ksplit(int tri, int64_t M, int64_t N, int64_t K, int64_t seg, int64_t batch) {
     if (tri != 2) return 1;
     const int64_t nb = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * batch, nseg = K / seg;
-    return (int)std::max<int64_t>(1, std::min<int64_t>(nseg, (1024 + nb - 1) / nb));
+    // ~2048 blocks (8 per CU): the K ranges differ 16x between m tiles, so the
+    // finer split balances the CUs (dR at cfg 2: 790 us at 8 slices, 518 at 16)
+    return (int)std::max<int64_t>(1, std::min<int64_t>(nseg, (2048 + nb - 1) / nb));
 }
 
 int gemm_bf16_tri(int tri, int64_t seg, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
@@ -400,7 +403,7 @@ int gemm_bf16_tri(int tri, int64_t seg, int ta, int tb, int64_t M, int64_t N, in
     g.seg = seg;
     g.ksplit = 1;
     g.kper = ((K + BK - 1) / BK) * BK;
-    // tri 2: split the segments so that about 1024 blocks (4 per CU) run
+    // tri 2: split the segments over blocks (gemm_bf16_tri_ksplit)
     g.ksplit = gemm_bf16_tri_ksplit(tri, M, N, K, seg, batch);
     if (epi == MSQ_EPI_ACCUM && g.ksplit > 1 && ws && c_dtype == MSQ_F32 &&
         splitk_ws_bytes(M, N, batch, g.ksplit) && ws_bytes >= splitk_ws_bytes(M, N, batch, g.ksplit))
@@ -507,10 +510,38 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
     plan128_ksplit(g, dtype, epilogue);
     g.ws = (float*)ws;
     hipStream_t s = (hipStream_t)stream;
-    if (dtype == MSQ_BF16 && !getenv("MSQ_GEMM128") &&
-        gemm256_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, (size_t)ws_bytes, s)) {
-        MSQ_LAUNCH_CHECK();
-        return MSQ_OK;
+    if (dtype == MSQ_BF16 && !getenv("MSQ_GEMM128")) {
+        // wave quantisation: M = B*S rows rarely divide by 256 (32 x 2054 =
+        // 256.75 tiles), and the partial last row of 256 tiles alone would
+        // take one more full round of the 256 tile on a few CUs. Run the
+        // whole 256-row tiles there and the tail rows with the 128 tile.
+        GemmArgs p = g;
+        const bool split = batch == 1 && epilogue != MSQ_EPI_ACCUM && M % 256 != 0 && M > 256 &&
+                           !getenv("MSQ_GEMM_NOTAIL") && gemm256_plan(p, ta, tb, epilogue) &&
+                           (int64_t)p.tiles_m * p.tiles_n % 256 != 0 &&
+                           (int64_t)p.tiles_m * p.tiles_n % 256 <= p.tiles_n;
+        if (split) {
+            const int64_t Mm = M / 256 * 256, esz = c_dtype == MSQ_BF16 ? 2 : 4, xsz = aux_dtype == MSQ_BF16 ? 2 : 4;
+            GemmArgs t = g;
+            t.M = M - Mm;
+            t.m_off = Mm;
+            t.A = (const char*)A + (ta ? Mm : Mm * lda) * 2;
+            t.C = (char*)C + Mm * ldc * esz;
+            if (aux) t.aux = (const char*)aux + Mm * ld_aux * xsz;
+            t.tiles_m = (int)((t.M + BM - 1) / BM);
+            g.M = Mm;
+            if (gemm256_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, 0, s)) {
+                const int rc = c_dtype == MSQ_BF16 ? dispatch_epi<true, bf16>(t, ta, tb, epilogue, aux_dtype, s)
+                                                   : dispatch_epi<true, float>(t, ta, tb, epilogue, aux_dtype, s);
+                if (rc) return msq_set_error(MSQ_ERR_ARG, "msq_gemm: unsupported combination");
+                MSQ_LAUNCH_CHECK();
+                return MSQ_OK;
+            }
+            g.M = M;
+        } else if (gemm256_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, (size_t)ws_bytes, s)) {
+            MSQ_LAUNCH_CHECK();
+            return MSQ_OK;
+        }
     }
     if (!(epilogue == MSQ_EPI_ACCUM && g.ksplit > 1 && splitk_ws_bytes(M, N, batch, g.ksplit) &&
           (size_t)ws_bytes >= splitk_ws_bytes(M, N, batch, g.ksplit)))

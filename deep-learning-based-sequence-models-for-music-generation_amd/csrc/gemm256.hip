@@ -127,7 +127,7 @@ __device__ __forceinline__ void read_set(bf16x8 (&f)[2][NF], const lds_t* slot, 
 
 // LAB: ablation switches for tools/gemm256_lab.hip only (0 in the library):
 // 1 = no LDS-DMA in the K loop, 2 = no MFMA, 4 = no ping-pong stagger,
-// 8 = K slice innermost in the block order
+// 8 = K slice innermost in the block order, 16 = no epilogue stores
 template <int TA, int TB, int EPI, typename TC, typename TX, int LAB = 0>
 __global__ __launch_bounds__(NT, 1) void gemm256_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -310,6 +310,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(GemmArgs g) {
                 for (int j = 0; j < 2; ++j) {
                     const int64_t n = n0 + b * 128 + wc * 32 + j * 16 + 4 * (lane >> 4);
                     if (n >= g.N) continue;
+                    if ((LAB & 16) && acc[a][b][i][j][0] != 12345.f) continue;
                     epi_apply<EPI, TC, TX>(g, C, X, m, n, acc[a][b][i][j], wsp);
                 }
         }

@@ -195,3 +195,32 @@ def test_adam_matches_torch():
         ops.adam_step(P, gr.to(dev), M, Vv, step, 5e-5, shadow=sh)
     assert _rel(P, p.detach()) < 1e-6
     assert torch.equal(sh.cpu(), P.cpu().bfloat16())
+
+
+@pytest.mark.parametrize("epi", ["drop", "relu_mask", "none"])
+def test_gemm256_tail_rows_split(epi):
+    """M = 64*256 + 100 rows, N = 1024: the 256 tile runs rows [0, 16384) and
+    the 128 tile the 100 tail rows (msq_gemm_ex wave-quantisation split); the
+    dropout hash must stay keyed by the GLOBAL row."""
+    from oracle import dropout as odrop
+    g = torch.Generator().manual_seed(21)
+    M, N, K = 64 * 256 + 100, 1024, 128
+    a = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * 0.1).bfloat16()
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g)
+    base = a.float() @ w.float().t()
+    A, W = a.to(dev), w.to(dev)
+    if epi == "drop":
+        seed, site, p = 77, 3, 0.2
+        o = ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_BIAS_RESID, bias=bias.to(dev), aux=res.to(dev),
+                     drop=(seed, site, p))
+        keep = torch.from_numpy(odrop.keep(seed, site, M, N, p))
+        ref = res + torch.where(keep, (base + bias) * odrop.scale(p), torch.zeros(()))
+        assert _rel(o, ref) < 2e-3
+    elif epi == "relu_mask":
+        o = ops.gemm(A, W, out_dtype=torch.bfloat16, epilogue=L.EPI_RELU_MASK, aux=res.bfloat16().to(dev))
+        assert _rel(o.float(), base * (res.bfloat16().float() > 0)) < 1e-2
+    else:
+        o = ops.gemm(A, W, out_dtype=torch.float32)
+        assert _rel(o, base) < 2e-3

@@ -61,7 +61,7 @@ def main():
                   bias=bias if epi in (L.EPI_BIAS, L.EPI_BIAS_RELU, L.EPI_BIAS_RESID) else None, aux=aux)
         fl = 2.0 * m * n * k
         res = {}
-        for tag, env in (("g128", "MSQ_GEMM128"), ("g256", None)):
+        for tag, env in (("g128", "MSQ_GEMM128"), ("g256nt", "MSQ_GEMM_NOTAIL"), ("g256", None)):
             os.environ.pop("MSQ_GEMM128", None)
             os.environ.pop("MSQ_GEMM_NOTAIL", None)
             if env:

@@ -7,6 +7,7 @@
 #include <vector>
 
 int msq_set_error(int code, const char*, ...) { return code; }
+void splitk_reduce(const GemmArgs&, hipStream_t) {}
 
 __global__ void fill(bf16* p, int64_t n, uint32_t seed) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -19,7 +20,7 @@ __global__ void fill(bf16* p, int64_t n, uint32_t seed) {
 static int g_ta = 0, g_tb = 0;
 template <int LAB, int TA, int TB>
 float run_t(GemmArgs g, int iters) {
-    auto k = gemm256_kernel<TA, TB, MSQ_EPI_NONE, float, float, LAB>;
+    auto k = gemm256_kernel<TA, TB, MSQ_EPI_NONE, bf16, float, LAB>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * HALF);
     const int nblk = g.tiles_m * g.tiles_n * g.batch * g.ksplit;
     hipEvent_t a, b;
@@ -63,7 +64,7 @@ int main(int argc, char** argv) {
     const double fl = 2.0 * M * N * K;
     struct V { const char* name; float (*fn)(GemmArgs, int); };
     V vs[] = {{"full", run<0>}, {"no-dma", run<1>}, {"no-mfma", run<2>}, {"no-dma,no-mfma", run<3>},
-              {"no-stagger", run<4>}, {"kslice-inner", run<8>}, {"full(again)", run<0>}};
+              {"no-stagger", run<4>}, {"no-store", run<16>}, {"full(again)", run<0>}};
     printf("M=%lld N=%lld K=%lld ta=%d tb=%d ksplit=%d\n", (long long)M, (long long)N, (long long)K, g_ta, g_tb, ksplit);
     for (auto& v : vs) {
         float ms = v.fn(g, 20);
