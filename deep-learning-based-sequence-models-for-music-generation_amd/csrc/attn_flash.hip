@@ -229,18 +229,20 @@ __global__ void flash_bwd_meta_kernel(AttnArgs a, const float* __restrict__ meta
 }  // namespace
 
 namespace {
-// zero the part of dQR[h][b][i][r] that the consumers read but pass A does not
-// write: r in [S-1-i-DQR_BAND, S-1-i) (below the written band) and the row pad
-// [S, ldr). pass B and the triangular GEMMs never read further below the band.
+// zero the part of dQR[h][b][i][r] that the consumers read but the key/value
+// pass does not write: r in [S-1-i-DQR_BAND, S-1-i) (below the written band)
+// and the row pad [S, ldr); and the row pad of dSj. The dq kernel and the dR
+// product never read further below the band.
 constexpr int DQR_BAND = 256;
-__global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, int64_t ldr, int64_t S, int64_t rows) {
+__global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, bf16* __restrict__ dsj, int64_t ldr, int64_t S,
+                                     int64_t rows) {
     const int64_t row = blockIdx.x * 4LL + (threadIdx.x >> 6);  // (h, b, i) flattened
     if (row >= rows) return;
     const int64_t i = row % S;
     bf16* p = dqr + row * ldr;
     const int64_t lo = max<int64_t>(0, S - 1 - i - DQR_BAND), hi = S - 1 - i;
     for (int64_t r = lo + (threadIdx.x & 63); r < hi; r += 64) p[r] = (bf16)0.f;
-    for (int64_t r = S + (threadIdx.x & 63); r < ldr; r += 64) p[r] = (bf16)0.f;
+    for (int64_t r = S + (threadIdx.x & 63); r < ldr; r += 64) p[r] = dsj[row * ldr + r] = (bf16)0.f;
 }
 }  // namespace
 
@@ -279,8 +281,8 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     p += align256((size_t)B * H * 64 * 4);
     float* dr_ws = (float*)p;
 
-    hipLaunchKernelGGL(dqr_band_zero_kernel, dim3((unsigned)((H * B * S + 3) / 4)), dim3(256), 0, s, dqr, ldr, S,
-                       H * B * S);
+    hipLaunchKernelGGL(dqr_band_zero_kernel, dim3((unsigned)((H * B * S + 3) / 4)), dim3(256), 0, s, dqr, dsj, ldr,
+                       S, H * B * S);
     hipMemsetAsync(meta_ds, 0, (size_t)B * H * 64 * 4, s);
     hipLaunchKernelGGL(flash_bwd_pre_kernel, dim3((unsigned)((B * S * H + 3) / 4)), dim3(256), 0, s, a, dout, ldo, out, Dv);
     // key/value pass: dK, dV, and dS in both layouts

@@ -147,7 +147,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    Stager<TA, TB> st;
+    // two register stages (prefetch distance 2): tile t+2 is fetched while
+    // tile t is multiplied and tile t+1 waits in registers for its LDS buffer
+    Stager<TA, TB> st0, st1;
     // K range(s) of this block: segments [sg_lo, sg_hi), segment s covers
     // [kb(s), ke(s)); tri 0 / 1 use a single segment
     int64_t sg_lo = 0, sg_hi = 1, kb0 = (int64_t)kslice * g.kper, ke0 = min<int64_t>(g.K, kb0 + g.kper), imin = 0;
@@ -162,28 +164,23 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
     }
     auto seg_kb = [&](int64_t sg) { return g.tri == 2 ? sg * g.seg + imin : kb0; };
     auto seg_ke = [&](int64_t sg) { return g.tri == 2 ? (sg + 1) * g.seg : ke0; };
+    // load cursor: segment cs, tile start ck, segment end cke
     int64_t cs = sg_lo, ck = seg_kb(cs), cke = seg_ke(cs);
-    while (cs < sg_hi && ck >= cke) {
-        ++cs;
-        if (cs < sg_hi) ck = seg_kb(cs), cke = seg_ke(cs);
-    }
-    if (cs < sg_hi) {
-        st.load(g, A, B, m0, n0, ck, cke, tid);
-        st.store(smem, smem + BM * BK * 2, tid);
-    }
-    __syncthreads();
-
-    for (int kt = 0; cs < sg_hi; ++kt) {
-        const int cur = kt & 1;
-        char* sa = smem + cur * STAGE;
-        char* sb = sa + BM * BK * 2;
-        ck += BK;
+    auto skip_empty = [&]() {
         while (cs < sg_hi && ck >= cke) {
             ++cs;
             if (cs < sg_hi) ck = seg_kb(cs), cke = seg_ke(cs);
         }
-        const bool more = cs < sg_hi;
-        if (more) st.load(g, A, B, m0, n0, ck, cke, tid);
+    };
+    // loads the cursor's tile into x and advances; false when the range is done
+    auto fetch = [&](Stager<TA, TB>& x) {
+        if (cs >= sg_hi) return false;
+        x.load(g, A, B, m0, n0, ck, cke, tid);
+        ck += BK;
+        skip_empty();
+        return true;
+    };
+    auto mma = [&](const char* sa, const char* sb) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             bf16x8 af[4], bfr[4];
@@ -197,8 +194,29 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
                 for (int j = 0; j < 4; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         }
-        if (more) st.store(smem + (cur ^ 1) * STAGE, smem + (cur ^ 1) * STAGE + BM * BK * 2, tid);
+    };
+    char* sa0 = smem;
+    char* sb0 = smem + BM * BK * 2;
+    char* sa1 = smem + STAGE;
+    char* sb1 = sa1 + BM * BK * 2;
+    skip_empty();
+    bool v0 = fetch(st0);
+    if (v0) st0.store(sa0, sb0, tid);
+    bool v1 = fetch(st1);
+    __syncthreads();
+    // LDS buffer 0 holds tile t (valid: v0), st1 holds tile t+1 (v1)
+    while (v0) {
+        const bool v2 = fetch(st0);
+        mma(sa0, sb0);
+        if (v1) st1.store(sa1, sb1, tid);
         __syncthreads();
+        if (!v1) break;
+        const bool v3 = fetch(st1);
+        mma(sa1, sb1);
+        if (v2) st0.store(sa0, sb0, tid);
+        __syncthreads();
+        v0 = v2;
+        v1 = v3;
     }
 
     // epilogue: lane holds C[m][n..n+3]
