@@ -462,13 +462,8 @@ __global__ __launch_bounds__(NT) void finish2_kernel(LossArgs a, const float* __
     ldf<N>(colsum + b * Vp + v, cs);
 #pragma unroll
     for (int k = 0; k < 5; ++k) ldf<N>(wtp + (int64_t)k * Vp + v, wt[k]);
-    for (int64_t t = t0; t < t1; ++t) {
-        const int64_t row = b * a.T + t;
-        const int bk = bucket_of(a, a.src[row]);
-        const int y = (int)a.trg[row];
-        const float lse = row_lse[row];
-        float ov[N], d[N];
-        ldv<T, N>((const T*)a.o + row * a.ld + v, ov);
+    auto one = [&](int64_t row, const float (&ov)[N], int bk, int y, float lse) {
+        float d[N];
 #pragma unroll
         for (int i = 0; i < N; ++i) {
             const float wv = bk == 0 ? wt[0][i] : bk == 1 ? wt[1][i] : bk == 2 ? wt[2][i] : bk == 3 ? wt[3][i] : wt[4][i];
@@ -477,6 +472,30 @@ __global__ __launch_bounds__(NT) void finish2_kernel(LossArgs a, const float* __
             d[i] = (v + i < a.V) ? -wv * dz + fexp(oc) * cs[i] : 0.f;  // pad columns stay 0
         }
         stv<TD, N>(dout + row * ldd + v, d);
+    };
+    // 4 rows per step: their loads are all in flight before the first use
+    constexpr int U = 4;
+    int64_t t = t0;
+    for (; t + U <= t1; t += U) {
+        float ov[U][N];
+        int bk[U], y[U];
+        float lse[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t row = b * a.T + t + u;
+            ldv<T, N>((const T*)a.o + row * a.ld + v, ov[u]);
+            bk[u] = bucket_of(a, a.src[row]);
+            y[u] = (int)a.trg[row];
+            lse[u] = row_lse[row];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) one(b * a.T + t + u, ov[u], bk[u], y[u], lse[u]);
+    }
+    for (; t < t1; ++t) {
+        const int64_t row = b * a.T + t;
+        float ov[N];
+        ldv<T, N>((const T*)a.o + row * a.ld + v, ov);
+        one(row, ov, bucket_of(a, a.src[row]), (int)a.trg[row], row_lse[row]);
     }
 }
 

@@ -142,3 +142,33 @@ def test_bf16_path_against_oracle():
         nr = ((g - r).norm() / r.norm()).item()
         cos = (g @ r / (g.norm() * r.norm())).item()
         assert nr < 8e-2 and cos > 0.995, (k, nr, cos)
+
+
+@pytest.mark.parametrize("B,T", [(2, 300), (1, 2048)])
+def test_filtered_ce_bf16_streaming_rows(B, T):
+    """bf16 logits in the padded [B, T, V_pad] layout (V_pad = 17920) through the
+    three-pass streaming loss (colstats2 / rowstats2 / finish2), T spanning
+    several 64-row blocks of rowstats2 and partial 4-row groups of finish2,
+    against the oracle (train.py:133-138 + CrossEntropyLoss) on the same
+    bf16-rounded logits in fp32. Tolerance: loss 1e-4 relative, dlogits 2e-2
+    of max (bf16 output)."""
+    from midiseq.loss import ce_forward_backward
+    vocab = REAL
+    g = torch.Generator().manual_seed(5)
+    Vp = (vocab.size + 255) // 256 * 256
+    full = (torch.randn(B, T, Vp, generator=g) * 2).bfloat16()
+    full[:, :, vocab.size:] = 0
+    rng = np.random.default_rng(7)
+    w = np.stack([grammar_tokens(rng, vocab, T + 1) for _ in range(B)])
+    src, trg = torch.from_numpy(w[:, :-1].copy()), torch.from_numpy(w[:, 1:].copy())
+    lr = full[:, :, :vocab.size].float().requires_grad_(True)
+    ref = oloss.loss(src, trg, lr, vocab)
+    ref.backward()
+    x = full.to(dev)
+    dl = torch.zeros_like(x)
+    loss, _ = ce_forward_backward(src.to(dev), x, trg.to(dev), vocab.size, dlogits=dl)
+    torch.cuda.synchronize()
+    assert abs(loss.item() - ref.item()) < 1e-4 * abs(ref.item())
+    got = dl[:, :, :vocab.size].float().cpu()
+    assert ((got - lr.grad).abs().max() / lr.grad.abs().max()).item() < 2e-2
+    assert dl[:, :, vocab.size:].abs().max().item() == 0
