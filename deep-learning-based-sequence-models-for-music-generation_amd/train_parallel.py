@@ -116,15 +116,47 @@ def new_model(type_name="transformer", precision="bf16", **kw):
     return Transformer(TransformerConfig(precision=precision, **kw))
 
 
-def train(model, type_name="transformer", data=None, steps=100, log_every=10, lr=LEARNING_RATE):
-    """Mirrors train_parallel.train: init RCCL, replicate the model, loop."""
+def save_model(model, loss, pretrained_path, type_name="transformer"):
+    """train.py:69-77: state_dict (the reference's keys, incl. the tril
+    buffers) to <pretrained>/<type>/loss_<loss>_time_<now>.pth."""
+    from datetime import datetime
+    now = datetime.now().strftime("%Y-%m-%d-%H-%M-%S")
+    path = os.path.join(pretrained_path, type_name, f"loss_{loss:.2f}_time_{now}.pth")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    torch.save({k: v.detach().cpu() for k, v in model.state_dict().items()}, path)
+    return path
+
+
+def load_model(type_name, path, precision="bf16", device="cuda", **kw):
+    """train.py:63-67 (load_model): a reference-format .pth (per-head
+    key/query/value, tril buffers) into the MI355X engine. Loaded with
+    weights_only=True: nothing in the file is executed."""
+    model = new_model(type_name, precision=precision, **kw)
+    model.load_state_dict(torch.load(path, map_location="cpu", weights_only=True))
+    return model.to(device)
+
+
+def train(model, type_name="transformer", data=None, steps=100, log_every=10, lr=LEARNING_RATE, save_dir=None,
+          save_every=0):
+    """Mirrors train_parallel.train: init RCCL, replicate the model, loop.
+    data: an iterable of device batches (src, trg, meta) — e.g. the train
+    loader of data.DatasetLoader — or None for synthetic grammar batches."""
     rank, local, world = setup_distributed()
     dev = torch.device("cuda", local)
     model.to(dev)
     step = TrainStep(model, lr=lr)
     if data is None:
         data = SyntheticMIDI(2, model.cfg.block_len, dev, rank)
-    it = iter(data)
+
+    def batches():
+        while True:  # epochs of a finite loader, as the reference's epoch loop
+            n = 0
+            for b in data:
+                n += 1
+                yield b
+            if n == 0:
+                raise ValueError("empty data loader")
+    it = batches()
     t0 = time.time()
     log = []
     for i in range(steps):
@@ -133,4 +165,6 @@ def train(model, type_name="transformer", data=None, steps=100, log_every=10, lr
         if (i + 1) % log_every == 0 and rank == 0:
             log.append({"Step": i + 1, "Loss": f"{loss.item():.4f}", "elapsed_s": time.time() - t0})
             print(f"Step: {i + 1}, Loss: {log[-1]['Loss']}")
+        if save_dir and save_every and (i + 1) % save_every == 0 and rank == 0:
+            save_model(model, loss.item(), save_dir, type_name)
     return log

@@ -234,6 +234,18 @@ int msq_mamba_conv_bwd(void* dzxbcdt, const float* dxc, int64_t ld_dxc, const vo
                        const float* conv_w, const float* conv_b, float* g_conv_w, float* g_conv_b, int64_t B,
                        int64_t L, int64_t d_inner, int64_t nheads, void* stream);
 
+/* ---- data feed (processing/dataset.py:171-195 SequenceDataset.__getitem__)
+ * B training windows of T+1 tokens cut from the device-resident token store
+ * (tokens int32, song s = tokens[song_off[s] .. + song_len[s]]): params[b] =
+ * {song, start, note_shift, velocity_shift, 2 x time_factor}; tokens past the
+ * song end are 0 (dataset.py:177-179); augment != 0 applies
+ * data_augementation (:134-168) with disc = {pitch, channel, dyn, length,
+ * time, tempo}. Writes src[b] = w[:-1], trg[b] = w[1:] (int64 [B, T]) and
+ * meta_out[b] = song_meta[song] (int64 [B, n_meta]).                        */
+int msq_window_gather(int64_t* src, int64_t* trg, int64_t* meta_out, const int32_t* tokens,
+                      const int64_t* song_off, const int64_t* song_len, const int64_t* song_meta, int n_meta,
+                      const int64_t* params, int64_t B, int64_t T, int augment, const int64_t* disc, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

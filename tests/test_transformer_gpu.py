@@ -172,3 +172,26 @@ def test_filtered_ce_bf16_streaming_rows(B, T):
     got = dl[:, :, :vocab.size].float().cpu()
     assert ((got - lr.grad).abs().max() / lr.grad.abs().max()).item() < 2e-2
     assert dl[:, :, vocab.size:].abs().max().item() == 0
+
+
+def test_checkpoint_save_load_reference_format(tmp_path):
+    """train.py:63-77: save_model writes the reference's state_dict keys
+    (per-head key/query/value, tril buffers) to a .pth; load_model reads it
+    back with weights_only=True into a fresh engine and trains on."""
+    from midiseq.train_parallel import save_model, load_model, TrainStep
+    vocab, mv, hp = CASES["small"]
+    m, p = build(vocab, mv, hp, "fp32")  # hs = 16: the exact path (bf16 MFMA attention needs hs = 128)
+    path = save_model(m, 1.2345, str(tmp_path), "transformer")
+    assert Path(path).name.startswith("loss_1.23_time_") and Path(path).parent.name == "transformer"
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    assert "blocks.1.sa.heads.7.query.weight" in sd and "blocks.0.sa.heads.0.tril" in sd
+    m2 = load_model("transformer", path, precision="fp32", device=dev, vocab_size=vocab.size,
+                    metadata_vocab_size=mv, dropout=0.0, **hp)
+    for k, v in p.items():
+        assert torch.equal(m2.state_dict()[k].cpu(), v), k
+    B, T = 2, hp["block_len"]
+    rng = np.random.default_rng(0)
+    w = torch.from_numpy(np.stack([grammar_tokens(rng, vocab, T + 1) for _ in range(B)])).to(dev)
+    meta = torch.randint(0, mv, (B, 6), device=dev)
+    loss = TrainStep(m2, grammar=grammar_for(vocab))(w[:, :-1], w[:, 1:], meta)
+    assert torch.isfinite(loss).item()
