@@ -91,7 +91,9 @@ _ws_cache = {}
 
 
 def workspace(nbytes, device, tag="ws"):
-    key = (tag, device)
+    """Scratch buffer of a launch, one per (tag, device, stream): launches on
+    different streams never share one."""
+    key = (tag, device, torch.cuda.current_stream(device).cuda_stream)
     buf = _ws_cache.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(nbytes, 1), device=device, dtype=torch.uint8)

@@ -185,7 +185,11 @@ class _Acts:
             f32 = torch.float32
             e = lambda *s, dt=act: torch.empty(*s, device=device, dtype=dt)  # noqa: E731
             need_copy = act != f32 or cfg.dropout > 0  # fp32 + dropout: masked fp32 copy
-            self._bwd = dict(gres=e(M, d, dt=f32), gb=e(M, d) if need_copy else None, dtmp=e(M, d),
+            # gb / gb2: the bf16 branch gradients of the FFN / attention halves
+            # of a block (two buffers so the weight-gradient stream can still
+            # read one while the main stream writes the other)
+            self._bwd = dict(gres=e(M, d, dt=f32), gb=e(M, d) if need_copy else None,
+                             gb2=e(M, d) if need_copy and act != f32 else None, dtmp=e(M, d),
                              dh=e(M, 4 * d), dqkv=e(M, 3 * d), df=e(self.B * self.T, d),
                              dlogits=torch.zeros(self.B * self.T, cfg.v_pad, device=device, dtype=act))
         return self._bwd
@@ -302,51 +306,119 @@ class TransformerEngine:
         d, H, hs, S, M, V = cfg.n_embd, cfg.n_heads, cfg.head_size, T + N_META, A.M, cfg.vocab_size
         scale = d ** -0.5
         dl = dlogits[:, :V]
+        seed, p = A.drop if A.drop is not None else (0, 0.0)
+        dsite = (lambda site: (seed, site, p)) if p > 0 else (lambda site: None)  # noqa: E731
+        hook = getattr(self, "layer_grad_ready", None)
+        # Weight gradients (dW GEMMs, and the bias column sums when they read a
+        # bf16 branch gradient) only feed the optimizer, not the next layer's
+        # backward: on the bf16 path they run on a second stream, overlapped
+        # with the dX / LayerNorm / attention chain of the main stream. Each
+        # side launch waits for the main stream's producer of its inputs; the
+        # main stream waits for the side stream before it overwrites a buffer
+        # the side still reads (gb / gb2 / dh / dqkv, one layer of slack).
+        ov = Bw["gb2"] is not None
+        main = torch.cuda.current_stream(self.device)
+        if ov and getattr(self, "_dw_stream", None) is None:
+            self._dw_stream = torch.cuda.Stream(device=self.device)
+        side = self._dw_stream if ov else main
+        pending = {}
+
+        def on_side(key, fn):
+            if not ov:
+                fn()
+                return
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                fn()
+            done = torch.cuda.Event()
+            done.record(side)
+            pending[key] = done
+
+        def before_write(key):
+            ev = pending.pop(key, None)
+            if ev is not None:
+                main.wait_event(ev)
+
+        def layer_done(key):
+            if hook is None:
+                return
+            if not ov:
+                hook(key)
+                return
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):  # the bucket's event then follows both streams
+                hook(key)
+
         # lm_head (model_transformer.py:147,161)
-        ops.gemm(dlogits, A.f, ta=True, tb=True, out=G["lm_w"], epilogue=L.EPI_ACCUM)  # pad columns are 0
-        ops.colsum(dl, G["lm_b"][:V], accumulate=True)
+        def lm_w():
+            ops.gemm(dlogits, A.f, ta=True, tb=True, out=G["lm_w"], epilogue=L.EPI_ACCUM)  # pad columns are 0
+            ops.colsum(dl, G["lm_b"][:V], accumulate=True)
+        on_side("dlogits", lm_w)
         ops.gemm(dlogits, W["lm_w"], tb=True, out=Bw["df"])
         gres = Bw["gres"]
         gres.zero_()
         gb = Bw["gb"] if Bw["gb"] is not None else gres
+        gb2 = Bw["gb2"] if ov else gb
         if Bw["gb"] is not None:
             gb.zero_()
         # dropout: gb is the gradient INTO the dropped branch (gres masked by the
         # keep mask of the site whose output was added to the residual there);
         # the bias gradients then sum gb instead of gres
-        seed, p = A.drop if A.drop is not None else (0, 0.0)
-        dsite = (lambda site: (seed, site, p)) if p > 0 else (lambda site: None)  # noqa: E731
-        gbias = gb if p > 0 else gres
+        side_bias = p > 0  # bias sums of gres (fp32, updated in place) stay on the main stream
         ops.layernorm_bwd(gres, Bw["df"], A.x[cfg.n_layer], A.stf[0], A.stf[1], P["lnf_w"], G["lnf_w"], G["lnf_b"],
                           dx_copy=Bw["gb"], seg=(T, N_META), drop=dsite(DROP_FFN + cfg.n_layer - 1))
-        hook = getattr(self, "layer_grad_ready", None)
-        if hook is not None:
-            hook("head")
+        layer_done("head")
         for l in reversed(range(cfg.n_layer)):
             # FFN (model_transformer.py:92-105,120)
-            ops.gemm(gb, A.h[l], ta=True, tb=True, out=G[f"{l}.w2"], epilogue=L.EPI_ACCUM)
-            ops.colsum(gbias, G[f"{l}.b2"], accumulate=True)
+            def ffn2_w(l=l):
+                ops.gemm(gb, A.h[l], ta=True, tb=True, out=G[f"{l}.w2"], epilogue=L.EPI_ACCUM)
+                if side_bias:
+                    ops.colsum(gb, G[f"{l}.b2"], accumulate=True)
+            on_side("gb", ffn2_w)
+            if not side_bias:
+                ops.colsum(gres, G[f"{l}.b2"], accumulate=True)
+            before_write("dh")
             ops.gemm(gb, W[f"{l}.w2"], tb=True, out=Bw["dh"], epilogue=L.EPI_RELU_MASK, aux=A.h[l])
-            ops.gemm(Bw["dh"], A.c[l], ta=True, tb=True, out=G[f"{l}.w1"], epilogue=L.EPI_ACCUM)
-            ops.colsum(Bw["dh"], G[f"{l}.b1"], accumulate=True)
+
+            def ffn1_w(l=l):
+                ops.gemm(Bw["dh"], A.c[l], ta=True, tb=True, out=G[f"{l}.w1"], epilogue=L.EPI_ACCUM)
+                ops.colsum(Bw["dh"], G[f"{l}.b1"], accumulate=True)
+            on_side("dh", ffn1_w)
             ops.gemm(Bw["dh"], W[f"{l}.w1"], tb=True, out=Bw["dtmp"])
+            before_write("gb2")
             ops.layernorm_bwd(gres, Bw["dtmp"], A.xm[l], A.st2[l, 0], A.st2[l, 1], P[f"{l}.ln2_w"], G[f"{l}.ln2_w"],
-                              G[f"{l}.ln2_b"], dx_copy=Bw["gb"], drop=dsite(DROP_PROJ + l))
+                              G[f"{l}.ln2_b"], dx_copy=gb2 if Bw["gb"] is not None else None,
+                              drop=dsite(DROP_PROJ + l))
             # attention (model_transformer.py:41-90,119)
-            ops.gemm(gb, A.o[l], ta=True, tb=True, out=G[f"{l}.wproj"], epilogue=L.EPI_ACCUM)
-            ops.colsum(gbias, G[f"{l}.bproj"], accumulate=True)
-            ops.gemm(gb, W[f"{l}.wproj"], tb=True, out=Bw["dtmp"])
+
+            def proj_w(l=l):
+                ops.gemm(gb2, A.o[l], ta=True, tb=True, out=G[f"{l}.wproj"], epilogue=L.EPI_ACCUM)
+                if side_bias:
+                    ops.colsum(gb2, G[f"{l}.bproj"], accumulate=True)
+            on_side("gb2", proj_w)
+            if not side_bias:
+                ops.colsum(gres, G[f"{l}.bproj"], accumulate=True)
+            ops.gemm(gb2, W[f"{l}.wproj"], tb=True, out=Bw["dtmp"])
+            before_write("dqkv")
             relattn_bwd(Bw["dtmp"], A.o[l], A.lse[l], A.qkv[l], W[f"{l}.R"], B, S, H, hs, scale, dqkv=Bw["dqkv"],
                         dR=G[f"{l}.R"], drop=(A._masks[l], p) if p > 0 else None)
-            ops.gemm(Bw["dqkv"], A.a[l], ta=True, tb=True, out=G[f"{l}.wqkv"], epilogue=L.EPI_ACCUM)
+
+            def qkv_w(l=l):
+                ops.gemm(Bw["dqkv"], A.a[l], ta=True, tb=True, out=G[f"{l}.wqkv"], epilogue=L.EPI_ACCUM)
+            on_side("dqkv", qkv_w)
             ops.gemm(Bw["dqkv"], W[f"{l}.wqkv"], tb=True, out=Bw["dtmp"])
+            before_write("gb")
             ops.layernorm_bwd(gres, Bw["dtmp"], A.x[l], A.st1[l, 0], A.st1[l, 1], P[f"{l}.ln1_w"], G[f"{l}.ln1_w"],
                               G[f"{l}.ln1_b"], dx_copy=Bw["gb"], drop=dsite(DROP_FFN + l - 1) if l > 0 else None)
-            if hook is not None:
-                hook(l)
+            layer_done(l)
         ops.embed_bwd(G["tok_emb"], G["meta_emb"], gres, idx, meta)
-        if hook is not None:
-            hook(-1)
+        layer_done(-1)
+        if ov:
+            main.wait_stream(side)  # the optimizer reads every gradient
 
     def bucket_ranges(self):
         from .ddp import transformer_buckets
