@@ -61,8 +61,9 @@ SIGNATURES = {
     "msq_mamba_ssd_fwd": (_i, [_p, _i64, _p, _p, _i64, _p, _i64, _i, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "msq_mamba_gnorm_fwd": (_i, [_p, _i64, _p, _p, _i64, _p, _i64, _i, _p, _i64, _i64, _f, _p]),
     "msq_mamba_gnorm_bwd": (_i, [_p, _p, _p, _i64, _p, _i64, _i, _p, _p, _p, _i64, _p, _i64, _i64, _p]),
+    "msq_mamba_ssd_bwd_workspace": (_sz, [_i64, _i64, _i64]),
     "msq_mamba_ssd_bwd": (_i, [_p, _i64, _p, _p, _i64, _p, _p, _i64, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _i64,
-                               _i64, _i64, _i64, _p]),
+                               _i64, _i64, _i64, _p, _p]),
     "msq_mamba_conv_bwd": (_i, [_p, _p, _i64, _p, _i64, _i, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "msq_relattn_bwd_workspace": (_sz, [_i, _i64, _i64, _i64]),
     "msq_relattn_bwd": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64,

@@ -12,6 +12,7 @@
 //   gate : y * silu(z) -> RMSNorm(eps) * w
 // Backward kernels mirror these (chunked SSD backward, reverse over chunks).
 #include "common.h"
+#include "attn_tiles.h"
 
 namespace {
 
@@ -647,10 +648,583 @@ void allow_lds(K kernel, size_t bytes) {
     hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+
+// ================================================================== SSD, bf16 MFMA chunk-parallel path
+// The sequential walk over chunks above keeps one workgroup per (batch, head)
+// busy for the whole sequence with fp32 FMA products read from LDS. The bf16
+// path splits the same SSD block form (mamba_ssm's chunk_state / state_passing
+// / chunk_scan) into three launches:
+//   state : per (b, h, chunk)  S_c = sum_s e^{cum_last - cum_s} dt_s x_s B_s^T    [p][n]
+//   pass  : per (b, h, p, n)   H_c = entry state: H_0 = 0, H_{c+1} = e^{cum_last_c} H_c + S_c
+//                              (in place over S; the entry states are what the backward reads)
+//   out   : per (b, h, chunk)  y = (C B^T o L) (dt x) + e^{cum_t} C H_c^T + D x
+// with every 64x64x64 product on v_mfma_f32_16x16x32_bf16 (bf16 operands -- x, B, C
+// are the bf16 conv output; dt x, the decay-masked C B^T and H are rounded to bf16 as
+// mamba_ssm's Triton kernels do -- fp32 accumulation). Tiles live in LDS as 64-row
+// images with 256-B rows in the dual swizzle of cdna_hip_programming.md T10 (b), read
+// either as K-contiguous rows (ds_read_b128) or transposed (ds_read_b64_tr_b16).
+namespace ssd2 {
+using attn::cat8;
+using attn::tr_read;
+constexpr int IMG = 64 * 256;  // bytes of one tile image
+
+__device__ __forceinline__ int offd(int row, int ch) {
+    return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+}
+// An image holds two 64-column tiles side by side: half 0 in chunks 0-7, half 1
+// in chunks 8-15 (offd is a bijection on (row, chunk), so they never collide).
+// K-contiguous fragment: image rows rb .. rb+15, k = 32 ks + 8 g .. +7 of tile half hf
+__device__ __forceinline__ bf16x8 fk(const char* s, int rb, int ks, int lane, int hf) {
+    return *(const bf16x8*)(s + offd(rb + (lane & 15), 8 * hf + ks * 4 + (lane >> 4)));
+}
+// transposed fragment: image rows are k (32 ks + 8 g + 0..3 / 4..7), columns cb + (lane & 15)
+// of tile half hf
+__device__ __forceinline__ bf16x8 fm(const char* s, int cb, int ks, int lane, int hf) {
+    const int i = lane & 15, q = i >> 2, pp = i & 3, g = lane >> 4;
+    const int kA = ks * 32 + 8 * g + q, ch = 8 * hf + (cb >> 3) + (pp >> 1), sub = (pp & 1) * 8;
+    return cat8(tr_read(s, offd(kA, ch) + sub), tr_read(s, offd(kA + 4, ch) + sub));
+}
+// acc[i][j] (lane (il, g), element r) = sum_k A[rb + 16 i + il][k] Bt[cb + 16 j + 4 g + r][k]
+// over k < 64; A rows from image sa (K-contiguous, or transposed when AT), Bt rows likewise
+template <bool AT, bool BT>
+__device__ __forceinline__ void mm(f32x4 (&acc)[2][2], const char* sa, int ha, const char* sb, int hb, int rb, int cb,
+                                   int lane) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 av[2], bv[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            av[i] = AT ? fm(sa, rb + 16 * i, ks, lane, ha) : fk(sa, rb + 16 * i, ks, lane, ha);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            bv[j] = BT ? fm(sb, cb + 16 * j, ks, lane, hb) : fk(sb, cb + 16 * j, ks, lane, hb);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = attn::mfma(bv[j], av[i], acc[i][j]);
+    }
+}
+__device__ __forceinline__ void zero22(f32x4 (&a)[2][2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) a[i][j] = attn::zero4();
+}
+__device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
+    union { u32x4 u; bf16 e[8]; } r;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r.e[k] = (bf16)v[k];
+    return r.u;
+}
+__device__ __forceinline__ void unpack8(u32x4 u, float (&v)[8]) {
+    union { u32x4 u; bf16 e[8]; } r;
+    r.u = u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = (float)r.e[k];
+}
+
+// chunk geometry + dt / cumulative decay of one (b, h, chunk); threads 0..63 (wave 0)
+struct Chunk {
+    int64_t b, h, c, t0;
+    int nval;
+};
+__device__ __forceinline__ Chunk chunk_of(const MambaArgs& a, int nch) {
+    Chunk k;
+    const int64_t bh = blockIdx.x / nch;
+    k.c = blockIdx.x % nch;
+    k.b = bh / a.nheads;
+    k.h = bh % a.nheads;
+    k.t0 = k.c * Q;
+    k.nval = (int)min<int64_t>(Q, a.L - k.t0);
+    return k;
+}
+__device__ __forceinline__ void dt_cum(const MambaArgs& a, const Chunk& k, const bf16* zx, const float* dt_bias,
+                                       float A, float* sdt, float* scum, int tid) {
+    if (tid < 64) {
+        const int64_t t = k.t0 + tid;
+        float d = 0.f;
+        if (tid < k.nval) d = softplus((float)zx[(k.b * a.L + t) * a.ldz + a.d_inner + a.conv_dim + k.h] + dt_bias[k.h]);
+        sdt[tid] = d;
+        float v = d * A;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const float u = __shfl_up(v, o, 64);
+            if (tid >= o) v += u;
+        }
+        scum[tid] = v;
+    }
+}
+// 16-B chunk e (row e >> 3, chunk e & 7) of a 64-column bf16 tile starting at column col0 of xc rows
+__device__ __forceinline__ u32x4 ld_chunk(const MambaArgs& a, const Chunk& k, const bf16* xc, int64_t col0, int e) {
+    const int row = e >> 3, ch = e & 7;
+    if (row >= k.nval) return (u32x4){0u, 0u, 0u, 0u};
+    return *(const u32x4*)(xc + (k.b * a.L + k.t0 + row) * a.ldxc + col0 + ch * 8);
+}
+
+// state: S_c [p][n] into the chunk's slot of `states`, e^{cum_last} factor into clast
+__global__ __launch_bounds__(256) void state_kernel(MambaArgs a, const bf16* __restrict__ xc,
+                                                    const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
+                                                    const float* __restrict__ A_log, float* __restrict__ states,
+                                                    float* __restrict__ clast, int nch) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* sXB = smem;  // half 0: dt x e^{cum_last - cum_s} [s][p]; half 1: B [s][n]
+    float* sdt = (float*)(smem + IMG);
+    float* scum = sdt + 64;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const Chunk k = chunk_of(a, nch);
+    const float A = -expf(A_log[k.h]);
+    u32x4 xr[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int e = tid + 256 * u;
+        xr[u] = ld_chunk(a, k, xc, k.h * P, e);
+        *(u32x4*)(sXB + offd(e >> 3, 8 + (e & 7))) = ld_chunk(a, k, xc, a.d_inner, e);
+    }
+    dt_cum(a, k, zx, dt_bias, A, sdt, scum, tid);
+    __syncthreads();
+    const float cl = scum[k.nval - 1];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int e = tid + 256 * u, row = e >> 3;
+        const float f = row < k.nval ? sdt[row] * expf(cl - scum[row]) : 0.f;
+        float v[8];
+        unpack8(xr[u], v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] *= f;
+        *(u32x4*)(sXB + offd(row, e & 7)) = pack8(v);
+    }
+    __syncthreads();
+    f32x4 acc[2][2];
+    zero22(acc);
+    const int rb = 32 * (w >> 1), cb = 32 * (w & 1);
+    mm<true, true>(acc, sXB, 0, sXB, 1, rb, cb, lane);  // [p][n] = sum_s X[s][p] B[s][n]
+    float* st = states + ((k.b * a.nheads + k.h) * nch + k.c) * (int64_t)(P * N);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            *(f32x4*)(st + (rb + 16 * i + (lane & 15)) * N + cb + 16 * j + 4 * (lane >> 4)) = acc[i][j];
+    if (tid == 0) clast[(k.b * a.nheads + k.h) * nch + k.c] = cl;
+}
+
+// pass: in place over the per-chunk S, H_0 = 0, H_{c+1} = e^{cum_last_c} H_c + S_c
+__global__ __launch_bounds__(256) void pass_kernel(float* __restrict__ states, const float* __restrict__ clast,
+                                                   int64_t nbh, int nch) {
+    const int64_t e = blockIdx.x * 256LL + threadIdx.x;  // (bh, p, n)
+    if (e >= nbh * P * N) return;
+    const int64_t bh = e / (P * N), pn = e % (P * N);
+    float* st = states + bh * nch * (int64_t)(P * N) + pn;
+    const float* cl = clast + bh * nch;
+    float hcur = 0.f;
+    for (int c = 0; c < nch; ++c) {
+        const float sc = st[(int64_t)c * P * N];
+        st[(int64_t)c * P * N] = hcur;
+        hcur = expf(cl[c]) * hcur + sc;
+    }
+}
+
+// out: y = (C B^T o L) (dt x) + e^{cum_t} C H_c^T + D x
+__global__ __launch_bounds__(256) void out_kernel(MambaArgs a, const bf16* __restrict__ xc,
+                                                  const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
+                                                  const float* __restrict__ A_log, const float* __restrict__ Dp,
+                                                  float* __restrict__ y, int64_t ldy, const float* __restrict__ states,
+                                                  int nch) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* sCB = smem;           // half 0: C [t][n];     half 1: B [s][n]
+    char* sXH = smem + IMG;     // half 0: dt x [s][p];  half 1: H [p][n]
+    char* sM = smem + 2 * IMG;  // half 0: (C B^T) o L [t][s]
+    float* sdt = (float*)(smem + 3 * IMG);
+    float* scum = sdt + 64;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, il = lane & 15, g = lane >> 4;
+    const Chunk k = chunk_of(a, nch);
+    const float A = -expf(A_log[k.h]), Dh = Dp[k.h];
+    u32x4 xr[2];
+    const float* st = states + ((k.b * a.nheads + k.h) * nch + k.c) * (int64_t)(P * N);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
+        xr[u] = ld_chunk(a, k, xc, k.h * P, e);
+        *(u32x4*)(sCB + offd(row, 8 + ch)) = ld_chunk(a, k, xc, a.d_inner, e);
+        *(u32x4*)(sCB + offd(row, ch)) = ld_chunk(a, k, xc, a.d_inner + N, e);
+        const f32x4 h0 = *(const f32x4*)(st + row * N + ch * 8), h1 = *(const f32x4*)(st + row * N + ch * 8 + 4);
+        const float hv[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        *(u32x4*)(sXH + offd(row, 8 + ch)) = pack8(hv);
+    }
+    dt_cum(a, k, zx, dt_bias, A, sdt, scum, tid);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int e = tid + 256 * u, row = e >> 3;
+        float v[8];
+        unpack8(xr[u], v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] *= sdt[row];
+        *(u32x4*)(sXH + offd(row, e & 7)) = pack8(v);
+    }
+    const int rb = 32 * (w >> 1), cb = 32 * (w & 1);
+    f32x4 gm[2][2], y2[2][2];
+    zero22(gm);
+    zero22(y2);
+    mm<false, false>(gm, sCB, 0, sCB, 1, rb, cb, lane);  // [t][s] = sum_n C[t][n] B[s][n]
+    mm<false, false>(y2, sCB, 0, sXH, 1, rb, cb, lane);  // [t][p] = sum_n C[t][n] H[p][n]
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int t = rb + 16 * i + il, s0 = cb + 16 * j + 4 * g;
+            union { uint64_t u; bf16 e[4]; } mv;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int s = s0 + r;
+                mv.e[r] = (bf16)(s <= t ? gm[i][j][r] * expf(scum[t] - scum[s]) : 0.f);
+            }
+            *(uint64_t*)(sM + offd(t, s0 >> 3) + (s0 & 7) * 2) = mv.u;
+        }
+    __syncthreads();
+    f32x4 y1[2][2];
+    zero22(y1);
+    mm<false, true>(y1, sM, 0, sXH, 0, rb, cb, lane);  // [t][p] = sum_s M[t][s] X[s][p]
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int t = rb + 16 * i + il;
+        if (t >= k.nval) continue;
+        const float et = expf(scum[t]);
+        const int64_t row = k.b * a.L + k.t0 + t;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int pcol = cb + 16 * j + 4 * g;
+            const f32x4 xv = load4(xc + row * a.ldxc + k.h * P + pcol);
+            *(f32x4*)(y + row * ldy + k.h * P + pcol) = y1[i][j] + et * y2[i][j] + Dh * xv;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- SSD backward, bf16 MFMA path
+// dH_c = gradient of the chunk-EXIT state (= entry of chunk c+1) satisfies the
+// reverse recurrence dH_{c-1} = e^{cum_last_c} dH_c + U_c, U_c = sum_t e^{cum_t} dY_t^T C_t:
+//   uterm : per (b, h, chunk)  U_c   [p][n]            (into the workspace)
+//   rpass : per (b, h, p, n)   in place U -> dH (exit gradient of every chunk)
+//   grad  : per (b, h, chunk)  everything else from (H_c entry, dH_c exit): the eight
+//           64^3 products of the chunk backward on MFMA, dx / dB / dC / ddt and the
+//           per-head parameter gradients (the same algebra as ssd_bwd_kernel above).
+__global__ __launch_bounds__(256) void uterm_kernel(MambaArgs a, const bf16* __restrict__ xc,
+                                                    const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
+                                                    const float* __restrict__ A_log, const float* __restrict__ dY,
+                                                    int64_t ldy, float* __restrict__ U, int nch) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* sYC = smem;  // half 0: e^{cum_t} dY [t][p]; half 1: C [t][n]
+    float* sdt = (float*)(smem + IMG);
+    float* scum = sdt + 64;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const Chunk k = chunk_of(a, nch);
+    const float A = -expf(A_log[k.h]);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int e = tid + 256 * u;
+        *(u32x4*)(sYC + offd(e >> 3, 8 + (e & 7))) = ld_chunk(a, k, xc, a.d_inner + N, e);
+    }
+    dt_cum(a, k, zx, dt_bias, A, sdt, scum, tid);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (row < k.nval) {
+            const float* src = dY + (k.b * a.L + k.t0 + row) * ldy + k.h * P + ch * 8;
+            const f32x4 d0 = *(const f32x4*)src, d1 = *(const f32x4*)(src + 4);
+            const float et = expf(scum[row]);
+            v[0] = d0[0] * et; v[1] = d0[1] * et; v[2] = d0[2] * et; v[3] = d0[3] * et;
+            v[4] = d1[0] * et; v[5] = d1[1] * et; v[6] = d1[2] * et; v[7] = d1[3] * et;
+        }
+        *(u32x4*)(sYC + offd(row, ch)) = pack8(v);
+    }
+    __syncthreads();
+    f32x4 acc[2][2];
+    zero22(acc);
+    const int rb = 32 * (w >> 1), cb = 32 * (w & 1);
+    mm<true, true>(acc, sYC, 0, sYC, 1, rb, cb, lane);  // [p][n] = sum_t Ys[t][p] C[t][n]
+    float* dst = U + ((k.b * a.nheads + k.h) * nch + k.c) * (int64_t)(P * N);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            *(f32x4*)(dst + (rb + 16 * i + (lane & 15)) * N + cb + 16 * j + 4 * (lane >> 4)) = acc[i][j];
+}
+
+// in place: dH = 0; for c = last .. 0: out[c] = dH; dH = e^{cum_last_c} dH + U_c
+__global__ __launch_bounds__(256) void rpass_kernel(float* __restrict__ U, const float* __restrict__ clast,
+                                                    int64_t nbh, int nch) {
+    const int64_t e = blockIdx.x * 256LL + threadIdx.x;
+    if (e >= nbh * P * N) return;
+    const int64_t bh = e / (P * N), pn = e % (P * N);
+    float* u = U + bh * nch * (int64_t)(P * N) + pn;
+    const float* cl = clast + bh * nch;
+    float d = 0.f;
+    for (int c = nch - 1; c >= 0; --c) {
+        const float uc = u[(int64_t)c * P * N];
+        u[(int64_t)c * P * N] = d;
+        d = expf(cl[c]) * d + uc;
+    }
+}
+
+template <typename TD>
+__global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* __restrict__ xc,
+                                                      const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
+                                                      const float* __restrict__ A_log, const float* __restrict__ Dp,
+                                                      const float* __restrict__ dY, int64_t ldy,
+                                                      const float* __restrict__ states, const float* __restrict__ dHx,
+                                                      float* __restrict__ dxc, TD* __restrict__ dzx,
+                                                      float* __restrict__ gA_log, float* __restrict__ gD,
+                                                      float* __restrict__ gdt_bias, int nch) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* sCB = smem;            // C [t][n]   | B [s][n]
+    char* sXY = smem + IMG;      // dt x [s][p] | dY [t][p]
+    char* sHD = smem + 2 * IMG;  // H [p][n]   | dH [p][n]
+    char* sMG = smem + 3 * IMG;  // M [t][s]   | dG [t][s]
+    float* sdt = (float*)(smem + 4 * IMG);
+    float* scum = sdt + 64;
+    float* sdcum = scum + 64;
+    float* sddt = sdcum + 64;
+    float* sred = sddt + 64;  // 8 block-reduction slots
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, il = lane & 15, g = lane >> 4;
+    const Chunk k = chunk_of(a, nch);
+    const float A = -expf(A_log[k.h]), Dh = Dp[k.h];
+    const int64_t slot = ((k.b * a.nheads + k.h) * nch + k.c) * (int64_t)(P * N);
+    const float* Hs = states + slot;
+    const float* dHs = dHx + slot;
+    u32x4 xr[2];
+    float hdh = 0.f;  // sum dH o H (the cum_last term)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
+        xr[u] = ld_chunk(a, k, xc, k.h * P, e);
+        *(u32x4*)(sCB + offd(row, 8 + ch)) = ld_chunk(a, k, xc, a.d_inner, e);
+        *(u32x4*)(sCB + offd(row, ch)) = ld_chunk(a, k, xc, a.d_inner + N, e);
+        float hv[8], dv[8], yv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        {
+            const f32x4 h0 = *(const f32x4*)(Hs + row * N + ch * 8), h1 = *(const f32x4*)(Hs + row * N + ch * 8 + 4);
+            const f32x4 d0 = *(const f32x4*)(dHs + row * N + ch * 8), d1 = *(const f32x4*)(dHs + row * N + ch * 8 + 4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) hv[q] = h0[q], hv[4 + q] = h1[q], dv[q] = d0[q], dv[4 + q] = d1[q];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) hdh += hv[q] * dv[q];
+        }
+        if (row < k.nval) {
+            const float* src = dY + (k.b * a.L + k.t0 + row) * ldy + k.h * P + ch * 8;
+            const f32x4 d0 = *(const f32x4*)src, d1 = *(const f32x4*)(src + 4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) yv[q] = d0[q], yv[4 + q] = d1[q];
+        }
+        *(u32x4*)(sHD + offd(row, ch)) = pack8(hv);
+        *(u32x4*)(sHD + offd(row, 8 + ch)) = pack8(dv);
+        *(u32x4*)(sXY + offd(row, 8 + ch)) = pack8(yv);
+    }
+    dt_cum(a, k, zx, dt_bias, A, sdt, scum, tid);
+    if (tid < 64) sdcum[tid] = sddt[tid] = 0.f;
+    hdh = wave_sum(hdh);
+    if (lane == 0) sred[w] = hdh;
+    __syncthreads();
+    const int nv = k.nval;
+    const float cl = scum[nv - 1];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int e = tid + 256 * u, row = e >> 3;
+        float v[8];
+        unpack8(xr[u], v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] *= sdt[row];
+        *(u32x4*)(sXY + offd(row, e & 7)) = pack8(v);
+    }
+    const int rb = 32 * (w >> 1), cb = 32 * (w & 1);
+    // M = (C B^T) o L ; dM = dY XS^T (s <= t)
+    f32x4 mt[2][2], dm[2][2];
+    zero22(mt);
+    mm<false, false>(mt, sCB, 0, sCB, 1, rb, cb, lane);  // [t][s]
+    __syncthreads();  // XS written
+    zero22(dm);
+    mm<false, false>(dm, sXY, 1, sXY, 0, rb, cb, lane);  // [t][s] = sum_p dY[t][p] XS[s][p]
+    float rowq[2] = {0.f, 0.f}, colq[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) colq[q] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int t = rb + 16 * i + il, s0 = cb + 16 * j + 4 * g;
+            union { uint64_t u; bf16 e[4]; } mv, gv;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int s = s0 + r;
+                const float L_ = s <= t ? expf(scum[t] - scum[s]) : 0.f;
+                const float m = mt[i][j][r] * L_;
+                const float d = s <= t ? dm[i][j][r] : 0.f;
+                const float q = d * m;
+                rowq[i] += q;
+                colq[j * 4 + r] += q;
+                mv.e[r] = (bf16)m;
+                gv.e[r] = (bf16)(d * L_);
+            }
+            *(uint64_t*)(sMG + offd(t, s0 >> 3) + (s0 & 7) * 2) = mv.u;
+            *(uint64_t*)(sMG + offd(t, 8 + (s0 >> 3)) + (s0 & 7) * 2) = gv.u;
+        }
+    // dcum_t += sum_s dM M ; dcum_s -= sum_t dM M
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        float v = rowq[i];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if (g == 0) atomicAdd(&sdcum[rb + 16 * i + il], v);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        float v = colq[q];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+        if (il == 0) atomicAdd(&sdcum[cb + 16 * (q >> 2) + 4 * g + (q & 3)], -v);
+    }
+    __syncthreads();  // M, dG images
+    // dXS = M^T dY + w_s (B dH^T) ; dx = dXS dt + D dY ; ddt_s += sum_p dXS x ; dcum_s -= w_s sum_p XS t1
+    f32x4 dxs[2][2], t1[2][2];
+    zero22(dxs);
+    zero22(t1);
+    mm<true, true>(dxs, sMG, 0, sXY, 1, rb, cb, lane);   // [s][p] = sum_t M[t][s] dY[t][p]
+    mm<false, false>(t1, sCB, 1, sHD, 1, rb, cb, lane);  // [s][p] = sum_n B[s][n] dH[p][n]
+    float gd = 0.f, dws_tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int s = rb + 16 * i + il;
+        const float ws = s < nv ? expf(cl - scum[s]) : 0.f;
+        float ddt_p = 0.f, dws = 0.f;
+        const int64_t row = k.b * a.L + k.t0 + s;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int pc = cb + 16 * j + 4 * g;
+            f32x4 xv = (f32x4){0.f, 0.f, 0.f, 0.f}, yv = xv;
+            if (s < nv) {
+                xv = load4(xc + row * a.ldxc + k.h * P + pc);
+                yv = *(const f32x4*)(dY + row * ldy + k.h * P + pc);
+            }
+            f32x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float tot = dxs[i][j][r] + ws * t1[i][j][r];
+                ddt_p += tot * xv[r];
+                dws += xv[r] * sdt[s] * t1[i][j][r] * ws;
+                gd += yv[r] * xv[r];
+                o[r] = tot * sdt[s] + Dh * yv[r];
+            }
+            if (s < nv) *(f32x4*)(dxc + row * a.ldxc + k.h * P + pc) = o;
+        }
+        ddt_p += __shfl_xor(ddt_p, 16, 64);
+        ddt_p += __shfl_xor(ddt_p, 32, 64);
+        dws += __shfl_xor(dws, 16, 64);
+        dws += __shfl_xor(dws, 32, 64);
+        if (g == 0) {
+            atomicAdd(&sddt[s], ddt_p);
+            atomicAdd(&sdcum[s], -dws);
+        }
+        dws_tot += dws;  // every g holds the same row sum: counted once below
+    }
+    // dC = dG B + e^{cum_t} dY H ; dcum_t += e^{cum_t} sum_n C dyh
+    {
+        f32x4 dc[2][2], dyh[2][2];
+        zero22(dc);
+        zero22(dyh);
+        mm<false, true>(dc, sMG, 1, sCB, 1, rb, cb, lane);   // [t][n] = sum_s dG[t][s] B[s][n]
+        mm<false, true>(dyh, sXY, 1, sHD, 0, rb, cb, lane);  // [t][n] = sum_p dY[t][p] H[p][n]
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int t = rb + 16 * i + il;
+            const float et = expf(scum[t]);
+            float rs = 0.f;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int n0 = cb + 16 * j + 4 * g;
+                union { uint64_t u; bf16 e[4]; } cv;
+                cv.u = *(const uint64_t*)(sCB + offd(t, n0 >> 3) + (n0 & 7) * 2);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    rs += et * (float)cv.e[r] * dyh[i][j][r];
+                    dc[i][j][r] += et * dyh[i][j][r];
+                }
+                if (t < nv) {
+                    float* rowp = dxc + (k.b * a.L + k.t0 + t) * a.ldxc + a.d_inner + N + n0;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) atomicAdd(rowp + r, dc[i][j][r]);
+                }
+            }
+            rs += __shfl_xor(rs, 16, 64);
+            rs += __shfl_xor(rs, 32, 64);
+            if (g == 0) atomicAdd(&sdcum[t], rs);
+        }
+    }
+    // dB = dG^T C + w_s (XS dH)
+    {
+        f32x4 db[2][2], tb[2][2];
+        zero22(db);
+        zero22(tb);
+        mm<true, true>(db, sMG, 1, sCB, 0, rb, cb, lane);    // [s][n] = sum_t dG[t][s] C[t][n]
+        mm<false, true>(tb, sXY, 0, sHD, 1, rb, cb, lane);   // [s][n] = sum_p XS[s][p] dH[p][n]
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int s = rb + 16 * i + il;
+            if (s >= nv) continue;
+            const float ws = expf(cl - scum[s]);
+            float* rowp = dxc + (k.b * a.L + k.t0 + s) * a.ldxc + a.d_inner;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) atomicAdd(rowp + cb + 16 * j + 4 * g + r, db[i][j][r] + ws * tb[i][j][r]);
+        }
+    }
+    // dcum_last += sum_s dws_s + e^{cum_last} sum dH o H
+    dws_tot = wave_sum(dws_tot) * 0.25f;  // each row sum was held by its 4 g-lanes
+    gd = wave_sum(gd);
+    if (lane == 0) {
+        atomicAdd(&sdcum[nv - 1], dws_tot);
+        sred[4 + w] = gd;
+    }
+    __syncthreads();
+    if (tid == 0) sdcum[nv - 1] += expf(cl) * (sred[0] + sred[1] + sred[2] + sred[3]);
+    __syncthreads();
+    if (tid < 64) {
+        // da_t = sum_{tau >= t} dcum_tau ; ddt = A da + sum_p dXS x ; d dt_raw = ddt sigmoid(raw)
+        float v = tid < nv ? sdcum[tid] : 0.f;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const float u = __shfl_down(v, o, 64);
+            if (tid + o < 64) v += u;
+        }
+        float gA = 0.f, gdb = 0.f;
+        if (tid < nv) {
+            const int64_t t = k.t0 + tid;
+            const float ddt = A * v + sddt[tid];
+            gA = sdt[tid] * v;
+            const float raw = (float)zx[(k.b * a.L + t) * a.ldz + a.d_inner + a.conv_dim + k.h] + dt_bias[k.h];
+            const float draw = ddt * sigm(raw);
+            dzx[(k.b * a.L + t) * a.ldz + a.d_inner + a.conv_dim + k.h] = (TD)draw;
+            gdb = draw;
+        }
+        gA = wave_sum(gA);
+        gdb = wave_sum(gdb);
+        if (tid == 0) {
+            atomicAdd(gA_log + k.h, gA * A);  // A = -exp(A_log) -> dA/dA_log = A
+            atomicAdd(gdt_bias + k.h, gdb);
+            atomicAdd(gD + k.h, sred[4] + sred[5] + sred[6] + sred[7]);
+        }
+    }
+}
+
+constexpr size_t UTERM_LDS = IMG + 512, GRAD_LDS = 4 * IMG + 2048;  // + sdt, scum, sdcum, sddt, sred
+
+constexpr size_t STATE_LDS = IMG + 512, OUT_LDS = 3 * IMG + 512;
+}  // namespace ssd2
 }  // namespace
 
 extern "C" size_t msq_mamba_states_size(int64_t B, int64_t L, int64_t nheads) {
-    return (size_t)B * nheads * ((L + Q - 1) / Q) * P * N * sizeof(float);
+    // chunk-entry states [B][H][nch][P][N] + per-chunk decay sums cum_last [B][H][nch]
+    const int64_t nch = (L + Q - 1) / Q;
+    return (size_t)B * nheads * nch * (P * N + 1) * sizeof(float);
 }
 
 #define MAMBA_CHECK()                                                                                         \
@@ -678,6 +1252,21 @@ extern "C" int msq_mamba_ssd_fwd(float* y, int64_t ldy, float* states, const voi
     MAMBA_CHECK();
     const MambaArgs a = mk(B, L, d_inner, nheads, ldz, ldxc);
     hipStream_t s = (hipStream_t)stream;
+    const int nch = (int)((L + Q - 1) / Q);
+    if (dtype == MSQ_BF16 && !getenv("MSQ_MAMBA_SSD_V1")) {
+        float* clast = states + B * nheads * nch * (int64_t)(P * N);
+        const dim3 gch((unsigned)(B * nheads * nch));
+        allow_lds(ssd2::state_kernel, ssd2::STATE_LDS);
+        allow_lds(ssd2::out_kernel, ssd2::OUT_LDS);
+        hipLaunchKernelGGL(ssd2::state_kernel, gch, dim3(256), ssd2::STATE_LDS, s, a, (const bf16*)xc,
+                           (const bf16*)zxbcdt, dt_bias, A_log, states, clast, nch);
+        hipLaunchKernelGGL(ssd2::pass_kernel, dim3((unsigned)((B * nheads * P * N + 255) / 256)), dim3(256), 0, s,
+                           states, clast, B * nheads, nch);
+        hipLaunchKernelGGL(ssd2::out_kernel, gch, dim3(256), ssd2::OUT_LDS, s, a, (const bf16*)xc,
+                           (const bf16*)zxbcdt, dt_bias, A_log, D, y, ldy, states, nch);
+        MSQ_LAUNCH_CHECK();
+        return MSQ_OK;
+    }
     const dim3 grid((unsigned)(B * nheads));
     allow_lds(ssd_fwd_kernel<bf16>, FWD_LDS);
     allow_lds(ssd_fwd_kernel<float>, FWD_LDS);
@@ -711,17 +1300,39 @@ extern "C" int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const float* y, int
     return MSQ_OK;
 }
 
+extern "C" size_t msq_mamba_ssd_bwd_workspace(int64_t B, int64_t L, int64_t nheads) {
+    return (size_t)B * nheads * ((L + Q - 1) / Q) * P * N * sizeof(float);
+}
+
 extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, const float* dY, int64_t ldy,
                                  const float* states, const void* xc, int64_t ldxc, const void* zxbcdt, int64_t ldz,
                                  int dtype, const float* dt_bias, const float* A_log, const float* D, float* gA_log,
                                  float* gD, float* gdt_bias, int64_t B, int64_t L, int64_t d_inner, int64_t nheads,
-                                 void* stream) {
+                                 void* workspace, void* stream) {
     MAMBA_CHECK();
     MSQ_CHECK_ARG(ld_dxc == ldxc, "msq_mamba_ssd_bwd: dxc must share the xBC row stride");
     const MambaArgs a = mk(B, L, d_inner, nheads, ldz, ldxc);
     hipStream_t s = (hipStream_t)stream;
     // dB / dC columns are accumulated with atomics across heads
     hipMemset2DAsync(dxc + d_inner, ldxc * sizeof(float), 0, 2 * N * sizeof(float), B * L, s);
+    if (dtype == MSQ_BF16 && !getenv("MSQ_MAMBA_SSD_V1")) {
+        MSQ_CHECK_ARG(workspace, "msq_mamba_ssd_bwd: the bf16 path needs msq_mamba_ssd_bwd_workspace() bytes");
+        const int nch = (int)((L + Q - 1) / Q);
+        const float* clast = states + B * nheads * nch * (int64_t)(P * N);
+        float* U = (float*)workspace;
+        const dim3 gch((unsigned)(B * nheads * nch));
+        allow_lds(ssd2::uterm_kernel, ssd2::UTERM_LDS);
+        allow_lds(ssd2::grad_kernel<bf16>, ssd2::GRAD_LDS);
+        hipLaunchKernelGGL(ssd2::uterm_kernel, gch, dim3(256), ssd2::UTERM_LDS, s, a, (const bf16*)xc,
+                           (const bf16*)zxbcdt, dt_bias, A_log, dY, ldy, U, nch);
+        hipLaunchKernelGGL(ssd2::rpass_kernel, dim3((unsigned)((B * nheads * P * N + 255) / 256)), dim3(256), 0, s,
+                           U, clast, B * nheads, nch);
+        hipLaunchKernelGGL(ssd2::grad_kernel<bf16>, gch, dim3(256), ssd2::GRAD_LDS, s, a, (const bf16*)xc,
+                           (const bf16*)zxbcdt, dt_bias, A_log, D, dY, ldy, states, U, dxc, (bf16*)dzxbcdt, gA_log,
+                           gD, gdt_bias, nch);
+        MSQ_LAUNCH_CHECK();
+        return MSQ_OK;
+    }
     const dim3 grid((unsigned)(B * nheads));
     allow_lds(ssd_bwd_kernel<bf16, bf16>, BWD_LDS);
     allow_lds(ssd_bwd_kernel<float, float>, BWD_LDS);

@@ -242,6 +242,8 @@ class MambaEngine:
                           seg=(T, N_META))
         if hook is not None:
             hook("head")
+        # per-chunk state gradients of the bf16 SSD backward (msq_mamba_ssd_bwd_workspace)
+        ssd_ws = ops.workspace(L.lib().msq_mamba_ssd_bwd_workspace(Bb, Ll, H), self.device, "ssd_bwd")
         for l in reversed(range(cfg.n_layers)):
             gin = gxb
             if self.act == torch.bfloat16:
@@ -255,7 +257,7 @@ class MambaEngine:
             call("msq_mamba_ssd_bwd", ptr(Bw["dxc"]), cfg.conv_dim, ptr(Bw["dzx"]), ptr(Bw["dy"]), di,
                  ptr(A.states[l]), ptr(A.xc[l]), cfg.conv_dim, ptr(A.zx[l]), cfg.d_in_proj, dtc,
                  ptr(P[f"{l}.dt_bias"]), ptr(P[f"{l}.A_log"]), ptr(P[f"{l}.D"]), ptr(G[f"{l}.A_log"]), ptr(G[f"{l}.D"]),
-                 ptr(G[f"{l}.dt_bias"]), Bb, Ll, di, H, s)
+                 ptr(G[f"{l}.dt_bias"]), Bb, Ll, di, H, ptr(ssd_ws), s)
             call("msq_mamba_conv_bwd", ptr(Bw["dzx"]), ptr(Bw["dxc"]), cfg.conv_dim, ptr(A.zx[l]), cfg.d_in_proj, dtc,
                  ptr(P[f"{l}.conv_w"]), ptr(P[f"{l}.conv_b"]), ptr(G[f"{l}.conv_w"]), ptr(G[f"{l}.conv_b"]), Bb, Ll,
                  di, H, s)

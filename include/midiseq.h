@@ -224,11 +224,14 @@ int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const float* y, int64_t ldy, c
                         int dtype, const float* w, const float* rstd, const float* dout, int64_t ldd, float* dw,
                         int64_t rows, int64_t d_inner, void* stream);
 /* dxc fp32 [B*L, ldxc]: dx (written) | dB, dC (reduced over heads); dt_raw
- * grads into dzxbcdt[:, d_inner+conv_dim+h]; gA_log / gD / gdt_bias accumulate. */
+ * grads into dzxbcdt[:, d_inner+conv_dim+h]; gA_log / gD / gdt_bias accumulate.
+ * workspace: msq_mamba_ssd_bwd_workspace() bytes (the bf16 path's per-chunk
+ * state gradients; the fp32 path ignores it and accepts NULL).               */
+size_t msq_mamba_ssd_bwd_workspace(int64_t B, int64_t L, int64_t nheads);
 int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, const float* dY, int64_t ldy, const float* states,
                       const void* xc, int64_t ldxc, const void* zxbcdt, int64_t ldz, int dtype, const float* dt_bias,
                       const float* A_log, const float* D, float* gA_log, float* gD, float* gdt_bias, int64_t B,
-                      int64_t L, int64_t d_inner, int64_t nheads, void* stream);
+                      int64_t L, int64_t d_inner, int64_t nheads, void* workspace, void* stream);
 /* d(xBC_raw) into dzxbcdt[:, d_inner : d_inner+conv_dim]; conv grads accumulate. */
 int msq_mamba_conv_bwd(void* dzxbcdt, const float* dxc, int64_t ld_dxc, const void* zxbcdt, int64_t ldz, int dtype,
                        const float* conv_w, const float* conv_b, float* g_conv_w, float* g_conv_b, int64_t B,
