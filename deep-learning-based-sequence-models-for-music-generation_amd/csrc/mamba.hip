@@ -52,56 +52,78 @@ __global__ void conv_fwd_kernel(MambaArgs a, const T* __restrict__ zx, const flo
 }
 
 // dpre = dout * silu'(pre); dzx_in[t] = sum_k w[k] dpre[t+3-k]; dw, dbias via per-block partials (atomics)
+// block: 64 channels (lanes) x 4 waves; wave ws walks the contiguous time segment
+// [t0, t1) of CONV_SEG steps with a sliding window: each input and each dout is
+// loaded once (plus a 3-step halo), pre / dpre computed once per step.
+constexpr int CONV_SEG = 64;
 template <typename T, typename TD>
-__global__ void conv_bwd_kernel(MambaArgs a, const T* __restrict__ zx, const float* __restrict__ w,
-                                const float* __restrict__ bias, const float* __restrict__ dout, int64_t ldd,
-                                TD* __restrict__ dzx, float* __restrict__ dw, float* __restrict__ dbias) {
-    // block: 64 channels x 4 time-slices; grid (conv_dim/64, B, tchunks)
+__global__ __launch_bounds__(256) void conv_bwd_kernel(MambaArgs a, const T* __restrict__ zx, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, const float* __restrict__ dout,
+                                                       int64_t ldd, TD* __restrict__ dzx, float* __restrict__ dw,
+                                                       float* __restrict__ dbias) {
+    __shared__ float red[4][5][64];
     const int lane = threadIdx.x & 63, ws = threadIdx.x >> 6;
     const int64_t c = blockIdx.x * 64 + lane;
     const int64_t b = blockIdx.y;
-    const int64_t per = (a.L + gridDim.z - 1) / gridDim.z;
-    const int64_t t0 = blockIdx.z * per, t1 = min(a.L, t0 + per);
-    if (c >= a.conv_dim) return;
-    const T* src = zx + b * a.L * a.ldz + a.d_inner + c;
-    const float* dsrc = dout + b * a.L * ldd + c;
-    float wk[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) wk[k] = w[c * 4 + k];
-    const float bc = bias[c];
-    auto pre_at = [&](int64_t t) {
-        float acc = bc;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t tt = t - 3 + k;
-            if (tt >= 0) acc += wk[k] * (float)src[tt * a.ldz];
-        }
-        return acc;
-    };
-    auto dpre_at = [&](int64_t t) {
-        if (t >= a.L) return 0.f;
-        const float p = pre_at(t);
-        const float s = sigm(p);
-        return dsrc[t * ldd] * s * (1.f + p * (1.f - s));
-    };
+    const int64_t t0 = ((int64_t)blockIdx.z * 4 + ws) * CONV_SEG, t1 = min(a.L, t0 + CONV_SEG);
     float gw[4] = {0.f, 0.f, 0.f, 0.f}, gb = 0.f;
-    for (int64_t t = t0 + ws; t < t1; t += 4) {
-        // d input at time t: sum_k w[k] * dpre[t + 3 - k]
-        float di = 0.f;
+    if (c < a.conv_dim && t0 < a.L) {
+        const T* src = zx + b * a.L * a.ldz + a.d_inner + c;
+        const float* dsrc = dout + b * a.L * ldd + c;
+        float wk[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) di += wk[k] * dpre_at(t + 3 - k);
-        dzx[(b * a.L + t) * a.ldz + a.d_inner + c] = (TD)di;
-        const float dp = dpre_at(t);
-        gb += dp;
+        for (int k = 0; k < 4; ++k) wk[k] = w[c * 4 + k];
+        const float bc = bias[c];
+        // input window in[tau-3 .. tau], dpre ring of tau-3 .. tau
+        float win[4], dp[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t tt = t - 3 + k;
-            if (tt >= 0) gw[k] += dp * (float)src[tt * a.ldz];
+        for (int k = 0; k < 3; ++k) {
+            const int64_t tt = t0 - 3 + k;
+            win[k + 1] = tt >= 0 ? (float)src[tt * a.ldz] : 0.f;
+        }
+        const int64_t tend = min(a.L, t1 + 3);
+        for (int64_t tau = t0; tau < t1 + 3; ++tau) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) win[k] = win[k + 1], dp[k] = dp[k + 1];
+            float d = 0.f;
+            if (tau < tend) {
+                win[3] = (float)src[tau * a.ldz];
+                float pre = bc;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) pre += wk[k] * win[k];
+                const float sg = sigm(pre);
+                d = dsrc[tau * ldd] * sg * (1.f + pre * (1.f - sg));
+                if (tau < t1) {
+                    gb += d;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) gw[k] += d * win[k];
+                }
+            } else {
+                win[3] = 0.f;
+            }
+            dp[3] = d;
+            // dzx_in[tau - 3] = sum_k w[k] dpre[tau - k]
+            const int64_t t = tau - 3;
+            if (t >= t0 && t < t1) {
+                float di = 0.f;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) di += wk[k] * dp[3 - k];
+                dzx[(b * a.L + t) * a.ldz + a.d_inner + c] = (TD)di;
+            }
         }
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) atomicAdd(dw + c * 4 + k, gw[k]);
-    atomicAdd(dbias + c, gb);
+    for (int k = 0; k < 4; ++k) red[ws][k][lane] = gw[k];
+    red[ws][4][lane] = gb;
+    __syncthreads();
+    if (ws == 0 && c < a.conv_dim) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const float v = red[0][k][lane] + red[1][k][lane] + red[2][k][lane] + red[3][k][lane];
+            if (k < 4) atomicAdd(dw + c * 4 + k, v);
+            else atomicAdd(dbias + c, v);
+        }
+    }
 }
 
 // ------------------------------------------------------------------ 64^3 tile product helper
@@ -578,7 +600,10 @@ __global__ __launch_bounds__(256) void gnorm_fwd_kernel(const float* __restrict_
 }
 
 // dn = dout*w ; dg = r (dn - n mean(dn n)) ; dy = dg silu(z) ; dz = dg y silu'(z) ; dw += dout n
-template <typename TZ, typename TD>
+// One wave per row, the row's y / z / dout held in registers (one HBM pass):
+// lane owns columns 4 lane + 256 k, k < NK (NK = ceil(d_inner / 256), compile time).
+constexpr int GN_K = 16;
+template <typename TZ, typename TD, int NK>
 __global__ __launch_bounds__(256) void gnorm_bwd_kernel(const float* __restrict__ y, int64_t ldy,
                                                         const TZ* __restrict__ z, int64_t ldz,
                                                         const float* __restrict__ w, const float* __restrict__ rstd,
@@ -586,51 +611,74 @@ __global__ __launch_bounds__(256) void gnorm_bwd_kernel(const float* __restrict_
                                                         float* __restrict__ dy, TD* __restrict__ dz,
                                                         float* __restrict__ dw, int64_t rows, int dn) {
     const int lane = threadIdx.x & 63;
-    // per-thread column partials for dw: block handles a stride of rows
-    float pw[64];
+    float pw[NK][4];
 #pragma unroll
-    for (int i = 0; i < 64; ++i) pw[i] = 0.f;
+    for (int k = 0; k < NK; ++k) pw[k][0] = pw[k][1] = pw[k][2] = pw[k][3] = 0.f;
     for (int64_t row = blockIdx.x * 4LL + (threadIdx.x >> 6); row < rows; row += (int64_t)gridDim.x * 4) {
         const float r = rstd[row];
+        f32x4 yv[NK], zv[NK], dv[NK];
         float s = 0.f;
-        for (int c = lane * 4; c < dn; c += 256) {
-            const f32x4 yv = *(const f32x4*)(y + row * ldy + c);
-            const f32x4 zv = load4(z + row * ldz + c);
-            const f32x4 dv = *(const f32x4*)(dout + row * ldd + c);
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const int c = lane * 4 + 256 * k;
+            yv[k] = zv[k] = dv[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (c < dn) {
+                yv[k] = *(const f32x4*)(y + row * ldy + c);
+                zv[k] = load4(z + row * ldz + c);
+                dv[k] = *(const f32x4*)(dout + row * ldd + c);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const int c = lane * 4 + 256 * k;
+            if (c >= dn) continue;
             const f32x4 wv = *(const f32x4*)(w + c);
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const float n = yv[t] * silu(zv[t]) * r;
-                s += dv[t] * wv[t] * n;
-            }
+            for (int t = 0; t < 4; ++t) s += dv[k][t] * wv[t] * yv[k][t] * silu(zv[k][t]) * r;
         }
         const float mdn = wave_sum(s) / dn;
-        int k = 0;
-        for (int c = lane * 4; c < dn; c += 256, ++k) {
-            const f32x4 yv = *(const f32x4*)(y + row * ldy + c);
-            const f32x4 zv = load4(z + row * ldz + c);
-            const f32x4 dv = *(const f32x4*)(dout + row * ldd + c);
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const int c = lane * 4 + 256 * k;
+            if (c >= dn) continue;
             const f32x4 wv = *(const f32x4*)(w + c);
-            f32x4 o;
-            float zo[4];
+            f32x4 o, zo;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                const float sg = sigm(zv[t]);
-                const float sl = zv[t] * sg;
-                const float n = yv[t] * sl * r;
-                const float dg = r * (dv[t] * wv[t] - n * mdn);
+                const float sg = sigm(zv[k][t]);
+                const float sl = zv[k][t] * sg;
+                const float n = yv[k][t] * sl * r;
+                const float dg = r * (dv[k][t] * wv[t] - n * mdn);
                 o[t] = dg * sl;
-                zo[t] = dg * yv[t] * sg * (1.f + zv[t] * (1.f - sg));
-                if (k < 16) pw[k * 4 + t] += dv[t] * n;
+                zo[t] = dg * yv[k][t] * sg * (1.f + zv[k][t] * (1.f - sg));
+                pw[k][t] += dv[k][t] * n;
             }
             *(f32x4*)(dy + row * ldy + c) = o;
-            store4(dz + row * ldz + c, (f32x4){zo[0], zo[1], zo[2], zo[3]});
+            store4(dz + row * ldz + c, zo);
         }
     }
-    int k = 0;
-    for (int c = lane * 4; c < dn && k < 16; c += 256, ++k)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) atomicAdd(dw + c + t, pw[k * 4 + t]);
+    for (int k = 0; k < NK; ++k) {
+        const int c = lane * 4 + 256 * k;
+        if (c >= dn) continue;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) atomicAdd(dw + c + t, pw[k][t]);
+    }
+}
+
+template <typename TZ, typename TD>
+void gnorm_bwd_launch(dim3 grid, hipStream_t s, const float* y, int64_t ldy, const TZ* z, int64_t ldz, const float* w,
+                      const float* rstd, const float* dout, int64_t ldd, float* dy, TD* dz, float* dw, int64_t rows,
+                      int dn) {
+    const int need = (dn + 255) / 256;
+#define GN(K) hipLaunchKernelGGL((gnorm_bwd_kernel<TZ, TD, K>), grid, dim3(256), 0, s, y, ldy, z, ldz, w, rstd, dout, \
+                                 ldd, dy, dz, dw, rows, dn)
+    if (need <= 1) GN(1);
+    else if (need <= 2) GN(2);
+    else if (need <= 4) GN(4);
+    else if (need <= 8) GN(8);
+    else GN(16);
+#undef GN
 }
 
 MambaArgs mk(int64_t B, int64_t L, int64_t d_inner, int64_t nheads, int64_t ldz, int64_t ldxc) {
@@ -973,7 +1021,8 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
                                                       const float* __restrict__ A_log, const float* __restrict__ Dp,
                                                       const float* __restrict__ dY, int64_t ldy,
                                                       const float* __restrict__ states, const float* __restrict__ dHx,
-                                                      float* __restrict__ dxc, TD* __restrict__ dzx,
+                                                      float* __restrict__ dxc, float* __restrict__ dbc,
+                                                      TD* __restrict__ dzx,
                                                       float* __restrict__ gA_log, float* __restrict__ gD,
                                                       float* __restrict__ gdt_bias, int nch) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1147,11 +1196,8 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
                     rs += et * (float)cv.e[r] * dyh[i][j][r];
                     dc[i][j][r] += et * dyh[i][j][r];
                 }
-                if (t < nv) {
-                    float* rowp = dxc + (k.b * a.L + k.t0 + t) * a.ldxc + a.d_inner + N + n0;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) atomicAdd(rowp + r, dc[i][j][r]);
-                }
+                if (t < nv)  // this head's dC row (summed over heads by dbc_reduce_kernel)
+                    *(f32x4*)(dbc + ((k.b * a.L + k.t0 + t) * a.nheads + k.h) * (2 * N) + N + n0) = dc[i][j];
             }
             rs += __shfl_xor(rs, 16, 64);
             rs += __shfl_xor(rs, 32, 64);
@@ -1170,11 +1216,9 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
             const int s = rb + 16 * i + il;
             if (s >= nv) continue;
             const float ws = expf(cl - scum[s]);
-            float* rowp = dxc + (k.b * a.L + k.t0 + s) * a.ldxc + a.d_inner;
+            float* rowp = dbc + ((k.b * a.L + k.t0 + s) * a.nheads + k.h) * (2 * N);
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) atomicAdd(rowp + cb + 16 * j + 4 * g + r, db[i][j][r] + ws * tb[i][j][r]);
+            for (int j = 0; j < 2; ++j) *(f32x4*)(rowp + cb + 16 * j + 4 * g) = db[i][j] + ws * tb[i][j];
         }
     }
     // dcum_last += sum_s dws_s + e^{cum_last} sum dH o H
@@ -1213,6 +1257,18 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
             atomicAdd(gD + k.h, sred[4] + sred[5] + sred[6] + sred[7]);
         }
     }
+}
+
+// dxc[bt][d_inner + c] = sum_h dbc[bt][h][c]   (dB | dC, c < 2N)
+__global__ __launch_bounds__(256) void dbc_reduce_kernel(const float* __restrict__ dbc, float* __restrict__ dxc,
+                                                         int64_t rows, int64_t nheads, int64_t ldxc, int64_t d_inner) {
+    const int64_t e = blockIdx.x * 256LL + threadIdx.x;  // (row, 4-column group)
+    if (e >= rows * (2 * N / 4)) return;
+    const int64_t row = e / (2 * N / 4), c = (e % (2 * N / 4)) * 4;
+    const float* p = dbc + row * nheads * (2 * N) + c;
+    f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int64_t h = 0; h < nheads; ++h) acc += *(const f32x4*)(p + h * (2 * N));
+    *(f32x4*)(dxc + row * ldxc + d_inner + c) = acc;
 }
 
 constexpr size_t UTERM_LDS = IMG + 512, GRAD_LDS = 4 * IMG + 2048;  // + sdt, scum, sdcum, sddt, sred
@@ -1291,17 +1347,22 @@ extern "C" int msq_mamba_gnorm_fwd(void* out, int64_t ldo, float* rstd, const fl
 extern "C" int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const float* y, int64_t ldy, const void* zxbcdt,
                                    int64_t ldz, int dtype, const float* w, const float* rstd, const float* dout,
                                    int64_t ldd, float* dw, int64_t rows, int64_t d_inner, void* stream) {
-    MSQ_CHECK_ARG(rows > 0 && d_inner % 4 == 0 && d_inner <= 4096, "mamba gnorm bwd: bad sizes");
+    MSQ_CHECK_ARG(rows > 0 && d_inner % 4 == 0 && d_inner <= 256 * GN_K, "mamba gnorm bwd: bad sizes");
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid(1024);
-    if (dtype == MSQ_BF16) hipLaunchKernelGGL((gnorm_bwd_kernel<bf16, bf16>), grid, dim3(256), 0, s, y, ldy, (const bf16*)zxbcdt, ldz, w, rstd, dout, ldd, dy, (bf16*)dzxbcdt, dw, rows, (int)d_inner);
-    else hipLaunchKernelGGL((gnorm_bwd_kernel<float, float>), grid, dim3(256), 0, s, y, ldy, (const float*)zxbcdt, ldz, w, rstd, dout, ldd, dy, (float*)dzxbcdt, dw, rows, (int)d_inner);
+    if (dtype == MSQ_BF16)
+        gnorm_bwd_launch<bf16, bf16>(grid, s, y, ldy, (const bf16*)zxbcdt, ldz, w, rstd, dout, ldd, dy, (bf16*)dzxbcdt,
+                                     dw, rows, (int)d_inner);
+    else
+        gnorm_bwd_launch<float, float>(grid, s, y, ldy, (const float*)zxbcdt, ldz, w, rstd, dout, ldd, dy,
+                                       (float*)dzxbcdt, dw, rows, (int)d_inner);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }
 
 extern "C" size_t msq_mamba_ssd_bwd_workspace(int64_t B, int64_t L, int64_t nheads) {
-    return (size_t)B * nheads * ((L + Q - 1) / Q) * P * N * sizeof(float);
+    // per-chunk state gradients [B][H][nch][P][N] | per-head dB, dC rows [B*L][H][2N]
+    return (size_t)B * nheads * ((L + Q - 1) / Q) * P * N * sizeof(float) + (size_t)B * L * nheads * 2 * N * sizeof(float);
 }
 
 extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, const float* dY, int64_t ldy,
@@ -1314,12 +1375,12 @@ extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, cons
     const MambaArgs a = mk(B, L, d_inner, nheads, ldz, ldxc);
     hipStream_t s = (hipStream_t)stream;
     // dB / dC columns are accumulated with atomics across heads
-    hipMemset2DAsync(dxc + d_inner, ldxc * sizeof(float), 0, 2 * N * sizeof(float), B * L, s);
     if (dtype == MSQ_BF16 && !getenv("MSQ_MAMBA_SSD_V1")) {
         MSQ_CHECK_ARG(workspace, "msq_mamba_ssd_bwd: the bf16 path needs msq_mamba_ssd_bwd_workspace() bytes");
         const int nch = (int)((L + Q - 1) / Q);
         const float* clast = states + B * nheads * nch * (int64_t)(P * N);
         float* U = (float*)workspace;
+        float* dbc = U + B * nheads * nch * (int64_t)(P * N);
         const dim3 gch((unsigned)(B * nheads * nch));
         allow_lds(ssd2::uterm_kernel, ssd2::UTERM_LDS);
         allow_lds(ssd2::grad_kernel<bf16>, ssd2::GRAD_LDS);
@@ -1328,11 +1389,14 @@ extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, cons
         hipLaunchKernelGGL(ssd2::rpass_kernel, dim3((unsigned)((B * nheads * P * N + 255) / 256)), dim3(256), 0, s,
                            U, clast, B * nheads, nch);
         hipLaunchKernelGGL(ssd2::grad_kernel<bf16>, gch, dim3(256), ssd2::GRAD_LDS, s, a, (const bf16*)xc,
-                           (const bf16*)zxbcdt, dt_bias, A_log, D, dY, ldy, states, U, dxc, (bf16*)dzxbcdt, gA_log,
-                           gD, gdt_bias, nch);
+                           (const bf16*)zxbcdt, dt_bias, A_log, D, dY, ldy, states, U, dxc, dbc, (bf16*)dzxbcdt,
+                           gA_log, gD, gdt_bias, nch);
+        hipLaunchKernelGGL(ssd2::dbc_reduce_kernel, dim3((unsigned)((B * L * (2 * N / 4) + 255) / 256)), dim3(256), 0,
+                           s, dbc, dxc, B * L, nheads, ldxc, d_inner);
         MSQ_LAUNCH_CHECK();
         return MSQ_OK;
     }
+    hipMemset2DAsync(dxc + d_inner, ldxc * sizeof(float), 0, 2 * N * sizeof(float), B * L, s);
     const dim3 grid((unsigned)(B * nheads));
     allow_lds(ssd_bwd_kernel<bf16, bf16>, BWD_LDS);
     allow_lds(ssd_bwd_kernel<float, float>, BWD_LDS);
@@ -1349,7 +1413,7 @@ extern "C" int msq_mamba_conv_bwd(void* dzxbcdt, const float* dxc, int64_t ld_dx
     MSQ_CHECK_ARG(B > 0 && L > 0 && d_inner == nheads * P && ldz % 4 == 0, "mamba conv bwd: bad sizes");
     const MambaArgs a = mk(B, L, d_inner, nheads, ldz, ld_dxc);
     hipStream_t s = (hipStream_t)stream;
-    const unsigned tch = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, L / 64));
+    const unsigned tch = (unsigned)((L + 4 * CONV_SEG - 1) / (4 * CONV_SEG));
     const dim3 grid((unsigned)((a.conv_dim + 63) / 64), (unsigned)B, tch);
     if (dtype == MSQ_BF16) hipLaunchKernelGGL((conv_bwd_kernel<bf16, bf16>), grid, dim3(256), 0, s, a, (const bf16*)zxbcdt, conv_w, conv_b, dxc, ld_dxc, (bf16*)dzxbcdt, g_conv_w, g_conv_b);
     else hipLaunchKernelGGL((conv_bwd_kernel<float, float>), grid, dim3(256), 0, s, a, (const float*)zxbcdt, conv_w, conv_b, dxc, ld_dxc, (float*)dzxbcdt, g_conv_w, g_conv_b);
