@@ -33,21 +33,36 @@ __device__ __forceinline__ float softplus(float x) { return x > 20.f ? x : log1p
 
 // ------------------------------------------------------------------ conv
 // out[b,t,c] = silu(bias[c] + sum_k w[c,k] * in[b, t-3+k, c]), in = zxbcdt[:, off + c]
+// block: 64 channels (lanes) x 4 waves, each wave a contiguous segment of CONV_SEG
+// steps with a sliding 4-tap window (one load per input element)
+constexpr int CONV_SEG = 64;
 template <typename T, typename TO>
-__global__ void conv_fwd_kernel(MambaArgs a, const T* __restrict__ zx, const float* __restrict__ w,
-                                const float* __restrict__ bias, TO* __restrict__ out) {
-    const int64_t total = a.B * a.L * a.conv_dim;
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t c = e % a.conv_dim, bt = e / a.conv_dim;
-        const int64_t t = bt % a.L;
-        const T* src = zx + bt * a.ldz + a.d_inner + c;
-        float acc = bias[c];
+__global__ __launch_bounds__(256) void conv_fwd_kernel(MambaArgs a, const T* __restrict__ zx, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, TO* __restrict__ out) {
+    const int lane = threadIdx.x & 63, ws = threadIdx.x >> 6;
+    const int64_t c = blockIdx.x * 64 + lane;
+    const int64_t b = blockIdx.y;
+    const int64_t t0 = ((int64_t)blockIdx.z * 4 + ws) * CONV_SEG, t1 = min(a.L, t0 + CONV_SEG);
+    if (c >= a.conv_dim || t0 >= a.L) return;
+    const T* src = zx + b * a.L * a.ldz + a.d_inner + c;
+    TO* dst = out + b * a.L * a.ldxc + c;
+    float wk[4], win[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t tt = t - 3 + k;
-            if (tt >= 0) acc += w[c * 4 + k] * (float)src[(k - 3) * a.ldz];
-        }
-        out[bt * a.ldxc + c] = (TO)silu(acc);
+    for (int k = 0; k < 4; ++k) wk[k] = w[c * 4 + k];
+    const float bc = bias[c];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int64_t tt = t0 - 3 + k;
+        win[k + 1] = tt >= 0 ? (float)src[tt * a.ldz] : 0.f;
+    }
+    for (int64_t t = t0; t < t1; ++t) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) win[k] = win[k + 1];
+        win[3] = (float)src[t * a.ldz];
+        float acc = bc;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc += wk[k] * win[k];
+        dst[t * a.ldxc] = (TO)silu(acc);
     }
 }
 
@@ -55,7 +70,6 @@ __global__ void conv_fwd_kernel(MambaArgs a, const T* __restrict__ zx, const flo
 // block: 64 channels (lanes) x 4 waves; wave ws walks the contiguous time segment
 // [t0, t1) of CONV_SEG steps with a sliding window: each input and each dout is
 // loaded once (plus a 3-step halo), pre / dpre computed once per step.
-constexpr int CONV_SEG = 64;
 template <typename T, typename TD>
 __global__ __launch_bounds__(256) void conv_bwd_kernel(MambaArgs a, const T* __restrict__ zx, const float* __restrict__ w,
                                                        const float* __restrict__ bias, const float* __restrict__ dout,
@@ -657,13 +671,15 @@ __global__ __launch_bounds__(256) void gnorm_bwd_kernel(const float* __restrict_
             store4(dz + row * ldz + c, zo);
         }
     }
+    // dw: the 4 waves' column partials summed in LDS, then one atomic per column per block
+    __shared__ float red[4][256 * NK];
+    const int ws = threadIdx.x >> 6;
 #pragma unroll
-    for (int k = 0; k < NK; ++k) {
-        const int c = lane * 4 + 256 * k;
-        if (c >= dn) continue;
+    for (int k = 0; k < NK; ++k)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) atomicAdd(dw + c + t, pw[k][t]);
-    }
+        for (int t = 0; t < 4; ++t) red[ws][lane * 4 + 256 * k + t] = pw[k][t];
+    __syncthreads();
+    for (int c = threadIdx.x; c < dn; c += 256) atomicAdd(dw + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
 }
 
 template <typename TZ, typename TD>
@@ -1292,11 +1308,10 @@ extern "C" int msq_mamba_conv_fwd(void* xc, int64_t ldxc, const void* zxbcdt, in
                                   int64_t nheads, void* stream) {
     MAMBA_CHECK();
     const MambaArgs a = mk(B, L, d_inner, nheads, ldz, ldxc);
-    const int64_t total = B * L * a.conv_dim;
-    const int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
+    const dim3 grid((unsigned)((a.conv_dim + 63) / 64), (unsigned)B, (unsigned)((L + 4 * CONV_SEG - 1) / (4 * CONV_SEG)));
     hipStream_t s = (hipStream_t)stream;
-    if (dtype == MSQ_BF16) hipLaunchKernelGGL((conv_fwd_kernel<bf16, bf16>), dim3(grid), dim3(256), 0, s, a, (const bf16*)zxbcdt, conv_w, conv_b, (bf16*)xc);
-    else hipLaunchKernelGGL((conv_fwd_kernel<float, float>), dim3(grid), dim3(256), 0, s, a, (const float*)zxbcdt, conv_w, conv_b, (float*)xc);
+    if (dtype == MSQ_BF16) hipLaunchKernelGGL((conv_fwd_kernel<bf16, bf16>), grid, dim3(256), 0, s, a, (const bf16*)zxbcdt, conv_w, conv_b, (bf16*)xc);
+    else hipLaunchKernelGGL((conv_fwd_kernel<float, float>), grid, dim3(256), 0, s, a, (const float*)zxbcdt, conv_w, conv_b, (float*)xc);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }
@@ -1349,7 +1364,7 @@ extern "C" int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const float* y, int
                                    int64_t ldd, float* dw, int64_t rows, int64_t d_inner, void* stream) {
     MSQ_CHECK_ARG(rows > 0 && d_inner % 4 == 0 && d_inner <= 256 * GN_K, "mamba gnorm bwd: bad sizes");
     hipStream_t s = (hipStream_t)stream;
-    const dim3 grid(1024);
+    const dim3 grid(512);  // two workgroups per CU; each reduces its dw partials in LDS first
     if (dtype == MSQ_BF16)
         gnorm_bwd_launch<bf16, bf16>(grid, s, y, ldy, (const bf16*)zxbcdt, ldz, w, rstd, dout, ldd, dy, (bf16*)dzxbcdt,
                                      dw, rows, (int)d_inner);
