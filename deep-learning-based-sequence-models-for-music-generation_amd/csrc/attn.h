@@ -8,8 +8,9 @@ struct AttnArgs {
     const void* qkv; int64_t ldq;  // [B*S, ldq]: q | k | v, head h at col h*hs
     const void* R;                 // [H, S_max, hs]
     // attention-probability dropout (model_transformer.py:80); null = none.
-    // keep bit of (b,h,i,j): rowmask[((b*H+h)*S+i)*mask_ld + j/32] >> (j%32),
-    // the same bit transposed in colmask (dropout.hip); kept p scaled by keep_scale
+    // keep bit of (b,h,i,j) in the block-transposed words of dropout.hip:
+    // rowmask (uint32) [((bh*nb + i/64)*nb + j/64)*64 + i%64][j%64 / 32] >> (j%32),
+    // colmask the same with (i, j) swapped; nb = mask_ld / 2; kept p scaled by keep_scale
     const uint32_t* rowmask = nullptr;
     const uint32_t* colmask = nullptr;
     int64_t mask_ld = 0;
@@ -17,7 +18,19 @@ struct AttnArgs {
 };
 
 __device__ __forceinline__ float keep_bit(const AttnArgs& a, int64_t bh, int64_t i, int64_t j) {
-    return (a.rowmask[(bh * a.S + i) * a.mask_ld + (j >> 5)] >> (j & 31)) & 1u ? a.keep_scale : 0.f;
+    const int64_t nb = a.mask_ld >> 1;
+    const int64_t w = (((bh * nb + (i >> 6)) * nb + (j >> 6)) * 64 + (i & 63)) * 2 + ((j >> 5) & 1);
+    return (a.rowmask[w] >> (j & 31)) & 1u ? a.keep_scale : 0.f;
+}
+
+// bytes of one (b,h)'s mask words in either layout
+__host__ __device__ __forceinline__ int64_t mask_bh_bytes(int64_t mask_ld) {
+    return (mask_ld >> 1) * (mask_ld >> 1) * 512;
+}
+// uint32 word offset, inside one (b,h), of the words of row `r` (query for rowmask,
+// key for colmask) against 32 columns starting at c (c % 32 == 0)
+__host__ __device__ __forceinline__ int64_t mask_word(int64_t mask_ld, int64_t r, int64_t c) {
+    return (((r >> 6) * (mask_ld >> 1) + (c >> 6)) * 64 + (r & 63)) * 2 + ((c >> 5) & 1);
 }
 
 // exact fp32 path (attn_exact.hip)

@@ -136,13 +136,13 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const 
     };
     const int64_t mld = a.mask_ld;
     const __amdgpu_buffer_rsrc_t rm =
-        make_rsrc(DROP ? (const void*)(a.colmask + (int64_t)(b * H + h) * S * mld) : (const void*)a.R,
-                  DROP ? (uint32_t)(S * mld * 4) : 0u);
+        make_rsrc(DROP ? (const void*)(a.colmask + (int64_t)(b * H + h) * (mask_bh_bytes(mld) / 4)) : (const void*)a.R,
+                  DROP ? (uint32_t)mask_bh_bytes(mld) : 0u);
     auto stage_m = [&](int t) {  // keep words colmask[b,h,j][i0/32] of the block's keys (waves 2-3)
         if (DROP && w >= 2 && w < 4) {
             const int i0 = it0 + QT * t, key = j0 + 64 * (w - 2) + lane;
             dma4(rm, smem + O_D + (t & 1) * KB * 4 + (w - 2) * 256,
-                 key < S ? (uint32_t)((key * mld + i0 / 32) * 4) : OOB);
+                 key < S ? (uint32_t)(mask_word(mld, key, i0) * 4) : OOB);
         }
     };
     auto stage_r = [&](int c) {  // R chunk c into ring slot c % NCH
@@ -300,7 +300,7 @@ int flash_bwd_kv3(const AttnArgs& a, const float* lse, const float* Dv, const bf
         attr = true;
     }
     if (a.S * a.ldq * 2 >= (int64_t)OOB || a.S * ldo * 2 >= (int64_t)OOB || a.n_meta > 8) return -1;
-    if (a.colmask && a.S * a.mask_ld * 4 >= (int64_t)OOB) return -1;
+    if (a.colmask && mask_bh_bytes(a.mask_ld) >= (int64_t)OOB) return -1;
     const dim3 grid((unsigned)((a.S + KB - 1) / KB), (unsigned)a.H, (unsigned)a.B);
     if (a.colmask)
         hipLaunchKernelGGL(flash_bwd_kv3_kernel<true>, grid, dim3(NT), LDS_BYTES, s, a, lse, Dv, dout, ldo, dqkv, ldd,

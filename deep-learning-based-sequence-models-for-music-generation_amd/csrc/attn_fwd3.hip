@@ -123,12 +123,12 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
     // keep words rowmask[b,h,i][kt]: waves 0-3 stage the block's 256 queries
     const int64_t mld = a.mask_ld;
     const __amdgpu_buffer_rsrc_t rm =
-        make_rsrc(DROP ? (const void*)(a.rowmask + (int64_t)(b * H + h) * S * mld) : (const void*)a.R,
-                  DROP ? (uint32_t)(S * mld * 4) : 0u);
+        make_rsrc(DROP ? (const void*)(a.rowmask + (int64_t)(b * H + h) * (mask_bh_bytes(mld) / 4)) : (const void*)a.R,
+                  DROP ? (uint32_t)mask_bh_bytes(mld) : 0u);
     auto stage_m = [&](int kt, int buf) {
         if (DROP && w < 4) {
             const int iq = i0 + 64 * w + lane;
-            const uint32_t vo = (iq >= 0 && iq < S) ? (uint32_t)((iq * mld + kt) * 4) : OOB;
+            const uint32_t vo = (iq >= 0 && iq < S) ? (uint32_t)(mask_word(mld, iq, 32 * kt) * 4) : OOB;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, (lds_char*)(smem + O_D + buf * QB * 4 + w * 256), 4, vo, 0,
                                                      0, 0);
         }
@@ -330,7 +330,7 @@ int flash_fwd3(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_
                                   LDS_BYTES);
         attr = true;
     }
-    if (a.rowmask && a.S * a.mask_ld * 4 >= (int64_t)OOB) return -1;
+    if (a.rowmask && mask_bh_bytes(a.mask_ld) >= (int64_t)OOB) return -1;
     if (a.S * a.ldq * 2 >= (int64_t)OOB || a.S * HS * 2 >= (int64_t)OOB || a.n_meta > 8) return -1;
     const dim3 grid((unsigned)((a.S + QB - 1) / QB), (unsigned)a.H, (unsigned)a.B);
     if (a.rowmask) hipLaunchKernelGGL((flash_fwd3_kernel<0, true>), grid, dim3(NT), LDS_BYTES, s, a, out, ldo, lse);

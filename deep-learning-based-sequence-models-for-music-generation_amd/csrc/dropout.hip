@@ -2,10 +2,12 @@
 // softmax output, model_transformer.py:80), drawn once per layer and step
 // from the counter-based hash of common.h.
 //
-// Two bit layouts of the same mask, both [B, H, S, ld] uint32 words
-// (ld = 2 * ceil(S / 64)):
-//   rowmask[b,h,i][w] bit t = keep(i, j = 32 w + t)   (forward: lanes own queries)
-//   colmask[b,h,j][w] bit t = keep(i = 32 w + t, j)   (backward: lanes own keys)
+// Two bit layouts of the same mask, both block-transposed: with nb = ceil(S/64)
+// one (b,h) owns nb*nb*64 uint64 words, 64 per 64x64 block, so the 64 words of
+// a block are one contiguous 512-B store of the wave that draws it:
+//   rowmask[((bh*nb + i/64)*nb + j/64)*64 + i%64] bit j%64 = keep(i, j)   (forward: lanes own queries)
+//   colmask[((bh*nb + j/64)*nb + i/64)*64 + j%64] bit i%64 = keep(i, j)   (backward: lanes own keys)
+// (as uint32 words: low word = keys / queries 0-31 of the block, high = 32-63).
 // One wave computes one 64x64 block of the causal lower block triangle: lane l
 // holds key j = 64 jb + l; per query row the 64 keep bits come out of one
 // __ballot (the row word), and each lane collects bit l of those ballots into
@@ -15,11 +17,14 @@
 
 namespace {
 
+// v_writelane_b32 (llvm.amdgcn.writelane): lane `lane` of `old` := uniform `val`
+__device__ int amdgcn_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
 __global__ __launch_bounds__(256) void attn_mask_kernel(uint32_t* __restrict__ rowmask, uint32_t* __restrict__ colmask,
                                                         int S, int ld, int nb, int ntri, int H, uint32_t seed,
                                                         uint32_t site0, uint32_t thr) {
     const int lane = threadIdx.x & 63;
-    const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int task = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     const int bh = blockIdx.y;
     if (task >= ntri) return;
     // task -> (ib, jb <= ib) of the lower block triangle
@@ -27,26 +32,50 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(uint32_t* __restrict__ r
     while (ib * (ib + 1) / 2 > task) --ib;
     while ((ib + 1) * (ib + 2) / 2 <= task) ++ib;
     const int jb = task - ib * (ib + 1) / 2;
-    (void)nb;
     const uint32_t base = drop_base(seed, site0 + (uint32_t)bh);
-    const uint32_t rk = drop_row(base, (uint32_t)(ib * 64 + lane));  // lane l: query row 64 ib + l
-    const uint32_t ck = (uint32_t)(jb * 64 + lane) * 0x85ebca6bu;   // lane l: key 64 jb + l
-    uint64_t myrow = 0, mycol = 0;
+    const uint32_t ck = (uint32_t)(jb * 64 + lane) * 0x85ebca6bu;  // lane l: key 64 jb + l
+    // row words: query row 64 ib + ii is one ballot; its row key is wave-uniform
+    // (scalar unit), written into lane ii with v_writelane
+    uint32_t rlo = 0, rhi = 0;
+#pragma unroll 16
     for (int ii = 0; ii < 64; ++ii) {
-        const uint32_t rki = __builtin_amdgcn_readlane(rk, ii);
-        const bool kp = drop_mix(rki ^ ck) >= thr;
-        const uint64_t bal = __ballot(kp);
-        myrow = lane == ii ? bal : myrow;
-        mycol |= ((bal >> lane) & 1ull) << ii;
+        const uint32_t rki = drop_row(base, (uint32_t)(ib * 64 + ii));
+        const uint64_t bal = __ballot(drop_mix(rki ^ ck) >= thr);
+        rlo = (uint32_t)amdgcn_writelane((int)(uint32_t)bal, ii, (int)rlo);
+        rhi = (uint32_t)amdgcn_writelane((int)(uint32_t)(bal >> 32), ii, (int)rhi);
     }
-    const int i = ib * 64 + lane, j = jb * 64 + lane;
-    if (i < S) *(uint64_t*)(rowmask + ((int64_t)bh * S + i) * ld + 2 * jb) = myrow;
-    if (j < S) *(uint64_t*)(colmask + ((int64_t)bh * S + j) * ld + 2 * ib) = mycol;
+    const uint64_t myrow = ((uint64_t)rhi << 32) | rlo;
+    // column words: 64x64 bit transpose across the wave, six butterfly stages;
+    // at stage s element (r, c) with r&s == 0, c&s != 0 swaps with (r+s, c-s)
+    uint64_t t = myrow;
+    const uint64_t hi_s[6] = {0xFFFFFFFF00000000ull, 0xFFFF0000FFFF0000ull, 0xFF00FF00FF00FF00ull,
+                              0xF0F0F0F0F0F0F0F0ull, 0xCCCCCCCCCCCCCCCCull, 0xAAAAAAAAAAAAAAAAull};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int sh = 32 >> k;
+        const uint64_t hm = hi_s[k];
+        const uint32_t plo = (uint32_t)__shfl_xor((int)(uint32_t)t, sh);
+        const uint32_t phi = (uint32_t)__shfl_xor((int)(uint32_t)(t >> 32), sh);
+        const uint64_t pt = ((uint64_t)phi << 32) | plo;
+        const uint64_t up = 0ull - (uint64_t)((lane >> (5 - k)) & 1);  // all ones on lanes with bit sh
+        t = (t & (hm ^ ~up)) | (((pt & hm) >> sh) & up) | (((pt & ~hm) << sh) & ~up);
+    }
+    const uint64_t mycol = t;
+    (void)S;
+    (void)ld;
+    const int64_t bhb = (int64_t)bh * nb;
+    ((uint64_t*)rowmask)[((bhb + ib) * nb + jb) * 64 + lane] = myrow;
+    ((uint64_t*)colmask)[((bhb + jb) * nb + ib) * 64 + lane] = mycol;
 }
 
 }  // namespace
 
 extern "C" int64_t msq_dropout_mask_ld(int64_t S) { return 2 * ((S + 63) / 64); }
+
+extern "C" int64_t msq_dropout_mask_words(int64_t B, int64_t H, int64_t S) {
+    const int64_t nb = (S + 63) / 64;
+    return B * H * nb * nb * 128;
+}
 
 extern "C" int msq_dropout_attn_mask(uint32_t* rowmask, uint32_t* colmask, int64_t B, int64_t H, int64_t S,
                                      uint32_t seed, uint32_t site0, float p, void* stream) {

@@ -145,8 +145,7 @@ def adam_step(p, g, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, shadow=Non
 
 def dropout_attn_mask(B, H, S, seed, site0, p, device, out=None):
     """(rowmask, colmask) keep bits of one layer's attention dropout (msq_dropout_attn_mask)."""
-    ld = L.lib().msq_dropout_mask_ld(S)
     if out is None:
-        out = torch.zeros(2, B * H * S * ld, device=device, dtype=torch.int32)
+        out = torch.zeros(2, L.lib().msq_dropout_mask_words(B, H, S), device=device, dtype=torch.int32)
     call("msq_dropout_attn_mask", ptr(out[0]), ptr(out[1]), B, H, S, int(seed), int(site0), float(p), stream())
     return out

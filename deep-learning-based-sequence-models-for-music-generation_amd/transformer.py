@@ -173,8 +173,7 @@ class _Acts:
 
     def masks(self, cfg, device):
         if self._masks is None:
-            ld = L.lib().msq_dropout_mask_ld(self.S)
-            n = self.B * cfg.n_heads * self.S * ld
+            n = L.lib().msq_dropout_mask_words(self.B, cfg.n_heads, self.S)
             self._masks = torch.zeros(cfg.n_layer if self.save else 1, 2, n, device=device, dtype=torch.int32)
         return self._masks
 

@@ -141,12 +141,15 @@ int msq_relattn_fwd(int dtype, void* out, int64_t ld_out, float* lse, const void
                     int64_t n_meta, void* stream);
 /* ---- attention-probability dropout (nn.Dropout(p) on the softmax output,
  * model_transformer.py:62,80; active in train() mode, config.yaml:16 p = 0.01).
- * Keep bits of one layer, both layouts [B, H, S, msq_dropout_mask_ld(S)] uint32:
- * rowmask[b,h,i][w] bit t = keep(i, 32w+t), colmask[b,h,j][w] bit t =
- * keep(32w+t, j); keep(i,j) = hash(seed, site0 + b*H + h, i, j) >= p*2^32
- * (counter-based, csrc/common.h). Only the causal lower block triangle is
- * written.                                                                  */
+ * Keep bits of one layer in two block-transposed layouts of
+ * msq_dropout_mask_words(B, H, S) uint32 each (nb = ceil(S/64), bh = b*H + h):
+ *   rowmask as uint64 [((bh*nb + i/64)*nb + j/64)*64 + i%64] bit j%64 = keep(i, j)
+ *   colmask as uint64 [((bh*nb + j/64)*nb + i/64)*64 + j%64] bit i%64 = keep(i, j)
+ * keep(i,j) = hash(seed, site0 + b*H + h, i, j) >= p*2^32 (counter-based,
+ * csrc/common.h). Only the causal lower block triangle is written.
+ * msq_dropout_mask_ld(S) = 2*nb, the uint32 words of one block row.          */
 int64_t msq_dropout_mask_ld(int64_t S);
+int64_t msq_dropout_mask_words(int64_t B, int64_t H, int64_t S);
 int msq_dropout_attn_mask(uint32_t* rowmask, uint32_t* colmask, int64_t B, int64_t H, int64_t S, uint32_t seed,
                           uint32_t site0, float p, void* stream);
 /* msq_relattn_fwd / _bwd with dropout p on the attention probabilities: the

@@ -37,11 +37,16 @@ def test_attn_mask_bits_match_oracle(S, p):
     B, H, seed, layer = 2, 3, 987654321, 5
     if S > 1000:
         B, H = 1, 2
-    ld = L.lib().msq_dropout_mask_ld(S)
+    nb = (S + 63) // 64
     m = ops.dropout_attn_mask(B, H, S, seed, DROP_ATTN + layer * 65536, p, dev)
     torch.cuda.synchronize()
-    rows = unpack(m[0].view(B, H, S, ld), S)          # [B,H,i,j]
-    cols = unpack(m[1].view(B, H, S, ld), S)          # [B,H,j,i]
+    assert m.shape[1] == L.lib().msq_dropout_mask_words(B, H, S) == B * H * nb * nb * 128
+
+    def dense(words):   # block-transposed [B,H,nb(r),nb(c),64(r%64),2] -> [B,H,r,c words]
+        w = words.view(B, H, nb, nb, 64, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, H, nb * 64, nb * 2)
+        return unpack(w[:, :, :S], S)
+    rows = dense(m[0])          # [B,H,i,j]
+    cols = dense(m[1])          # [B,H,j,i]
     ref = odrop.attn_keep(seed, layer, B, H, S, p)
     tri = np.tril(np.ones((S, S), dtype=bool))
     assert np.array_equal(rows[..., tri], ref[..., tri])
