@@ -147,6 +147,30 @@ def decode_leg(dev, rank, world, steps=3, B=64, T=2048):
                        "context": T}}
 
 
+def mamba_decode_leg(dev, rank, world, B=64, T0=1024, K=64, steps=2):
+    """Mamba (d=1024, 10 layers, bf16) cached decode of
+    B=64 prompts of T0 tokens per GPU (replicas): one prefill forward, then
+    one recurrent step per new token. Steady-state rate = K new tokens per
+    row over (time of prefill + K steps) - (time of prefill alone)."""
+    import random
+    from midiseq.generate import generate
+    from midiseq.mamba import Mamba
+    m = Mamba(precision="bf16").to(dev)
+    src, _, meta = SyntheticMIDI(B, T0, dev, rank, n_batches=1).batches[0]
+    run = lambda n: generate(m, 2048, src, meta, num_tokens=n, rng=random.Random(rank), device=dev,  # noqa: E731
+                             mode="cached")
+    el_pre = timed(lambda: run(1), steps, 1, world, dev)
+    el_all = timed(lambda: run(1 + K), steps, 1, world, dev)
+    el_exact = timed(lambda: generate(m, 2048, src, meta, num_tokens=1, rng=random.Random(rank), device=dev),
+                     steps, 1, world, dev)
+    del m
+    ms_step = (el_all - el_pre) / (steps * K) * 1e3
+    return {"value": round(world * B / (ms_step * 1e-3), 1), "unit": "new tokens/s", "ms_per_token_step": round(ms_step, 3),
+            "prefill_ms": round(el_pre / steps * 1e3, 2), "exact_full_forward_ms_per_step": round(el_exact / steps * 1e3, 2),
+            "config": {"workload": "Mamba cached decode (recurrent step, exact while prompt+new <= context)",
+                       "batch_per_gpu": B, "prompt": T0, "new_tokens": K, "context": 2048}}
+
+
 def mamba_leg(dev, rank, world, steps=3, B=8, T=4096):
     """Config 3: models/mamba (d=1024, 10 Mamba2 layers) train step at
     T=4096, B=8 per GPU, bf16."""
@@ -226,6 +250,8 @@ def main():
         extra["decode"] = decode_leg(dev, rank, world)
         torch.cuda.empty_cache()
         extra["mamba_train"] = mamba_leg(dev, rank, world)
+        torch.cuda.empty_cache()
+        extra["mamba_decode"] = mamba_decode_leg(dev, rank, world)
     M = args.batch * (args.seq + 6)
     ffn_flops = 2.0 * M * (4 * cfg.n_embd) * cfg.n_embd
     achieved = ffn_flops / (ffn_ms * 1e-3) / 1e12 if ffn_ms > 0 else 0.0

@@ -65,7 +65,12 @@ SIGNATURES = {
     "msq_mamba_ssd_bwd_workspace": (_sz, [_i64, _i64, _i64]),
     "msq_mamba_ssd_bwd": (_i, [_p, _i64, _p, _p, _i64, _p, _p, _i64, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _i64,
                                _i64, _i64, _i64, _p, _p]),
-    "msq_mamba_conv_bwd": (_i, [_p, _p, _i64, _p, _i64, _i, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "msq_mamba_ssd_fwd_state": (_i, [_p, _i64, _p, _p, _p, _i64, _p, _i64, _i, _p, _p, _p, _i64, _i64, _i64, _i64,
+                                     _p]),
+    "msq_mamba_conv_step": (_i, [_p, _i64, _p, _p, _i64, _i, _p, _p, _i64, _i64, _i64, _p]),
+    "msq_mamba_ssd_step": (_i, [_p, _i64, _p, _p, _i64, _p, _i64, _i, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "msq_filtered_logit_step": (_i, [_p, _i64, _p, _p, _i, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p]),
+    "msq_mamba_conv_bwd":(_i, [_p, _p, _i64, _p, _i64, _i, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "msq_relattn_bwd_workspace": (_sz, [_i, _i64, _i64, _i64]),
     "msq_relattn_bwd": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64,
                              _p, _p]),

@@ -199,7 +199,8 @@ template <typename T>
 __global__ __launch_bounds__(NT) void ssd_fwd_kernel(MambaArgs a, const T* __restrict__ xc,
                                                      const T* __restrict__ zx, const float* __restrict__ dt_bias,
                                                      const float* __restrict__ A_log, const float* __restrict__ Dp,
-                                                     float* __restrict__ y, int64_t ldy, float* __restrict__ states) {
+                                                     float* __restrict__ y, int64_t ldy, float* __restrict__ states,
+                                                     float* __restrict__ fin) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* sX = sm;              // dt*x  [t][p]
     float* sB = sX + 64 * LD;    // B     [t][n]
@@ -302,6 +303,11 @@ __global__ __launch_bounds__(NT) void ssd_fwd_kernel(MambaArgs a, const T* __res
         }
         __syncthreads();
         store44(sH, acc, tid);
+    }
+    if (fin) {  // state after the last position (cached decode)
+        __syncthreads();
+        float* f = fin + (b * a.nheads + h) * (int64_t)(P * N);
+        for (int e = tid; e < P * N; e += NT) f[e] = sH[(e >> 6) * LD + (e & 63)];
     }
 }
 
@@ -873,7 +879,7 @@ __global__ __launch_bounds__(256) void state_kernel(MambaArgs a, const bf16* __r
 
 // pass: in place over the per-chunk S, H_0 = 0, H_{c+1} = e^{cum_last_c} H_c + S_c
 __global__ __launch_bounds__(256) void pass_kernel(float* __restrict__ states, const float* __restrict__ clast,
-                                                   int64_t nbh, int nch) {
+                                                   int64_t nbh, int nch, float* __restrict__ fin) {
     const int64_t e = blockIdx.x * 256LL + threadIdx.x;  // (bh, p, n)
     if (e >= nbh * P * N) return;
     const int64_t bh = e / (P * N), pn = e % (P * N);
@@ -885,6 +891,7 @@ __global__ __launch_bounds__(256) void pass_kernel(float* __restrict__ states, c
         st[(int64_t)c * P * N] = hcur;
         hcur = expf(cl[c]) * hcur + sc;
     }
+    if (fin) fin[e] = hcur;  // state after the last position (cached decode)
 }
 
 // out: y = (C B^T o L) (dt x) + e^{cum_t} C H_c^T + D x
@@ -1316,10 +1323,10 @@ extern "C" int msq_mamba_conv_fwd(void* xc, int64_t ldxc, const void* zxbcdt, in
     return MSQ_OK;
 }
 
-extern "C" int msq_mamba_ssd_fwd(float* y, int64_t ldy, float* states, const void* xc, int64_t ldxc,
-                                 const void* zxbcdt, int64_t ldz, int dtype, const float* dt_bias,
-                                 const float* A_log, const float* D, int64_t B, int64_t L, int64_t d_inner,
-                                 int64_t nheads, void* stream) {
+extern "C" int msq_mamba_ssd_fwd_state(float* y, int64_t ldy, float* states, float* final_state, const void* xc,
+                                       int64_t ldxc, const void* zxbcdt, int64_t ldz, int dtype,
+                                       const float* dt_bias, const float* A_log, const float* D, int64_t B,
+                                       int64_t L, int64_t d_inner, int64_t nheads, void* stream) {
     MAMBA_CHECK();
     const MambaArgs a = mk(B, L, d_inner, nheads, ldz, ldxc);
     hipStream_t s = (hipStream_t)stream;
@@ -1332,7 +1339,7 @@ extern "C" int msq_mamba_ssd_fwd(float* y, int64_t ldy, float* states, const voi
         hipLaunchKernelGGL(ssd2::state_kernel, gch, dim3(256), ssd2::STATE_LDS, s, a, (const bf16*)xc,
                            (const bf16*)zxbcdt, dt_bias, A_log, states, clast, nch);
         hipLaunchKernelGGL(ssd2::pass_kernel, dim3((unsigned)((B * nheads * P * N + 255) / 256)), dim3(256), 0, s,
-                           states, clast, B * nheads, nch);
+                           states, clast, B * nheads, nch, final_state);
         hipLaunchKernelGGL(ssd2::out_kernel, gch, dim3(256), ssd2::OUT_LDS, s, a, (const bf16*)xc,
                            (const bf16*)zxbcdt, dt_bias, A_log, D, y, ldy, states, nch);
         MSQ_LAUNCH_CHECK();
@@ -1341,10 +1348,18 @@ extern "C" int msq_mamba_ssd_fwd(float* y, int64_t ldy, float* states, const voi
     const dim3 grid((unsigned)(B * nheads));
     allow_lds(ssd_fwd_kernel<bf16>, FWD_LDS);
     allow_lds(ssd_fwd_kernel<float>, FWD_LDS);
-    if (dtype == MSQ_BF16) hipLaunchKernelGGL(ssd_fwd_kernel<bf16>, grid, dim3(NT), FWD_LDS, s, a, (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, D, y, ldy, states);
-    else hipLaunchKernelGGL(ssd_fwd_kernel<float>, grid, dim3(NT), FWD_LDS, s, a, (const float*)xc, (const float*)zxbcdt, dt_bias, A_log, D, y, ldy, states);
+    if (dtype == MSQ_BF16) hipLaunchKernelGGL(ssd_fwd_kernel<bf16>, grid, dim3(NT), FWD_LDS, s, a, (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, D, y, ldy, states, final_state);
+    else hipLaunchKernelGGL(ssd_fwd_kernel<float>, grid, dim3(NT), FWD_LDS, s, a, (const float*)xc, (const float*)zxbcdt, dt_bias, A_log, D, y, ldy, states, final_state);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
+}
+
+extern "C" int msq_mamba_ssd_fwd(float* y, int64_t ldy, float* states, const void* xc, int64_t ldxc,
+                                 const void* zxbcdt, int64_t ldz, int dtype, const float* dt_bias,
+                                 const float* A_log, const float* D, int64_t B, int64_t L, int64_t d_inner,
+                                 int64_t nheads, void* stream) {
+    return msq_mamba_ssd_fwd_state(y, ldy, states, nullptr, xc, ldxc, zxbcdt, ldz, dtype, dt_bias, A_log, D, B, L,
+                                   d_inner, nheads, stream);
 }
 
 extern "C" int msq_mamba_gnorm_fwd(void* out, int64_t ldo, float* rstd, const float* y, int64_t ldy,

@@ -10,6 +10,16 @@ exactly like the reference (same call order, so seeded runs draw the same
 k's) and samples on the device by inverse CDF on a uniform per row (replacing
 torch.multinomial). The history stays on the device; the only per-step
 device->host traffic is the B last tokens needed for the host-side k choice.
+
+Cached mode (``mode="cached"``, Mamba only): while the
+window still holds the whole history (prompt + generated <= context_len) every
+Mamba2 mixer is causal and the final LayerNorm / head are per position, so the
+logits of the new last row equal one recurrent step from the mixer states
+after the previous row, and the time-axis log-softmax of filtered_logit only
+needs a running per-vocabulary LSE. The prompt is prefilled by one full
+forward (which also leaves the states); each later step is one
+``MambaEngine.step``. Once the window starts to slide the loop falls back to
+the exact full forward per step.
 """
 import random as _random
 
@@ -39,7 +49,7 @@ def choose_k(last_tokens, start, rng):
 
 @torch.no_grad()
 def generate(model, context_len, token_ids, meta_ids, num_tokens=1000, device="cuda", rng=None, uniforms=None,
-             grammar: Grammar = None, return_tensor=False):
+             grammar: Grammar = None, return_tensor=False, mode="exact"):
     """Returns a list of B token lists of length T0 + num_tokens (like the
     reference). ``rng`` defaults to the global ``random`` module (as in the
     reference); ``uniforms`` is an optional iterator of floats (one per row
@@ -63,18 +73,35 @@ def generate(model, context_len, token_ids, meta_ids, num_tokens=1000, device="c
     b = grammar.bounds
     last_host = token_ids[:, -1].tolist()
     gen = None
+    if mode not in ("exact", "cached"):
+        raise ValueError(f"mode must be 'exact' or 'cached', not {mode!r}")
+    cached = mode == "cached"
+    if cached and not hasattr(eng, "step"):
+        raise ValueError("cached decode needs a recurrent model (Mamba); the Transformer is length-anchored")
+    cache = None
+    ldz = (V + 3) // 4 * 4
+    z = torch.empty(B, 1, ldz, device=dev, dtype=torch.float32)
     for step in range(num_tokens):
         cur = T0 + step
         W = min(cur, context_len)
-        window = hist[:, cur - W:cur].contiguous()
-        logits = eng.forward(window, meta_ids, save=False)
-        A = eng.acts(B, W, save=False)
-        ldz = (V + 3) // 4 * 4
-        z = torch.empty(B, 1, ldz, device=dev, dtype=torch.float32)
-        col_lse = torch.empty(B, V, device=dev, dtype=torch.float32)
-        ws = workspace(L.lib().msq_filtered_workspace(B, W, V), dev, "loss")
-        call("msq_filtered_logit", ptr(z), ldz, ptr(A.logits), dt(A.logits), cfg.v_pad, ptr(window), ptr(wtab),
-             b[0], b[1], b[2], b[3], B, W, V, W - 1, ptr(col_lse), ptr(ws), stream())
+        if cached and cache is not None and cur <= context_len:
+            # one recurrent position: the token sampled last step (out_tok) at row cur-1
+            logits = eng.step(out_tok, cache)
+            call("msq_filtered_logit_step", ptr(z), ldz, ptr(cache.lse), ptr(logits), dt(logits), cfg.v_pad,
+                 ptr(out_tok), ptr(wtab), b[0], b[1], b[2], b[3], B, V, stream())
+        else:
+            window = hist[:, cur - W:cur].contiguous()
+            if cached and cur <= context_len:  # prefill: the whole prompt, states left in the cache
+                cache = eng.decode_cache(B)
+                logits = eng.forward(window, meta_ids, save=False, cache=cache)
+                col_lse = cache.lse
+            else:
+                logits = eng.forward(window, meta_ids, save=False)
+                col_lse = torch.empty(B, V, device=dev, dtype=torch.float32)
+            A = eng.acts(B, W, save=False)
+            ws = workspace(L.lib().msq_filtered_workspace(B, W, V), dev, "loss")
+            call("msq_filtered_logit", ptr(z), ldz, ptr(A.logits), dt(A.logits), cfg.v_pad, ptr(window), ptr(wtab),
+                 b[0], b[1], b[2], b[3], B, W, V, W - 1, ptr(col_lse), ptr(ws), stream())
         ks = choose_k(last_host, start, rng)
         if uniforms is not None:
             u = torch.tensor([next(uniforms) for _ in range(B)], dtype=torch.float32).to(dev)

@@ -138,6 +138,32 @@ class _MActs:
         return self._bwd
 
 
+class DecodeCache:
+    """Recurrent state of the cached decode for B rows:
+    per layer the conv window (fp32 [B, 3, conv_dim], last three pre-conv xBC
+    rows) and the SSM state (fp32 [B, H, 64, 64]); the running time-axis LSE
+    of the logits (fp32 [B, V]); step buffers for one position."""
+
+    def __init__(self, cfg, B, device, act):
+        f32 = torch.float32
+        e = lambda *s, dt=act: torch.empty(*s, device=device, dtype=dt)  # noqa: E731
+        self.B = B
+        self.conv = torch.zeros(cfg.n_layers, B, D_CONV - 1, cfg.conv_dim, device=device, dtype=f32)
+        self.ssm = torch.zeros(cfg.n_layers, B, cfg.nheads, HEADDIM, D_STATE, device=device, dtype=f32)
+        self.lse = e(B, cfg.vocab_size, dt=f32)
+        self.x = e(B, cfg.d_model, dt=f32)
+        self.xa = e(B, cfg.d_model)
+        self.zx = e(B, cfg.d_in_proj)
+        self.xc = e(B, cfg.conv_dim)
+        self.y = e(B, cfg.d_inner, dt=f32)
+        self.yn = e(B, cfg.d_inner)
+        self.rstd = e(B, dt=f32)
+        self.f = e(B, cfg.d_model)
+        self.stf = e(2, B, dt=f32)
+        self.logits = e(B, cfg.v_pad)
+        self.length = 0  # positions absorbed (metadata excluded)
+
+
 class MambaEngine:
     def __init__(self, cfg: MambaConfig, flat):
         self.cfg = cfg
@@ -179,7 +205,12 @@ class MambaEngine:
         c = self.cfg
         return A.B, A.L, c.d_inner, c.nheads
 
-    def forward(self, idx, meta, save=True, train=False):
+    def decode_cache(self, B):
+        return DecodeCache(self.cfg, B, self.device, self.act)
+
+    def forward(self, idx, meta, save=True, train=False, cache=None):
+        """cache (a DecodeCache, save=False): also leave every mixer's state
+        after the last position in it (the cached decode's prefill)."""
         # models/mamba/mamba.py has no dropout: train mode changes nothing
         cfg, P, W = self.cfg, self.P, self.W
         if not idx.is_cuda:
@@ -205,8 +236,11 @@ class MambaEngine:
             ops.gemm(xa, W[f"{l}.in_w"], out=zx)
             call("msq_mamba_conv_fwd", ptr(xc), cfg.conv_dim, ptr(zx), cfg.d_in_proj, dtc, ptr(P[f"{l}.conv_w"]),
                  ptr(P[f"{l}.conv_b"]), Bb, Ll, di, H, s)
-            call("msq_mamba_ssd_fwd", ptr(y), di, ptr(A.states[k]), ptr(xc), cfg.conv_dim, ptr(zx), cfg.d_in_proj, dtc,
-                 ptr(P[f"{l}.dt_bias"]), ptr(P[f"{l}.A_log"]), ptr(P[f"{l}.D"]), Bb, Ll, di, H, s)
+            call("msq_mamba_ssd_fwd_state", ptr(y), di, ptr(A.states[k]), ptr(cache.ssm[l]) if cache else None,
+                 ptr(xc), cfg.conv_dim, ptr(zx), cfg.d_in_proj, dtc, ptr(P[f"{l}.dt_bias"]), ptr(P[f"{l}.A_log"]),
+                 ptr(P[f"{l}.D"]), Bb, Ll, di, H, s)
+            if cache is not None:  # conv window: the last three pre-conv xBC rows
+                cache.conv[l].copy_(zx.view(B, Ll, cfg.d_in_proj)[:, Ll - (D_CONV - 1):, di:di + cfg.conv_dim])
             call("msq_mamba_gnorm_fwd", ptr(yn), di, ptr(A.rstd[k]), ptr(y), di, ptr(zx), cfg.d_in_proj, dtc,
                  ptr(P[f"{l}.norm_w"]), M, di, float(cfg.norm_eps), s)
             xo = A.xlast if l == cfg.n_layers - 1 else A.x[(l + 1) % 2]
@@ -218,7 +252,38 @@ class MambaEngine:
         V = cfg.vocab_size
         # full V_pad rows (pad rows of lm_w / lm_b are zero): 16-B aligned rows, 256-tile eligible
         ops.gemm(A.f, W["lm_w"], out=A.logits, epilogue=L.EPI_BIAS, bias=P["lm_b"])
+        if cache is not None:
+            cache.length = T
         return A.logits.view(B, T, cfg.v_pad)[:, :, :V]
+
+    @torch.no_grad()
+    def step(self, tok, cache):
+        """One recurrent position for every row: tok int64 [B] (contiguous) ->
+        logits [B, v_pad] (cache.logits) of that position; the cache advances.
+        Equal to the last row of forward() over the grown sequence."""
+        cfg, P, W = self.cfg, self.P, self.W
+        if not tok.is_cuda:
+            raise RuntimeError("the MI355X engine runs on the GPU only (no CPU fallback)")
+        self.refresh_shadow()
+        B, d, di, H = cache.B, cfg.d_model, cfg.d_inner, cfg.nheads
+        dtc = L.BF16 if self.act == torch.bfloat16 else L.F32
+        s = stream()
+        call("msq_embed_fwd", ptr(cache.x), ptr(P["tok_emb"]), ptr(P["meta_emb"]), ptr(tok), None, B, 1, 0, d, s)
+        ops.cast(cache.xa, cache.x)
+        for l in range(cfg.n_layers):
+            ops.gemm(cache.xa, W[f"{l}.in_w"], out=cache.zx)
+            call("msq_mamba_conv_step", ptr(cache.xc), cfg.conv_dim, ptr(cache.conv[l]), ptr(cache.zx), cfg.d_in_proj,
+                 dtc, ptr(P[f"{l}.conv_w"]), ptr(P[f"{l}.conv_b"]), B, di, H, s)
+            call("msq_mamba_ssd_step", ptr(cache.y), di, ptr(cache.ssm[l]), ptr(cache.xc), cfg.conv_dim, ptr(cache.zx),
+                 cfg.d_in_proj, dtc, ptr(P[f"{l}.dt_bias"]), ptr(P[f"{l}.A_log"]), ptr(P[f"{l}.D"]), B, di, H, s)
+            call("msq_mamba_gnorm_fwd", ptr(cache.yn), di, ptr(cache.rstd), ptr(cache.y), di, ptr(cache.zx),
+                 cfg.d_in_proj, dtc, ptr(P[f"{l}.norm_w"]), B, di, float(cfg.norm_eps), s)
+            ops.gemm(cache.yn, W[f"{l}.out_w"], out=cache.x)
+            ops.cast(cache.xa, cache.x)
+        ops.layernorm_fwd(cache.x, P["lnf_w"], P["lnf_b"], out=cache.f, mean=cache.stf[0], rstd=cache.stf[1])
+        ops.gemm(cache.f, W["lm_w"], out=cache.logits, epilogue=L.EPI_BIAS, bias=P["lm_b"])
+        cache.length += 1
+        return cache.logits
 
     def backward(self, dlogits, grads):
         cfg, P, W = self.cfg, self.P, self.W

@@ -240,6 +240,34 @@ int msq_mamba_conv_bwd(void* dzxbcdt, const float* dxc, int64_t ld_dxc, const vo
                        const float* conv_w, const float* conv_b, float* g_conv_w, float* g_conv_b, int64_t B,
                        int64_t L, int64_t d_inner, int64_t nheads, void* stream);
 
+/* ---- Mamba cached decode (scripts/generate.py:14-95
+ * with a Mamba model while prompt + new tokens <= context_len, where every
+ * mixer is causal and the per-step full forward equals one recurrent step).
+ * msq_mamba_ssd_fwd_state = msq_mamba_ssd_fwd + the state after the last
+ * position, final_state fp32 [B][H][64][64] (NULL = none): the prefill.      */
+int msq_mamba_ssd_fwd_state(float* y, int64_t ldy, float* states, float* final_state, const void* xc,
+                            int64_t ldxc, const void* zxbcdt, int64_t ldz, int dtype, const float* dt_bias,
+                            const float* A_log, const float* D, int64_t B, int64_t L, int64_t d_inner,
+                            int64_t nheads, void* stream);
+/* one position: xc[b] = silu(conv(conv_state[b] (fp32 [B][3][conv_dim], the
+ * last three pre-conv xBC rows, oldest first) ++ zxbcdt[b, xBC])); the state
+ * shifts in the new row.                                                     */
+int msq_mamba_conv_step(void* xc, int64_t ldxc, float* conv_state, const void* zxbcdt, int64_t ldz, int dtype,
+                        const float* conv_w, const float* conv_b, int64_t B, int64_t d_inner, int64_t nheads,
+                        void* stream);
+/* one position: h = exp(dt A) h + dt x B^T (ssm_state fp32 [B][H][64][64],
+ * in place); y[b] (fp32) = h C + D x.                                        */
+int msq_mamba_ssd_step(float* y, int64_t ldy, float* ssm_state, const void* xc, int64_t ldxc, const void* zxbcdt,
+                       int64_t ldz, int dtype, const float* dt_bias, const float* A_log, const float* D, int64_t B,
+                       int64_t d_inner, int64_t nheads, void* stream);
+/* filtered logit of one new position (train.py:133-138): col_lse fp32 [B][V]
+ * (the time-axis LSE over the positions so far, e.g. msq_filtered_logit's
+ * col_lse of the prefill) absorbs logits[b]; z[b] = -(o - lse) * W[class(tok[b])],
+ * tok[b] = the token at that position.                                       */
+int msq_filtered_logit_step(float* z, int64_t ldz, float* col_lse, const void* logits, int dtype, int64_t ld,
+                            const int64_t* tok, const float* wtab, int64_t b0, int64_t b1, int64_t b2, int64_t b3,
+                            int64_t B, int64_t V, void* stream);
+
 /* ---- data feed (processing/dataset.py:171-195 SequenceDataset.__getitem__)
  * B training windows of T+1 tokens cut from the device-resident token store
  * (tokens int32, song s = tokens[song_off[s] .. + song_len[s]]): params[b] =
