@@ -171,6 +171,48 @@ def mamba_decode_leg(dev, rank, world, B=64, T0=1024, K=64, steps=2):
                        "batch_per_gpu": B, "prompt": T0, "new_tokens": K, "context": 2048}}
 
 
+def midi_decode_leg(dev, rank, world, B=64, L=4048, iters=50, cpu_rows=4):
+    """token -> note decode (processing.decode +
+    revert_note_time) of the B=64 generated rows of cfg 5 (2048 prompt + 2000
+    new tokens, generate_midi_combined --retain) while they are in HBM: one
+    msq_midi_decode launch per batch, timed with HIP events on its stream.
+    Algorithmic bytes: 8 B read per token + 48 B written per note.
+    cpu_baseline: the oracle's per-row Python decode (the reference's loop) on
+    cpu_rows rows, scaled to tokens/s."""
+    from midiseq import midi
+    rows = SyntheticMIDI(B, L, dev, rank, n_batches=1).batches[0][0].contiguous()
+    nb = midi.decode_batch(rows)
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        midi.decode_batch(rows, out=nb)
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    notes = int(nb.count.sum())
+    nbytes = B * L * 8 + notes * 48
+    out = {"value": round(world * B * L / (ms * 1e-3), 1), "unit": "tokens/s", "ms_per_batch": round(ms, 4),
+           "notes_per_batch": notes, "achieved_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1), "peak_GBps": 8000.0,
+           "config": {"workload": "token->note decode of cfg 5 generated rows (msq_midi_decode)", "batch_per_gpu": B,
+                      "row_tokens": L}}
+    if rank == 0:
+        from oracle import midi as omidi
+        from midiseq.config import DEFAULT_DISC
+        rows_np = rows[:cpu_rows].cpu().numpy()
+        t0 = time.perf_counter()
+        for r in range(cpu_rows):
+            try:
+                omidi.decode(rows_np[r], DEFAULT_DISC.start_idx)
+            except ZeroDivisionError:  # a synthetic tempo-0 token; the walk itself ran
+                pass
+        el = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(cpu_rows * L / el, 1), "unit": "tokens/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle/midi.py decode of {cpu_rows} rows x {L} tokens"}
+    return out
+
+
 def mamba_leg(dev, rank, world, steps=3, B=8, T=4096):
     """Config 3: models/mamba (d=1024, 10 Mamba2 layers) train step at
     T=4096, B=8 per GPU, bf16."""
@@ -252,6 +294,7 @@ def main():
         extra["mamba_train"] = mamba_leg(dev, rank, world)
         torch.cuda.empty_cache()
         extra["mamba_decode"] = mamba_decode_leg(dev, rank, world)
+        extra["midi_decode"] = midi_decode_leg(dev, rank, world)
     M = args.batch * (args.seq + 6)
     ffn_flops = 2.0 * M * (4 * cfg.n_embd) * cfg.n_embd
     achieved = ffn_flops / (ffn_ms * 1e-3) / 1e12 if ffn_ms > 0 else 0.0

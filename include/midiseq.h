@@ -280,6 +280,19 @@ int msq_window_gather(int64_t* src, int64_t* trg, int64_t* meta_out, const int32
                       const int64_t* song_off, const int64_t* song_len, const int64_t* song_meta, int n_meta,
                       const int64_t* params, int64_t B, int64_t T, int augment, const int64_t* disc, void* stream);
 
+/* Token -> note decode of B generated rows (replaces processing/processing.py
+ * :171-214 decode + :154-169 revert_note_time, called per row by
+ * scripts/generate_midi_combined.py:143-156). rows int64 [B, ld], first L <=
+ * 16256 tokens used; disc = {pitch, channel, dyn, length, time, tempo}
+ * (config.yaml discretization); res_per_beat = resolution.bar_res. Row b's
+ * notes go to [b*cap, b*cap + min(count[b], cap)) of pitch / channel / dyn /
+ * tempo (int32), beat_start / beat_end (int64 beats) and t_start / t_end
+ * (fp64 seconds, bit-identical to the reference's Python floats); count[b] is
+ * the row's full note count. cap >= L/4 + 1 never truncates.                 */
+int msq_midi_decode(const int64_t* rows, int64_t B, int64_t L, int64_t ld, const int64_t* disc, int64_t res_per_beat,
+                    int64_t cap, int32_t* pitch, int32_t* channel, int32_t* dyn, int32_t* tempo, int64_t* beat_start,
+                    int64_t* beat_end, double* t_start, double* t_end, int64_t* count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
