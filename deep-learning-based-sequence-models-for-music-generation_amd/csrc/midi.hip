@@ -101,15 +101,35 @@ __global__ __launch_bounds__(64) void midi_decode_kernel(const int64_t* __restri
     // lane-chunk order with an odd chunk stride, so the per-lane walks below
     // read conflict-free LDS instead of 64 scattered HBM lines per step
     extern __shared__ int32_t tok_lds[];
-    for (int ch = 0; ch < 64; ++ch)
-        for (int off = lane; off < cs; off += 64)
-            if (ch * cs + off < n_tok) tok_lds[ch * csp + off] = (int32_t)row[ch * cs + off];
+    // 16 coalesced loads in flight per lane (one dependent HBM round trip per
+    // 1024 tokens instead of per 64); chunk of token i = i / cs via a float
+    // reciprocal with an exact integer fix-up
+    const float inv_cs = cs > 0 ? 1.0f / (float)cs : 0.0f;
+    for (int i0 = 0; i0 < n_tok; i0 += 64 * 16) {
+        int32_t v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int i = i0 + u * 64 + lane;
+            v[u] = i < n_tok ? (int32_t)row[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int i = i0 + u * 64 + lane;
+            if (i < n_tok) {
+                int ch = (int)((float)i * inv_cs);
+                ch -= ch * cs > i;
+                ch += (ch + 1) * cs <= i;
+                tok_lds[ch * csp + (i - ch * cs)] = v[u];
+            }
+        }
+    }
     __syncthreads();
     const int32_t* my = tok_lds + lane * csp;  // my[j] = token lo + j
 
     // pass 1: transition map of this chunk + last position of every class
     uint64_t m = IDENT;
     int l0 = -1, l1 = -1, l2 = -1, l3 = -1, l4 = -1;
+#pragma unroll 4
     for (int j = 0; j < hi - lo; ++j) {
         const int c = tok_class(my[j], d);
         l0 = c == 0 ? j : l0; l1 = c == 1 ? j : l1; l2 = c == 2 ? j : l2;
@@ -140,7 +160,8 @@ __global__ __launch_bounds__(64) void midi_decode_kernel(const int64_t* __restri
     {
         int st = state;
         int64_t tv = c3;
-        for (int j = 0; j < hi - lo; ++j) {
+    #pragma unroll 4
+    for (int j = 0; j < hi - lo; ++j) {
             const int64_t t = my[j];
             const int c = tok_class(t, d);
             tv = c == 3 ? t : tv;
@@ -163,7 +184,8 @@ __global__ __launch_bounds__(64) void midi_decode_kernel(const int64_t* __restri
         int st = state;
         int64_t v0 = c0, v1 = c1, v2 = c2, v3 = c3, v4 = c4;
         int64_t k = n_off, beat = beat_off;
-        for (int j = 0; j < hi - lo; ++j) {
+    #pragma unroll 4
+    for (int j = 0; j < hi - lo; ++j) {
             const int64_t t = my[j];
             const int c = tok_class(t, d);
             v0 = c == 0 ? t : v0; v1 = c == 1 ? t : v1; v2 = c == 2 ? t : v2;
@@ -191,19 +213,30 @@ __global__ __launch_bounds__(64) void midi_decode_kernel(const int64_t* __restri
     //   res = 60 / prev_tempo / res_per_beat
     //   ts  = prev_time + (beat - prev_beat) * res ; te = ts + (beat_end - beat) * res
     const int64_t n = min(n_tot, cap);
+    // raw note fields of one 64-note batch; the next batch's loads are issued
+    // before the current batch's add chain so their latency hides behind it
+    int32_t tp_c = 1, tp_n = 1;
+    int64_t pb_c = 0, bs_c = 0, be_c = 0, pb_n = 0, bs_n = 0, be_n = 0;
+    auto load = [&](int64_t k, int32_t& tp, int64_t& pb, int64_t& bs, int64_t& be) {
+        if (k < n) {
+            tp = tempo[base + (k == 0 ? 0 : k - 1)];
+            pb = k == 0 ? 0 : beat_start[base + k - 1];
+            bs = beat_start[base + k];
+            be = beat_end[base + k];
+        }
+    };
+    load(lane, tp_c, pb_c, bs_c, be_c);
     double prev_time = 0.0;
     for (int64_t k0 = 0; k0 < n; k0 += 64) {
         const int64_t k = k0 + lane;
         double inc_k = 0.0, dur_k = 0.0;
         if (k < n) {
-            const int64_t kp = k == 0 ? 0 : k - 1;
-            const double prev_tempo = (double)tempo[base + kp];
-            const double res = 60.0 / prev_tempo / res_per_beat;
-            const double pb = k == 0 ? 0.0 : (double)beat_start[base + k - 1];
-            const double bs = (double)beat_start[base + k];
-            inc_k = (bs - pb) * res;
-            dur_k = ((double)beat_end[base + k] - bs) * res;
+            const double res = 60.0 / (double)tp_c / res_per_beat;
+            const double bs = (double)bs_c;
+            inc_k = (bs - (double)pb_c) * res;
+            dur_k = ((double)be_c - bs) * res;
         }
+        load(k + 64, tp_n, pb_n, bs_n, be_n);
         // the add chain reads each lane's increment with v_readlane (scalar
         // broadcast, a few cycles) instead of an LDS-crossbar shuffle per step
         const uint64_t inc_bits = __builtin_bit_cast(uint64_t, inc_k);
@@ -221,6 +254,7 @@ __global__ __launch_bounds__(64) void midi_decode_kernel(const int64_t* __restri
             t_end[base + k] = ts + dur_k;
         }
         prev_time = __shfl(ts, (int)min((int64_t)63, n - 1 - k0), 64);
+        tp_c = tp_n; pb_c = pb_n; bs_c = bs_n; be_c = be_n;
     }
 }
 
