@@ -9,12 +9,13 @@
 // running sum of the time shifts, in beats; revert_note_time then maps beats
 // to seconds with a running fp64 sum that uses the PREVIOUS note's tempo.
 //
-// One wavefront per row, integer/byte work (no MFMA):
+// Four wavefronts per row (one workgroup), integer/byte work (no MFMA):
 //  * the "fields seen since the last note" state is a 4-bit mask, so the
 //    reference's sequential walk is a 16-state automaton; each lane folds its
 //    chunk of tokens into a transition map for all 16 start states at once
 //    (16 nibbles of one uint64, updated with bit ops), and a wave scan of map
-//    composition gives every lane its exact start state;
+//    composition (waves, then the 4 wave totals through LDS) gives every
+//    thread its exact start state;
 //  * field values at an emission are the last token of each class up to that
 //    point (a max-scan of positions), time shifts and note counts are
 //    exclusive wave sums;
@@ -25,8 +26,9 @@
 
 namespace {
 
-// chunk stride csp = cs | 1 <= 255 keeps the staged row within 64 KB of LDS
-constexpr int64_t MIDI_MAX_L = 64 * 254;
+constexpr int MIDI_WAVES = 4, MIDI_NT = 64 * MIDI_WAVES;  // 4 wavefronts share one row
+// chunk stride csp = cs | 1 <= 63 keeps the staged row (+ the wave totals) within 64 KB of LDS
+constexpr int64_t MIDI_MAX_L = MIDI_NT * 62;
 
 struct Disc {
     int64_t P, dyn0, len0, time0, tempo0;
@@ -83,7 +85,7 @@ __device__ __forceinline__ int64_t wave_excl_max(int64_t v, int lane) {
 // beat_start / beat_end (int64, pre-revert note times) and t_start / t_end
 // (fp64 seconds, revert_note_time). count[b] is the full note count even when
 // it exceeds cap (only the first cap notes are written).
-__global__ __launch_bounds__(64) void midi_decode_kernel(const int64_t* __restrict__ rows, int64_t ld, int64_t L,
+__global__ __launch_bounds__(MIDI_NT) void midi_decode_kernel(const int64_t* __restrict__ rows, int64_t ld, int64_t L,
                                                          int64_t cap, Disc d, double res_per_beat,
                                                          int32_t* __restrict__ pitch, int32_t* __restrict__ channel,
                                                          int32_t* __restrict__ dyn, int32_t* __restrict__ tempo,
@@ -91,12 +93,12 @@ __global__ __launch_bounds__(64) void midi_decode_kernel(const int64_t* __restri
                                                          int64_t* __restrict__ beat_end, double* __restrict__ t_start,
                                                          double* __restrict__ t_end, int64_t* __restrict__ count) {
 #pragma clang fp contract(off)
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t b = blockIdx.x;
     const int64_t* row = rows + b * ld;
     // positions fit int32 (L <= MIDI_MAX_L); no integer division inside the walks
-    const int n_tok = (int)L, cs = (n_tok + 63) / 64, csp = cs | 1;
-    const int lo = min(lane * cs, n_tok), hi = min(lo + cs, n_tok);
+    const int n_tok = (int)L, cs = (n_tok + MIDI_NT - 1) / MIDI_NT, csp = cs | 1;
+    const int lo = min(tid * cs, n_tok), hi = min(lo + cs, n_tok);
     // the row is staged once into LDS (coalesced int64 reads, int32 tokens) in
     // lane-chunk order with an odd chunk stride, so the per-lane walks below
     // read conflict-free LDS instead of 64 scattered HBM lines per step
@@ -105,16 +107,16 @@ __global__ __launch_bounds__(64) void midi_decode_kernel(const int64_t* __restri
     // 1024 tokens instead of per 64); chunk of token i = i / cs via a float
     // reciprocal with an exact integer fix-up
     const float inv_cs = cs > 0 ? 1.0f / (float)cs : 0.0f;
-    for (int i0 = 0; i0 < n_tok; i0 += 64 * 16) {
+    for (int i0 = 0; i0 < n_tok; i0 += MIDI_NT * 16) {
         int32_t v[16];
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
-            const int i = i0 + u * 64 + lane;
+            const int i = i0 + u * MIDI_NT + tid;
             v[u] = i < n_tok ? (int32_t)row[i] : 0;
         }
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
-            const int i = i0 + u * 64 + lane;
+            const int i = i0 + u * MIDI_NT + tid;
             if (i < n_tok) {
                 int ch = (int)((float)i * inv_cs);
                 ch -= ch * cs > i;
@@ -124,7 +126,7 @@ __global__ __launch_bounds__(64) void midi_decode_kernel(const int64_t* __restri
         }
     }
     __syncthreads();
-    const int32_t* my = tok_lds + lane * csp;  // my[j] = token lo + j
+    const int32_t* my = tok_lds + tid * csp;  // my[j] = token lo + j
 
     // pass 1: transition map of this chunk + last position of every class
     uint64_t m = IDENT;
@@ -144,16 +146,34 @@ __global__ __launch_bounds__(64) void midi_decode_kernel(const int64_t* __restri
         if (lane >= o) inc = compose(inc, prev);
     }
     const uint64_t before = __shfl_up(inc, 1, 64);
-    const int state = lane == 0 ? 0 : nib(before, 0);
+    // workgroup level: wave totals through LDS, each wave folds the earlier ones
+    __shared__ uint64_t wg_map[MIDI_WAVES];
+    __shared__ int64_t wg_last[5][MIDI_WAVES], wg_n[MIDI_WAVES], wg_td[MIDI_WAVES];
+    const int64_t gl[5] = {l0 >= 0 ? (int64_t)(lo + l0) : -1, l1 >= 0 ? (int64_t)(lo + l1) : -1,
+                           l2 >= 0 ? (int64_t)(lo + l2) : -1, l3 >= 0 ? (int64_t)(lo + l3) : -1,
+                           l4 >= 0 ? (int64_t)(lo + l4) : -1};
+    int64_t ex[5];
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        ex[c] = wave_excl_max(gl[c], lane);
+        if (lane == 63) wg_last[c][w] = max(ex[c], gl[c]);
+    }
+    if (lane == 63) wg_map[w] = inc;
+    __syncthreads();
+    uint64_t pre = IDENT;
+    for (int v = 0; v < w; ++v) pre = compose(wg_map[v], pre);
+    const int s0 = nib(pre, 0);
+    const int state = lane == 0 ? s0 : nib(before, s0);
     // value of the last token of each class before this chunk (a max-scan of
     // global positions; -1 = none yet). Positions map back to LDS once here.
-    auto carry = [&](int l) -> int64_t {
-        const int64_t gp = wave_excl_max(l >= 0 ? (int64_t)(lo + l) : (int64_t)-1, lane);
+    auto carry = [&](int c) -> int64_t {
+        int64_t gp = ex[c];
+        for (int v = 0; v < w; ++v) gp = max(gp, wg_last[c][v]);
         if (gp < 0) return -1;
         const int ch = (int)gp / cs;
         return tok_lds[ch * csp + ((int)gp - ch * cs)];
     };
-    const int64_t c0 = carry(l0), c1 = carry(l1), c2 = carry(l2), c3 = carry(l3), c4 = carry(l4);
+    const int64_t c0 = carry(0), c1 = carry(1), c2 = carry(2), c3 = carry(3), c4 = carry(4);
 
     // pass 2: notes and time-shift sum of this chunk from the exact start state
     int64_t n_loc = 0, td_loc = 0;
@@ -173,10 +193,22 @@ __global__ __launch_bounds__(64) void midi_decode_kernel(const int64_t* __restri
             }
         }
     }
-    const int64_t n_off = wave_excl_sum(n_loc, lane);
-    const int64_t beat_off = wave_excl_sum(td_loc, lane);
-    const int64_t n_tot = __shfl(n_off + n_loc, 63, 64);
-    if (lane == 0) count[b] = n_tot;
+    int64_t n_off = wave_excl_sum(n_loc, lane);
+    int64_t beat_off = wave_excl_sum(td_loc, lane);
+    if (lane == 63) {
+        wg_n[w] = n_off + n_loc;
+        wg_td[w] = beat_off + td_loc;
+    }
+    __syncthreads();
+    int64_t n_tot = 0;
+    for (int v = 0; v < MIDI_WAVES; ++v) {
+        if (v < w) {
+            n_off += wg_n[v];
+            beat_off += wg_td[v];
+        }
+        n_tot += wg_n[v];
+    }
+    if (tid == 0) count[b] = n_tot;
 
     // pass 3: write the notes (integer fields and beat times)
     const int64_t base = b * cap;
@@ -206,8 +238,8 @@ __global__ __launch_bounds__(64) void midi_decode_kernel(const int64_t* __restri
             }
         }
     }
-    __threadfence_block();
-    __builtin_amdgcn_s_barrier();
+    __syncthreads();  // workgroup-scope fence: wave 0 reads every wave's notes
+    if (w != 0) return;
 
     // pass 4: revert_note_time (processing.py:154-169), reference operation order:
     //   res = 60 / prev_tempo / res_per_beat
@@ -278,8 +310,8 @@ extern "C" int msq_midi_decode(const int64_t* rows, int64_t B, int64_t L, int64_
     d.tempo0 = d.time0 + disc[4];
     MSQ_CHECK_ARG(disc[0] > 0 && disc[1] > 0 && disc[2] > 0 && disc[3] > 0 && disc[4] > 0 && disc[5] > 0,
                   "msq_midi_decode: bad discretization");
-    const size_t lds = (size_t)64 * (((L + 63) / 64) | 1) * sizeof(int32_t);
-    hipLaunchKernelGGL(midi_decode_kernel, dim3((unsigned)B), dim3(64), lds, (hipStream_t)stream, rows, ld, L, cap, d,
+    const size_t lds = (size_t)MIDI_NT * (((L + MIDI_NT - 1) / MIDI_NT) | 1) * sizeof(int32_t);
+    hipLaunchKernelGGL(midi_decode_kernel, dim3((unsigned)B), dim3(MIDI_NT), lds, (hipStream_t)stream, rows, ld, L, cap, d,
                        (double)res_per_beat, pitch, channel, dyn, tempo, beat_start, beat_end, t_start, t_end, count);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;

@@ -17,7 +17,7 @@ from ._lib import call, ptr, stream
 from .config import DEFAULT_DISC, Discretization
 
 BAR_RES = 64  # config.yaml resolution.bar_res
-MAX_ROW = 64 * 254  # msq_midi_decode row limit (staged in 64 KB of LDS)
+MAX_ROW = 256 * 62  # msq_midi_decode row limit (staged in 64 KB of LDS)
 
 
 class MIDI_note:

@@ -283,7 +283,7 @@ int msq_window_gather(int64_t* src, int64_t* trg, int64_t* meta_out, const int32
 /* Token -> note decode of B generated rows (replaces processing/processing.py
  * :171-214 decode + :154-169 revert_note_time, called per row by
  * scripts/generate_midi_combined.py:143-156). rows int64 [B, ld], first L <=
- * 16256 tokens used; disc = {pitch, channel, dyn, length, time, tempo}
+ * 15872 tokens used; disc = {pitch, channel, dyn, length, time, tempo}
  * (config.yaml discretization); res_per_beat = resolution.bar_res. Row b's
  * notes go to [b*cap, b*cap + min(count[b], cap)) of pitch / channel / dyn /
  * tempo (int32), beat_start / beat_end (int64 beats) and t_start / t_end

@@ -46,7 +46,7 @@ def test_decode_matches_reference_golden():
         assert [x.time_start for x in notes] == ref_t[:, 0].tolist()
 
 
-@pytest.mark.parametrize("B,L", [(64, 4048), (3, 1), (5, 63), (2, 65), (1, 16256)])
+@pytest.mark.parametrize("B,L", [(64, 4048), (3, 1), (5, 63), (2, 65), (3, 257), (2, 1000), (1, 15872)])
 def test_decode_batch_matches_oracle(B, L):
     rng = np.random.default_rng(B * 1000 + L)
     s, V = REAL.start, REAL.size
