@@ -7,11 +7,38 @@ Prints ONE JSON line on rank 0 (contract in the task statement)."""
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+
+def launch_ranks():
+    """`python bench.py --gpus N` (N > 1) without a torchrun environment:
+    start N worker ranks as ONE child process (torch.distributed.run, one
+    process per GPU, rendezvous on 127.0.0.1), relay their output and exit
+    with their status. Runs before this process imports torch, so the parent
+    never touches a GPU (and never execs)."""
+    if "RANK" in os.environ:
+        return
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    n = ap.parse_known_args()[0].gpus
+    if n <= 1:
+        return
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
+if __name__ == "__main__":
+    launch_ranks()
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -237,9 +264,22 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.01, help="configs/common/config.yaml values.dropout")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the decode and Mamba legs")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU check of the launch: init gloo ranks, verify the world size, print, exit")
     args = ap.parse_args()
 
-    rank, local, world = setup_distributed()
+    rank, local, world = setup_distributed(backend="gloo" if args.dry_run else None)
+    assert world == args.gpus, f"bench.py --gpus {args.gpus} but the process group has {world} ranks"
+    if args.dry_run:
+        ranks = [None] * world
+        if world > 1:
+            dist.all_gather_object(ranks, rank)
+            dist.destroy_process_group()
+        else:
+            ranks = [rank]
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": ranks}), flush=True)
+        return
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     cfg = TransformerConfig(n_layer=args.layers, block_len=args.seq, precision="bf16", dropout=args.dropout)

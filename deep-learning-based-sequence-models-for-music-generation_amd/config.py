@@ -39,6 +39,11 @@ BLOCK_LEN = 2048                              # config.yaml values.block_len
 N_META = 6                                    # metadata tokens per piece
 LEARNING_RATE = 5e-5                          # config.yaml values.learning_rate
 DROPOUT = 0.01                                # config.yaml values.dropout
+EPOCHS = 10000                                # config.yaml values.epochs
+EVAL_INTERVAL = 10                            # config.yaml values.eval_interval (steps between loss logs)
+SAVE_INTERVAL = 10                            # config.yaml values.save_interval (epochs between saves)
+TEST_RATIO = 0.2                              # config.yaml values.test_ratio
+BATCH_SIZE = 2                                # config.yaml values.batch_size
 
 
 @dataclass

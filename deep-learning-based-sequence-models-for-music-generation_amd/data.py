@@ -75,10 +75,16 @@ class SequenceDataset:
 
     directory: ``<root>/<band>/<song>.npy`` int64 1-D token arrays.
     metadata: metadata.json path or its parsed dict (band names = directory names).
-    Songs are listed with os.walk and shuffled with ``rng`` (dataset.py:66-71)."""
+    Songs are listed with os.walk and shuffled (dataset.py:66-71) with
+    ``shuffle_rng`` (default: ``rng``); ``rng`` draws the window starts and
+    augmentation shifts. Under data parallelism the shuffle must be identical
+    on every rank (the train/test split and the DistributedSampler shards
+    index the shuffled list) while the window draws differ per rank, so
+    DatasetLoader passes a rank-independent ``shuffle_rng``."""
 
     def __init__(self, directory, metadata, block_len=BLOCK_LEN, device="cuda", disc: Discretization = None,
-                 augmentation=False, start_of_seq=False, end_of_seq=False, rng: random.Random = None):
+                 augmentation=False, start_of_seq=False, end_of_seq=False, rng: random.Random = None,
+                 shuffle_rng: random.Random = None):
         self.directory = directory
         self.sequence_length = block_len
         self.disc = disc or DEFAULT_DISC
@@ -94,7 +100,7 @@ class SequenceDataset:
                 if fn.endswith(".npy"):
                     self.file_paths.append(os.path.join(root, fn))
         self.num_files = len(self.file_paths)
-        self.rng.shuffle(self.file_paths)
+        (shuffle_rng or self.rng).shuffle(self.file_paths)
         if not self.file_paths:
             raise ValueError(f"no .npy token files under {directory}")
         # one pass over the corpus: lengths, token store, per-song metadata
@@ -226,13 +232,15 @@ class DatasetLoader:
     def __init__(self, directory, metadata, batch_size=2, test_ratio=0.2, block_len=BLOCK_LEN, device="cuda",
                  parallel=False, rank=0, world=1, seed=None, **dataset_kw):
         self.directory, self.batch_size, self.test_ratio = directory, batch_size, test_ratio
-        # g: split + DistributedSampler permutation (identical on every rank);
-        # gs: this rank's weighted draws; the dataset rng: its window starts
+        # g: split + DistributedSampler permutation, and the file shuffle
+        # (identical on every rank); gs: this rank's weighted draws; the
+        # dataset rng: this rank's window starts / augmentation draws
         self.g, self.gs = torch.Generator(), torch.Generator()
         if seed is not None:
             self.g.manual_seed(seed)
             self.gs.manual_seed(seed + 1000 + rank)
-            dataset_kw.setdefault("rng", random.Random(seed + rank))
+            dataset_kw.setdefault("shuffle_rng", random.Random(seed))
+            dataset_kw.setdefault("rng", random.Random(seed + 1 + rank))
         self.dataset = SequenceDataset(directory, metadata, block_len=block_len, device=device, **dataset_kw)
         self.file_prob = self.dataset.file_prob()
         test_size = int(len(self.dataset) * test_ratio)

@@ -107,8 +107,12 @@ def generate(model, context_len, token_ids, meta_ids, num_tokens=1000, device="c
             u = torch.tensor([next(uniforms) for _ in range(B)], dtype=torch.float32).to(dev)
         else:
             if gen is None:
+                # the reference samples with torch.multinomial, i.e. from torch's
+                # global RNG, and draws only the k's from Python's random: seed
+                # the device stream from torch's CPU generator so ``rng`` sees
+                # exactly the reference's random.choice sequence
                 gen = torch.Generator(device=dev)
-                gen.manual_seed(rng.getrandbits(63) if hasattr(rng, "getrandbits") else 1234)
+                gen.manual_seed(int(torch.randint(0, 2 ** 62, (1,)).item()))
             u = torch.rand(B, device=dev, generator=gen)
         kt = torch.tensor(ks, dtype=torch.int32).to(dev)
         call("msq_decode_sample", ptr(hist), ldh, cur, ptr(z), ldz, B, V, ptr(kt), ptr(u), ptr(out_tok),

@@ -15,7 +15,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops
-from .config import LEARNING_RATE, Grammar
+from .config import BLOCK_LEN, EPOCHS, EVAL_INTERVAL, LEARNING_RATE, SAVE_INTERVAL, Grammar
 from .ddp import GradBuckets
 from .loss import ce_forward_backward
 from .transformer import Transformer, TransformerConfig
@@ -95,12 +95,19 @@ class SyntheticMIDI:
                 yield b
 
 
-def setup_distributed():
-    """torchrun env -> (rank, local_rank, world); RCCL ("nccl") on MI355X."""
+def setup_distributed(backend=None):
+    """torchrun env (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*) -> (rank,
+    local_rank, world). backend "nccl" (= RCCL over xGMI on MI355X, the
+    default) binds the process to GPU LOCAL_RANK first (train_parallel.py:
+    144-145); "gloo" touches no GPU (CPU tests and dry runs)."""
     if "RANK" in os.environ and not dist.is_initialized():
         local = int(os.environ.get("LOCAL_RANK", 0))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = backend or "nccl"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     if dist.is_initialized():
         return dist.get_rank(), int(os.environ.get("LOCAL_RANK", 0)), dist.get_world_size()
     return 0, 0, 1
@@ -136,35 +143,113 @@ def load_model(type_name, path, precision="bf16", device="cuda", **kw):
     return model.to(device)
 
 
-def train(model, type_name="transformer", data=None, steps=100, log_every=10, lr=LEARNING_RATE, save_dir=None,
-          save_every=0):
-    """Mirrors train_parallel.train: init RCCL, replicate the model, loop.
-    data: an iterable of device batches (src, trg, meta) — e.g. the train
-    loader of data.DatasetLoader — or None for synthetic grammar batches."""
+def evaluate(model, loader, grammar=None):
+    """The validation pass of train_parallel.py:197-207: model.eval(), forward
+    + filtered CE under no_grad over the test loader, averaged over its
+    batches (a device scalar; the caller decides when to sync)."""
+    from .loss import filtered_cross_entropy
+    was = model.training
+    model.eval()
+    total, n = None, 0
+    with torch.no_grad():
+        for src, trg, meta in loader:
+            l = filtered_cross_entropy(src, model(src, meta), trg, grammar)
+            total = l if total is None else total + l
+            n += 1
+    model.train(was)
+    if n == 0:
+        return None
+    return total / n
+
+
+def _epoch_batches(data, steps_per_epoch):
+    """One epoch of ``data``: a finite loader (len() batches, the reference's
+    DataLoader) or ``steps_per_epoch`` batches of an endless stream."""
+    if hasattr(data, "__len__") and not isinstance(data, SyntheticMIDI):
+        yield from data
+        return
+    it = iter(data)
+    for _ in range(steps_per_epoch):
+        yield next(it)
+
+
+def train(model, type_name="transformer", data=None, test_data=None, epochs=EPOCHS, max_steps=None,
+          eval_interval=EVAL_INTERVAL, save_interval=SAVE_INTERVAL, lr=LEARNING_RATE, save_dir=None, log_file=None,
+          steps_per_epoch=100, grammar=None):
+    """Mirrors train_parallel.train (train_parallel.py:143-235): init RCCL,
+    replicate the model (one parameter broadcast), then per epoch: model.train()
+    and a pass over the train loader (loss logged every ``eval_interval`` steps
+    on rank 0), the epoch's average loss, model.eval() + validation loss under
+    no_grad over ``test_data``, a rank-0 save every ``save_interval`` epochs
+    named by the average validation loss, and on exit (normal end, max_steps,
+    or KeyboardInterrupt) a final rank-0 save and log dump.
+
+    data / test_data: iterables of device batches (src, trg, meta) — e.g.
+    ``data.DatasetLoader(...).get_dataloaders()`` — or None for synthetic
+    grammar batches (``steps_per_epoch`` of them per epoch). The per-step loss
+    stays on the device; the host reads it only at the log points (the
+    reference syncs with loss.item() every step, :185)."""
+    from datetime import datetime
+    import json
     rank, local, world = setup_distributed()
     dev = torch.device("cuda", local)
     model.to(dev)
-    step = TrainStep(model, lr=lr)
+    step = TrainStep(model, lr=lr, grammar=grammar)
     if data is None:
-        data = SyntheticMIDI(2, model.cfg.block_len, dev, rank)
-
-    def batches():
-        while True:  # epochs of a finite loader, as the reference's epoch loop
-            n = 0
-            for b in data:
-                n += 1
-                yield b
-            if n == 0:
-                raise ValueError("empty data loader")
-    it = batches()
-    t0 = time.time()
+        data = SyntheticMIDI(2, getattr(model.cfg, "block_len", BLOCK_LEN), dev, rank)
     log = []
-    for i in range(steps):
-        src, trg, meta = next(it)
-        loss = step(src, trg, meta)
-        if (i + 1) % log_every == 0 and rank == 0:
-            log.append({"Step": i + 1, "Loss": f"{loss.item():.4f}", "elapsed_s": time.time() - t0})
-            print(f"Step: {i + 1}, Loss: {log[-1]['Loss']}")
-        if save_dir and save_every and (i + 1) % save_every == 0 and rank == 0:
-            save_model(model, loss.item(), save_dir, type_name)
+
+    def note(msg):
+        if rank == 0:
+            print(msg)
+            log.append({"timestamp": str(datetime.now()), "message": msg})
+
+    def dump():
+        if rank == 0 and log_file:
+            os.makedirs(os.path.dirname(os.path.abspath(log_file)), exist_ok=True)
+            with open(log_file, "w") as f:
+                json.dump(log, f, indent=2)
+
+    note("Training started!")
+    avg_val = None
+    n_steps = 0
+    done = False
+    try:
+        for epoch in range(epochs):
+            model.train()
+            total, nb = None, 0
+            for src, trg, meta in _epoch_batches(data, steps_per_epoch):
+                loss = step(src, trg, meta)
+                total = loss.detach().clone() if total is None else total + loss.detach()
+                nb += 1
+                n_steps += 1
+                if nb % eval_interval == 0 and rank == 0:
+                    msg = f"{loss.item():.4f}"
+                    log.append({"Step": n_steps, "Loss": msg})
+                    print(f"Step: {n_steps}, Loss: {msg}")
+                if max_steps is not None and n_steps >= max_steps:
+                    done = True
+                    break
+            if nb == 0:
+                raise ValueError("empty data loader")
+            note(f"Epoch [{epoch + 1}/{epochs}], Average Loss: {(total / nb).item():.4f}")
+            if test_data is not None:
+                v = evaluate(model, test_data, grammar)
+                if v is not None:
+                    avg_val = v.item()
+                    note(f"Epoch [{epoch + 1}/{epochs}], Validation Loss: {avg_val:.4f}")
+            if save_dir and (epoch + 1) % save_interval == 0 and rank == 0:
+                save_model(model, avg_val if avg_val is not None else 0.0, save_dir, type_name)
+                dump()
+            if done:
+                break
+    except KeyboardInterrupt:
+        if rank == 0:
+            print("Interrupted!")
+    finally:
+        if rank == 0 and save_dir:
+            print("Saving model before exit...")
+            save_model(model, avg_val if avg_val is not None else 0.0, save_dir, type_name)
+        note("Training complete!")
+        dump()
     return log

@@ -23,7 +23,7 @@ import torch.nn as nn
 from . import _lib as L
 from . import ops
 from .attention import relattn_fwd, relattn_bwd
-from .config import N_META, VOCAB_SIZE, METADATA_VOCAB_SIZE, BLOCK_LEN
+from .config import N_META, VOCAB_SIZE, METADATA_VOCAB_SIZE, BLOCK_LEN, DROPOUT
 
 # dropout sites of the counter-based keep masks (csrc/common.h; oracle/dropout.py):
 # attention probabilities of layer l / batch b / head h, proj output, FFN output
@@ -36,7 +36,9 @@ class TransformerConfig:
     n_heads: int = 8
     n_layer: int = 8
     block_len: int = BLOCK_LEN
-    dropout: float = 0.0
+    # configs/common/config.yaml values.dropout, merged into the Transformer's
+    # params by get_transformer_dict (train_parallel.py:49-54)
+    dropout: float = DROPOUT
     vocab_size: int = VOCAB_SIZE
     metadata_vocab_size: int = METADATA_VOCAB_SIZE
     precision: str = "bf16"  # "bf16" (MFMA fast path) | "fp32" (exact parity path)
@@ -57,7 +59,7 @@ class TransformerConfig:
     def from_params(cls, params, **kw):
         """Accepts the reference's SimpleNamespace (train_parallel.py:49-54)."""
         return cls(n_embd=params.n_embd, n_heads=params.n_heads, n_layer=params.n_layer,
-                   block_len=params.block_len, dropout=getattr(params, "dropout", 0.0),
+                   block_len=params.block_len, dropout=getattr(params, "dropout", DROPOUT),
                    vocab_size=params.vocab_size, metadata_vocab_size=params.metadata_vocab_size, **kw)
 
 

@@ -1,0 +1,73 @@
+"""Worker of tests/test_ddp_gpu.py (not a test module): one rank of a
+world-2 data-parallel step on the ONE leased GPU, process group gloo over
+CUDA tensors, through the real TrainStep: forward, fused filtered CE, the
+two-stream backward with the engine's per-layer bucket hooks (ddp.GradBuckets
+all-reducing on its side stream), fused Adam with the 1/world scale.
+Rank 0 writes the averaged gradient and the updated parameters to an .npz.
+
+usage (under torch.distributed.run): ddp_worker.py <transformer|mamba> <same|split> <out.npz>"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import _pkgload  # noqa: E402
+
+_pkgload.load()
+from midiseq.train_parallel import TrainStep, setup_distributed  # noqa: E402
+
+
+def build_model(kind):
+    """Small bf16 configs on the MFMA paths (hs = 128 attention)."""
+    if kind == "transformer":
+        from midiseq.transformer import Transformer, TransformerConfig
+        return Transformer(TransformerConfig(n_embd=256, n_heads=2, n_layer=2, block_len=128, dropout=0.0))
+    from midiseq.mamba import Mamba
+    return Mamba(d_model=256, n_layers=2)
+
+
+def full_batch(T=128, B=4):
+    from oracle.fill import REAL, grammar_tokens
+    rng = np.random.default_rng(21)
+    w = np.stack([grammar_tokens(rng, REAL, T + 1) for _ in range(B)])
+    meta = np.array([[519, 279, 202, 202, 202, 178], [432, 277, 202, 202, 202, 173],
+                     [437, 279, 272, 202, 202, 180], [452, 272, 202, 202, 202, 184]][:B])
+    return torch.from_numpy(w[:, :-1].copy()), torch.from_numpy(w[:, 1:].copy()), torch.from_numpy(meta)
+
+
+def rank_slice(mode, rank, world, B=4):
+    if mode == "same":
+        return slice(0, B // world)
+    n = B // world
+    return slice(rank * n, (rank + 1) * n)
+
+
+def main():
+    kind, mode, out = sys.argv[1], sys.argv[2], sys.argv[3]
+    rank, _, world = setup_distributed(backend="gloo")
+    assert world == 2
+    torch.cuda.set_device(0)
+    model = build_model(kind).to("cuda")
+    if rank == 1:  # the parameter broadcast of TrainStep (DDP ctor) must overwrite this
+        with torch.no_grad():
+            model.flat.data.mul_(1.5)
+    step = TrainStep(model)
+    assert step.buckets is not None
+    src, trg, meta = full_batch()
+    sl = rank_slice(mode, rank, world)
+    loss = step(src[sl].cuda(), trg[sl].cuda(), meta[sl].cuda())
+    torch.cuda.synchronize()
+    if rank == 0:
+        np.savez(out, grads=(step.grads / world).cpu().numpy(), flat=model.flat.data.cpu().numpy(),
+                 loss=loss.item())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

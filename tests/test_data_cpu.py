@@ -85,3 +85,29 @@ def test_samplers(tmp_path):
     shards = [data.DeviceLoader(data._Subset(None, range(7)), 2, rank=r, world=3,
                                 generator=torch.Generator().manual_seed(5))._indices() for r in range(3)]
     assert all(len(s) == 3 for s in shards) and set(sum(shards, [])) == set(range(7))
+
+
+@pytest.mark.parametrize("parallel", [False, True])
+def test_ranks_share_split_and_shard_disjointly(tmp_path, parallel):
+    """world = 2: both ranks see the same shuffled song list and train/test
+    split (processing/dataset.py:66-71 shuffle, :280-288 random_split), draw
+    different windows, and with parallel=True (DistributedSampler) their train
+    shards partition the train songs."""
+    root = tmp_path
+    rng = np.random.default_rng(2)
+    for b in ("ABBA", "Mozart", "Bach"):
+        (root / b).mkdir()
+        for k in range(4):
+            np.save(root / b / f"s{k}.npy", rng.integers(0, 17914, size=int(rng.integers(40, 90))).astype(np.int64))
+    arts = [a for a in _artists() if a["name"] in ("ABBA", "Mozart", "Bach")]
+    dls = [data.DatasetLoader(str(root), {"artists": arts}, batch_size=2, test_ratio=0.34, block_len=16,
+                              device="cpu", parallel=parallel, rank=r, world=2, seed=7) for r in range(2)]
+    assert dls[0].dataset.file_paths == dls[1].dataset.file_paths
+    assert dls[0].train_dataset.indices == dls[1].train_dataset.indices
+    assert dls[0].test_dataset.indices == dls[1].test_dataset.indices
+    draws = [[dl.dataset.window_params(i)[1] for i in range(len(dl.dataset))] for dl in dls]
+    assert draws[0] != draws[1]
+    if parallel:
+        shards = [dl.get_dataloaders()[0]._indices() for dl in dls]
+        assert not set(shards[0]) & set(shards[1])
+        assert set(shards[0]) | set(shards[1]) == set(dls[0].train_dataset.indices)

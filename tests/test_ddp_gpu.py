@@ -1,0 +1,73 @@
+"""Data-parallel step on the GPU through the real engine:
+two ranks on the one leased GPU (gloo over CUDA tensors; RCCL needs one GPU
+per rank) run tests/ddp_worker.py — TrainStep with the backward's per-layer
+bucket hooks, the weight-gradient side stream and the all-reduce side stream
+— and are compared with a single process running the same TrainStep.
+
+* "same": both ranks get the same 2 sequences. Their SUM all-reduce divided
+  by world is then exactly the single-process gradient of those sequences
+  (x + x = 2x in fp32): a bucket that is never reduced, reduced twice, or
+  reduced before the dW stream wrote it shows up far above the tolerance
+  (fp32 atomics in the embedding backward: 1e-5 relative).
+* "split": the ranks get sequences 0-1 and 2-3; the averaged gradient equals
+  the single-process gradient of all 4 (the loss is a mean over B*T) up to
+  bf16 summation order.
+Reference loop: train_parallel.py:143-183 (DDP ctor broadcast, backward
+all-reduce, Adam)."""
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+HERE = Path(__file__).parent
+
+
+def _run_world2(kind, mode, tmp_path):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = tmp_path / f"{kind}_{mode}.npz"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(HERE / "ddp_worker.py"), kind, mode, str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=dict(os.environ, OMP_NUM_THREADS="4"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return np.load(out)
+
+
+def _single(kind, rows):
+    sys.path.insert(0, str(HERE))
+    import ddp_worker as w
+    from midiseq.train_parallel import TrainStep
+    model = w.build_model(kind).to("cuda")
+    step = TrainStep(model)
+    src, trg, meta = w.full_batch()
+    loss = step(src[rows].cuda(), trg[rows].cuda(), meta[rows].cuda())
+    torch.cuda.synchronize()
+    return step.grads.cpu().numpy(), model.flat.data.cpu().numpy(), loss.item()
+
+
+@pytest.mark.parametrize("kind", ["transformer", "mamba"])
+def test_world2_same_data_equals_single_process(kind, tmp_path):
+    got = _run_world2(kind, "same", tmp_path)
+    g, flat, loss = _single(kind, slice(0, 2))
+    assert abs(float(got["loss"]) - loss) <= 1e-5 * abs(loss)
+    err = np.abs(got["grads"] - g).max()
+    assert err <= 1e-5 * np.abs(g).max(), err
+    # parameters after one Adam step (scale 1/world folded into the kernel)
+    np.testing.assert_allclose(got["flat"], flat, rtol=0, atol=2e-7)
+
+
+@pytest.mark.parametrize("kind", ["transformer", "mamba"])
+def test_world2_split_batch_averages_gradients(kind, tmp_path):
+    got = _run_world2(kind, "split", tmp_path)
+    g, _, _ = _single(kind, slice(0, 4))
+    a, b = got["grads"].astype(np.float64), g.astype(np.float64)
+    nr = np.linalg.norm(a - b) / np.linalg.norm(b)
+    cos = float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
+    assert nr < 2e-2 and cos > 0.9995, (nr, cos)

@@ -51,3 +51,26 @@ def test_generate_bf16_runs_and_respects_grammar():
     seqs = generate(m, 64, src, meta, num_tokens=6, rng=random.Random(0))
     assert np.array(seqs).shape == (3, 70)
     assert all(0 <= t < REAL.size for row in seqs for t in row)
+
+
+def test_default_sampling_leaves_python_rng_to_the_k_choice():
+    """Without injected uniforms the device sampler is seeded from torch's RNG
+    (the reference's torch.multinomial stream), so the caller's Python
+    ``random`` only feeds the k choice of scripts/generate.py:47-56: replaying
+    choose_k over the generated rows with a fresh Random(seed) ends in the same
+    generator state as the one generate() consumed."""
+    from midiseq.generate import choose_k
+    vocab, mv, hp, steps = GCASES["small"]
+    cfg = TransformerConfig(vocab_size=vocab.size, metadata_vocab_size=mv, precision="fp32", **hp)
+    m = Transformer(cfg).to("cuda")
+    g4 = np.load(G / "g4_generate.npz")
+    src, meta = torch.from_numpy(g4["small_src"]), torch.from_numpy(g4["small_meta"])
+    rng = random.Random(77)
+    torch.manual_seed(5)
+    seqs = np.array(generate(m, hp["block_len"], src, meta, num_tokens=steps, rng=rng, grammar=grammar_for(vocab)))
+    replay = random.Random(77)
+    T0 = src.shape[1]
+    start = grammar_for(vocab).disc.start_idx
+    for s in range(steps):
+        choose_k(seqs[:, T0 + s - 1].tolist(), start, replay)
+    assert rng.getstate() == replay.getstate()

@@ -39,7 +39,7 @@ def grammar_for(v):
 
 
 def build(vocab, mv, hp, precision):
-    cfg = TransformerConfig(vocab_size=vocab.size, metadata_vocab_size=mv, precision=precision, **hp)
+    cfg = TransformerConfig(vocab_size=vocab.size, metadata_vocab_size=mv, precision=precision, dropout=0.0, **hp)
     m = Transformer(cfg).to(dev)
     shapes = otr.param_shapes(hp["n_embd"], hp["n_heads"], hp["n_layer"], hp["block_len"], vocab.size, mv)
     p = otr.filled_params(shapes)
