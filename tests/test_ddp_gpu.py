@@ -59,8 +59,12 @@ def test_world2_same_data_equals_single_process(kind, tmp_path):
     assert abs(float(got["loss"]) - loss) <= 1e-5 * abs(loss)
     err = np.abs(got["grads"] - g).max()
     assert err <= 1e-5 * np.abs(g).max(), err
-    # parameters after one Adam step (scale 1/world folded into the kernel)
-    np.testing.assert_allclose(got["flat"], flat, rtol=0, atol=2e-7)
+    # parameters after one Adam step (scale 1/world folded into the kernel).
+    # Step 1 of Adam moves each parameter by lr * g / (|g| + eps): where |g| is
+    # near eps (1e-8) the 1e-5-relative atomics noise of the gradient shows,
+    # so allow a few elements up to 2 % of lr (5e-5)
+    d = np.abs(got["flat"] - flat)
+    assert d.max() <= 1e-6 and (d > 2e-7).sum() <= 16, (d.max(), (d > 2e-7).sum())
 
 
 @pytest.mark.parametrize("kind", ["transformer", "mamba"])
