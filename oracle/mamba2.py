@@ -36,24 +36,62 @@ def mixer(p, pre, u, chunked=False):
     dt = F.softplus(dt + p[pre + "dt_bias"])             # [B, L, H]
     A = -torch.exp(p[pre + "A_log"])                      # [H]
     x = x.reshape(Bsz, L, H, HEADDIM)
-    h = torch.zeros(Bsz, H, HEADDIM, D_STATE, dtype=u.dtype)
-    ys = []
-    for t in range(L):
-        dA = torch.exp(dt[:, t] * A)                      # [B, H]
-        h = h * dA[:, :, None, None] + (dt[:, t, :, None] * x[:, t])[..., None] * Bm[:, t, None, None, :]
-        ys.append(torch.einsum("bhpn,bn->bhp", h, Cm[:, t]))
-    y = torch.stack(ys, dim=1) + p[pre + "D"][None, None, :, None] * x
+    if chunked:
+        y = ssd_chunked(x, dt, A, Bm, Cm) + p[pre + "D"][None, None, :, None] * x
+    else:
+        h = torch.zeros(Bsz, H, HEADDIM, D_STATE, dtype=u.dtype)
+        ys = []
+        for t in range(L):
+            dA = torch.exp(dt[:, t] * A)                      # [B, H]
+            h = h * dA[:, :, None, None] + (dt[:, t, :, None] * x[:, t])[..., None] * Bm[:, t, None, None, :]
+            ys.append(torch.einsum("bhpn,bn->bhp", h, Cm[:, t]))
+        y = torch.stack(ys, dim=1) + p[pre + "D"][None, None, :, None] * x
     y = y.reshape(Bsz, L, d_inner)
     g = y * F.silu(z)
     g = g * torch.rsqrt(g.pow(2).mean(-1, keepdim=True) + 1e-5) * p[pre + "norm.weight"]
     return g @ p[pre + "out_proj.weight"].t()
 
 
-def forward(p, tokens, meta, n_layers):
+def ssd_chunked(x, dt, A, Bm, Cm, Q=256):
+    """The same recurrence evaluated in chunks of Q positions (the SSD
+    "chunked scan" form of the Mamba2 paper: within a chunk y = (C B^T o decay)
+    (dt x), across chunks the state h carried by the recurrence at chunk
+    granularity). Equal to the sequential loop up to fp32 summation order; used
+    for long sequences, where autograd through 4 k single steps is slow.
+    x [B,L,H,P], dt [B,L,H], A [H], Bm/Cm [B,L,N] -> y [B,L,H,P] (no D skip)."""
+    Bsz, L, H, P = x.shape
+    N = Bm.shape[-1]
+    nc = -(-L // Q)
+    pad = nc * Q - L
+    if pad:  # zero tail: dt = 0 adds nothing and decays nothing
+        x, dt = F.pad(x, (0, 0, 0, 0, 0, pad)), F.pad(dt, (0, 0, 0, pad))
+        Bm, Cm = F.pad(Bm, (0, 0, 0, pad)), F.pad(Cm, (0, 0, 0, pad))
+    x, dt = x.view(Bsz, nc, Q, H, P), dt.view(Bsz, nc, Q, H)
+    Bm, Cm = Bm.view(Bsz, nc, Q, N), Cm.view(Bsz, nc, Q, N)
+    acum = torch.cumsum(dt * A, dim=2)                                  # [B,c,Q,H]
+    u = dt[..., None] * x                                               # [B,c,Q,H,P]
+    seg = acum.transpose(2, 3)[..., :, None] - acum.transpose(2, 3)[..., None, :]  # [B,c,H,t,s]
+    causal = torch.ones(Q, Q, dtype=torch.bool).tril()
+    decay = torch.exp(seg.masked_fill(~causal, float("-inf")))
+    cb = torch.einsum("bctn,bcsn->bcts", Cm, Bm)                        # [B,c,t,s]
+    y = torch.einsum("bchts,bcshp->bcthp", cb[:, :, None] * decay, u)   # intra-chunk
+    last = acum[:, :, -1:, :]                                           # [B,c,1,H]
+    st = torch.einsum("bcsn,bcsh,bcshp->bchpn", Bm, torch.exp(last - acum), u)  # chunk-local end states
+    h = torch.zeros(Bsz, H, P, N, dtype=x.dtype)
+    prev = []
+    for c in range(nc):
+        prev.append(h)
+        h = h * torch.exp(last[:, c, 0])[:, :, None, None] + st[:, c]
+    hp = torch.stack(prev, dim=1)                                       # [B,c,H,P,N] state entering chunk c
+    y = y + torch.einsum("bctn,bcth,bchpn->bcthp", Cm, torch.exp(acum), hp)
+    return y.reshape(Bsz, nc * Q, H, P)[:, :L]
+
+
+def forward(p, tokens, meta, n_layers, chunked=False):
     """Mamba.forward (mamba.py:27-35): NO residual, no per-layer norm."""
     x = torch.cat([p["metadata_embedding.weight"][meta], p["token_embedding.weight"][tokens]], dim=1)
     for i in range(n_layers):
-        x = mixer(p, f"layers.{i}.", x)
+        x = mixer(p, f"layers.{i}.", x, chunked)
     x = F.layer_norm(x, (x.shape[-1],), p["norm.weight"], p["norm.bias"], 1e-5)
     return (x @ p["output_layer.weight"].t() + p["output_layer.bias"])[:, META:]
 

@@ -4,6 +4,7 @@ Mamba2 mixer standing in for mamba_ssm.Mamba2 (tests/golden/make_golden.py)."""
 from pathlib import Path
 
 import numpy as np
+import pytest
 import torch
 
 from oracle import loss as oloss
@@ -20,12 +21,15 @@ def test_default_param_count_matches_reference_notebook():
     assert n == int(g5["default_param_count"]) == 101_972_666  # scripts/Test Accuracy.ipynb:52
 
 
-def test_mamba_fwd_bwd_matches_golden():
+@pytest.mark.parametrize("chunked", [False, True])
+def test_mamba_fwd_bwd_matches_golden(chunked):
+    """Both oracle forms (sequential recurrence; chunked SSD with Q = 256, which
+    T = 300 (+6 meta) crosses) against the reference's outputs."""
     g5 = np.load(G / "g5_mamba.npz")
     shapes = om.param_shapes(128, 2, REAL.size, 568)
     p = {k: v.requires_grad_(True) for k, v in om.filled_params(shapes).items()}
     src, trg, meta = (torch.from_numpy(g5[n]) for n in ("src", "trg", "meta"))
-    logits = om.forward(p, src, meta, 2)
+    logits = om.forward(p, src, meta, 2, chunked=chunked)
     loss = oloss.loss(src, trg, logits, REAL)
     loss.backward()
     assert abs(loss.item() - float(g5["loss"])) < 1e-4 * abs(float(g5["loss"]))
