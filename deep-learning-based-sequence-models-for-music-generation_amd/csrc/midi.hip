@@ -290,6 +290,98 @@ __global__ __launch_bounds__(MIDI_NT) void midi_decode_kernel(const int64_t* __r
     }
 }
 
+
+// Note -> token encode of a batch of songs (processing/processing.py:129-152
+// encode, + :111-126 adjust_note_time): the offline preprocessing step that
+// turns extracted notes into the .npy token rows the data feed reads.
+// One wavefront per song, 64 notes per step:
+//  * adjust_note_time is a running fp64 sum of (start - prev_start) /
+//    resolution, resolution from the PREVIOUS note's tempo: every lane forms
+//    its note's increment, then a 64-step readlane chain adds them in the
+//    reference's order (bit-identical doubles, FMA contraction off); int()
+//    truncation gives the note's start / end beat (a note whose end truncates
+//    to its start lasts one beat);
+//  * the token count of a note is 4, plus 1 when its time-shift token differs
+//    from the previous note's (the first note always emits one); an
+//    exclusive wave sum places every note's tokens.
+// Songs are independent: grid = n_songs.
+__global__ __launch_bounds__(64) void midi_encode_kernel(const int32_t* __restrict__ pitch,
+                                                         const int32_t* __restrict__ channel,
+                                                         const int32_t* __restrict__ dyn,
+                                                         const int32_t* __restrict__ tempo,
+                                                         const double* __restrict__ t_start,
+                                                         const double* __restrict__ t_end,
+                                                         const int64_t* __restrict__ song_off, int64_t P, int64_t C,
+                                                         int64_t D, int64_t Ln, int64_t Tm, int64_t Tp, Disc d,
+                                                         double res_per_beat, int64_t* __restrict__ tokens,
+                                                         int64_t* __restrict__ beat_start,
+                                                         int64_t* __restrict__ beat_end, int64_t* __restrict__ count) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x;
+    const int64_t s = blockIdx.x, o = song_off[s], n = song_off[s + 1] - o;
+    int64_t* out = tokens + 5 * o;
+    double run = 0.0;         // current_beats after the previous step's last note
+    int64_t bs_last = 0;      // time_prev (integer beat start of the previous note)
+    int64_t td_last = 0;      // time_delta_prev (a token id; 0 before the first note)
+    int64_t pos = 0;          // tokens written so far
+    for (int64_t k0 = 0; k0 < n; k0 += 64) {
+        const int64_t k = k0 + lane;
+        double inc = 0.0, dur = 0.0;
+        int32_t pi = 0, ch = 0, dy = 0, tp = 0;
+        if (k < n) {
+            const int64_t i = o + k;
+            const double prev_t = k == 0 ? 0.0 : t_start[i - 1];
+            const int32_t prev_tp = k == 0 ? tempo[o] : tempo[i - 1];
+            const double resolution = 60.0 / (double)prev_tp / res_per_beat;
+            const double ts = t_start[i];
+            inc = (ts - prev_t) / resolution;
+            dur = (t_end[i] - ts) / resolution;
+            pi = pitch[i];
+            ch = channel[i];
+            dy = dyn[i];
+            tp = tempo[i];
+        }
+        const uint64_t ib = __builtin_bit_cast(uint64_t, inc);
+        const int ilo = (int)(uint32_t)ib, ihi = (int)(uint32_t)(ib >> 32);
+        double cur = 0.0, r = run;
+#pragma unroll
+        for (int j = 0; j < 64; ++j) {
+            const uint64_t bj = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(ilo, j) |
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(ihi, j) << 32);
+            r = r + __builtin_bit_cast(double, bj);
+            if (j == lane) cur = r;
+        }
+        const int64_t last = min((int64_t)63, n - 1 - k0);
+        run = __shfl(cur, (int)last, 64);
+        const double fut = cur + dur;
+        const int64_t bs = (int64_t)cur;   // int(): truncation toward zero
+        const int64_t fe = (int64_t)fut;
+        const int64_t be = fe == bs ? bs + 1 : fe;
+        // previous note's beat start / time token (lane - 1, or the carry)
+        int64_t bs_prev = __shfl_up(bs, 1, 64);
+        if (lane == 0) bs_prev = bs_last;
+        const int64_t td = d.time0 + min(bs - bs_prev, Tm - 1);
+        int64_t td_prev = __shfl_up(td, 1, 64);
+        if (lane == 0) td_prev = td_last;
+        const int64_t cnt = k < n ? (td != td_prev ? 5 : 4) : 0;
+        const int64_t at = pos + wave_excl_sum(cnt, lane);
+        if (k < n) {
+            beat_start[o + k] = bs;
+            beat_end[o + k] = be;
+            int64_t* q = out + at;
+            q[0] = min((int64_t)pi + (int64_t)ch * P, P * C - 1);  // start_idx pitch = 0
+            q[1] = d.dyn0 + min((int64_t)dy, D - 1);
+            q[2] = d.len0 + min(be - bs, Ln - 1);
+            int e = 3;
+            if (td != td_prev) q[e++] = td;
+            q[e] = d.tempo0 + min((int64_t)tp, Tp - 1);
+        }
+        bs_last = __shfl(bs, (int)last, 64);
+        td_last = __shfl(td, (int)last, 64);
+        pos = __shfl(at + cnt, (int)last, 64);
+    }
+    if (lane == 0) count[s] = pos;
+}
 }  // namespace
 
 extern "C" int msq_midi_decode(const int64_t* rows, int64_t B, int64_t L, int64_t ld, const int64_t* disc,
@@ -313,6 +405,29 @@ extern "C" int msq_midi_decode(const int64_t* rows, int64_t B, int64_t L, int64_
     const size_t lds = (size_t)MIDI_NT * (((L + MIDI_NT - 1) / MIDI_NT) | 1) * sizeof(int32_t);
     hipLaunchKernelGGL(midi_decode_kernel, dim3((unsigned)B), dim3(MIDI_NT), lds, (hipStream_t)stream, rows, ld, L, cap, d,
                        (double)res_per_beat, pitch, channel, dyn, tempo, beat_start, beat_end, t_start, t_end, count);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
+extern "C" int msq_midi_encode(const int32_t* pitch, const int32_t* channel, const int32_t* dyn, const int32_t* tempo,
+                               const double* t_start, const double* t_end, const int64_t* song_off,
+                               int64_t n_songs, const int64_t* disc, int64_t res_per_beat, int64_t* tokens,
+                               int64_t* beat_start, int64_t* beat_end, int64_t* count, void* stream) {
+    MSQ_CHECK_ARG(n_songs >= 0 && song_off && disc && res_per_beat > 0, "msq_midi_encode: bad args");
+    MSQ_CHECK_ARG(pitch && channel && dyn && tempo && t_start && t_end, "msq_midi_encode: null note column");
+    MSQ_CHECK_ARG(tokens && beat_start && beat_end && count, "msq_midi_encode: null output");
+    MSQ_CHECK_ARG(disc[0] > 0 && disc[1] > 0 && disc[2] > 0 && disc[3] > 0 && disc[4] > 0 && disc[5] > 0,
+                  "msq_midi_encode: bad discretization");
+    if (n_songs == 0) return MSQ_OK;
+    Disc d{};
+    d.P = disc[0];
+    d.dyn0 = disc[0] * disc[1];
+    d.len0 = d.dyn0 + disc[2];
+    d.time0 = d.len0 + disc[3];
+    d.tempo0 = d.time0 + disc[4];
+    hipLaunchKernelGGL(midi_encode_kernel, dim3((unsigned)n_songs), dim3(64), 0, (hipStream_t)stream, pitch, channel, dyn,
+                       tempo, t_start, t_end, song_off, disc[0], disc[1], disc[2], disc[3], disc[4], disc[5], d,
+                       (double)res_per_beat, tokens, beat_start, beat_end, count);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }

@@ -1,10 +1,18 @@
-"""Token -> note decode of generated rows on the device.
+"""The note <-> token codec on the device.
 
-Drop-in for ``processing.decode(token_seq)`` (processing/processing.py:171-214,
-with revert_note_time :154-169) as called by scripts/generate_midi_combined.py
-:143-156 on each generated row. ``decode_batch`` runs ONE launch of
-``msq_midi_decode`` (csrc/midi.hip) over all B rows while they are still in
-HBM; ``decode`` returns the reference's list of ``MIDI_note`` for one row.
+* Decode: drop-in for ``processing.decode(token_seq)`` (processing/processing.py
+  :171-214, with revert_note_time :154-169) as called by scripts/
+  generate_midi_combined.py:143-156 on each generated row. ``decode_batch``
+  runs ONE launch of ``msq_midi_decode`` (csrc/midi.hip) over all B rows while
+  they are still in HBM; ``decode`` returns the reference's list of
+  ``MIDI_note`` for one row.
+* Encode: drop-in for ``processing.encode(midi_notes)`` (:129-152, with
+  adjust_note_time :111-126): ``encode_batch`` turns many songs' notes into
+  token rows in ONE launch of ``msq_midi_encode``; ``extract_midi`` (:57-83)
+  reads a .mid file through midiseq.smf (pretty_midi is absent here: parity
+  of extraction itself is unpinned) and ``preprocess_midi_files`` (:24-55)
+  writes the ``<out>/<model>/<band>/<song>.npy`` token store the data feed
+  loads.
 
 No CPU fallback: without libmidiseq.so the call raises RuntimeError.
 """
@@ -104,3 +112,105 @@ def decode(token_seq, disc: Discretization = DEFAULT_DISC):
     if not t.is_cuda:
         t = t.cuda()
     return decode_batch(t.contiguous(), disc).notes(0)
+
+
+def encode_batch(songs, disc: Discretization = DEFAULT_DISC, res_per_beat: int = BAR_RES, device="cuda"):
+    """songs: list of lists of MIDI_note (sorted by time_start; times in
+    seconds, integer tempos). Returns (tokens: list of int64 numpy arrays,
+    beats: list of int64 [n, 2] arrays = the notes' adjusted time_start /
+    time_end) from one msq_midi_encode launch."""
+    import numpy as np
+    off = np.zeros(len(songs) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(s) for s in songs])
+    n = int(off[-1])
+    cols = np.zeros((4, max(n, 1)), dtype=np.int32)
+    times = np.zeros((2, max(n, 1)), dtype=np.float64)
+    k = 0
+    for song in songs:
+        for m in song:
+            cols[:, k] = (int(m.pitch), int(m.channel), int(m.dynamic), int(m.tempo))
+            times[:, k] = (float(m.time_start), float(m.time_end))
+            k += 1
+    dev = torch.device(device)
+    c = torch.from_numpy(cols).to(dev)
+    t = torch.from_numpy(times).to(dev)
+    o = torch.from_numpy(off).to(dev)
+    tok = torch.empty(max(5 * n, 1), dtype=torch.int64, device=dev)
+    beats = torch.empty(2, max(n, 1), dtype=torch.int64, device=dev)
+    count = torch.empty(max(len(songs), 1), dtype=torch.int64, device=dev)
+    d = (ctypes.c_int64 * 6)(disc.pitch, disc.channel, disc.dyn, disc.length, disc.time, disc.tempo)
+    call("msq_midi_encode", ptr(c[0]), ptr(c[1]), ptr(c[2]), ptr(c[3]), ptr(t[0]), ptr(t[1]), ptr(o), len(songs), d,
+         res_per_beat, ptr(tok), ptr(beats[0]), ptr(beats[1]), ptr(count), stream())
+    tok, beats, count = tok.cpu().numpy(), beats.cpu().numpy(), count.cpu().numpy()
+    out_t = [tok[5 * off[i]:5 * off[i] + count[i]].copy() for i in range(len(songs))]
+    out_b = [beats[:, off[i]:off[i + 1]].T.copy() for i in range(len(songs))]
+    return out_t, out_b
+
+
+def encode(midi_notes, disc: Discretization = DEFAULT_DISC):
+    """processing.encode(midi_notes) drop-in: returns the token list and, like
+    the reference's adjust_note_time, rewrites each note's time_start /
+    time_end to integer beats."""
+    if not midi_notes:
+        raise IndexError("list index out of range")  # adjust_note_time reads midi_notes[0]
+    toks, beats = encode_batch([midi_notes], disc)
+    for m, (bs, be) in zip(midi_notes, beats[0]):
+        m.time_start, m.time_end = int(bs), int(be)
+    return [int(x) for x in toks[0]]
+
+
+def extract_midi(path):
+    """processing.extract_midi (processing.py:57-83) over midiseq.smf: the
+    non-drum notes of a .mid file with the tempo (round(bpm)) in force at each
+    note's start, de-duplicated and sorted by start time."""
+    from . import smf
+    raw, tempos = smf.read_midi(path)
+    notes = []
+    for p, a, b, vel, prog, drum in raw:
+        if drum:
+            continue
+        k = 0
+        while k + 1 < len(tempos) and tempos[k + 1][0] <= a:
+            k += 1
+        notes.append(MIDI_note(pitch=abs(p), time_start=abs(a), time_end=abs(b), dynamic=abs(vel), channel=abs(prog),
+                               tempo=round(tempos[k][1])))
+    return sorted(list(set(notes)), key=lambda n: n.time_start)
+
+
+def preprocess_midi_files(midi_folder, preprocess_folder, min_notes=200, batch=64):
+    """processing.preprocess_midi_files (processing.py:24-55): every
+    <midi_folder>/<model>/<band>/<song>.mid(i) with >= min_notes notes ->
+    <preprocess_folder>/<model>/<band>/<song>.npy token row; existing outputs
+    are kept. Songs are encoded ``batch`` at a time on the device."""
+    import os
+    from pathlib import Path
+    import numpy as np
+    todo = []
+    for root, _, files in os.walk(midi_folder):
+        for fn in files:
+            if fn.lower().endswith((".mid", ".midi")):
+                pth = Path(root) / fn
+                model, band = pth.parts[-3], pth.parts[-2]
+                dst = Path(preprocess_folder) / model / band / pth.stem
+                if not os.path.exists(str(dst) + ".npy"):
+                    todo.append((pth, dst))
+    written = []
+    for i in range(0, len(todo), batch):
+        songs, dsts = [], []
+        for src, dst in todo[i:i + batch]:
+            try:
+                notes = extract_midi(str(src))
+            except Exception:  # the reference skips unreadable files (bare except)
+                continue
+            if len(notes) < min_notes:
+                continue
+            songs.append(notes)
+            dsts.append(dst)
+        if not songs:
+            continue
+        toks, _ = encode_batch(songs)
+        for dst, t in zip(dsts, toks):
+            os.makedirs(dst.parent, exist_ok=True)
+            np.save(str(dst) + ".npy", t.astype(np.int64))
+            written.append(str(dst) + ".npy")
+    return written

@@ -293,6 +293,19 @@ int msq_midi_decode(const int64_t* rows, int64_t B, int64_t L, int64_t ld, const
                     int64_t cap, int32_t* pitch, int32_t* channel, int32_t* dyn, int32_t* tempo, int64_t* beat_start,
                     int64_t* beat_end, double* t_start, double* t_end, int64_t* count, void* stream);
 
+/* Note -> token encode of a batch of songs (replaces processing/processing.py
+ * :129-152 encode + :111-126 adjust_note_time, the preprocessing step of
+ * preprocess_midi_files :24-55). Song s = notes [song_off[s], song_off[s+1])
+ * of the note columns (sorted by start as extract_midi leaves them; times in
+ * seconds, tempo = round(bpm)); disc as above, res_per_beat = bar_res.
+ * Writes song s's tokens to tokens[5*song_off[s] ..] (5 slots per note),
+ * count[s] = its token count, and each note's integer beats (the notes'
+ * time_start / time_end after adjust_note_time) to beat_start / beat_end.   */
+int msq_midi_encode(const int32_t* pitch, const int32_t* channel, const int32_t* dyn, const int32_t* tempo,
+                    const double* t_start, const double* t_end, const int64_t* song_off, int64_t n_songs,
+                    const int64_t* disc, int64_t res_per_beat, int64_t* tokens, int64_t* beat_start, int64_t* beat_end,
+                    int64_t* count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

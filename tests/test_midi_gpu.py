@@ -80,3 +80,75 @@ def test_decode_errors_like_reference():
     notes = midi.decode([5, s["dyn"], s["length"], s["tempo"] + 9, 6, s["dyn"] + 1, s["length"] + 2, s["tempo"]])
     ref = omidi.decode([5, s["dyn"], s["length"], s["tempo"] + 9, 6, s["dyn"] + 1, s["length"] + 2, s["tempo"]], s)
     assert [(x.time_start, x.time_end) for x in notes] == [(r[6], r[7]) for r in ref]
+
+
+G8 = np.load(Path(__file__).parent / "golden" / "g8_encode.npz")
+
+
+def _g8_notes(s):
+    f, t = G8[f"notes_{s}"], G8[f"times_{s}"]
+    return [midi.MIDI_note(pitch=int(a[0]), time_start=float(b[0]), time_end=float(b[1]), dynamic=int(a[2]),
+                           channel=int(a[1]), tempo=int(a[3])) for a, b in zip(f, t)]
+
+
+def test_encode_batch_matches_reference_golden():
+    """msq_midi_encode over all G8 songs in one launch: tokens and adjusted
+    beats bit-exact against the reference's processing.encode (G8)."""
+    n = int(G8["n_songs"])
+    toks, beats = midi.encode_batch([_g8_notes(s) for s in range(n)])
+    for s in range(n):
+        np.testing.assert_array_equal(beats[s], G8[f"beats_{s}"])
+        np.testing.assert_array_equal(toks[s], G8[f"tokens_{s}"])
+
+
+def test_encode_dropin_mutates_notes_like_reference():
+    notes = _g8_notes(0)
+    toks = midi.encode(notes)
+    assert toks == G8["tokens_0"].tolist()
+    assert [(n.time_start, n.time_end) for n in notes] == [tuple(b) for b in G8["beats_0"].tolist()]
+
+
+def test_encode_large_batch_against_oracle():
+    """Many long songs (several 64-note steps, carries across steps) against
+    the oracle; then decode_batch of the encoded rows gives back the notes."""
+    rng = np.random.default_rng(11)
+    songs = []
+    for s in range(40):
+        n = int(rng.integers(1, 3000))
+        t = np.cumsum(rng.choice([0.0, 0.02, 0.3, 1.0], size=n))
+        tp = rng.integers(30, 240, size=n)
+        songs.append([midi.MIDI_note(pitch=int(rng.integers(0, 128)), time_start=float(t[k]),
+                                     time_end=float(t[k] + rng.random() * 2), dynamic=int(rng.integers(1, 128)),
+                                     channel=int(rng.integers(0, 128)), tempo=int(tp[k])) for k in range(n)])
+    toks, beats = midi.encode_batch(songs)
+    for s, notes in enumerate(songs):
+        rows = [[m.pitch, m.channel, m.dynamic, m.tempo, m.time_start, m.time_end] for m in notes]
+        np.testing.assert_array_equal(beats[s], np.array(omidi.adjust_note_time(rows)))
+        np.testing.assert_array_equal(toks[s], np.array(omidi.encode(rows, REAL.start)))
+    nb = midi.decode_batch(torch.from_numpy(toks[3]).cuda())
+    assert int(nb.count[0]) == len(songs[3])
+    np.testing.assert_array_equal(nb.pitch[0, :len(songs[3])].cpu().numpy(), [m.pitch for m in songs[3]])
+
+
+def test_extract_encode_from_smf_file(tmp_path):
+    """extract_midi over a file written by midiseq.smf: the notes come back
+    (parity of extraction vs pretty_midi is unpinned; the round trip is the
+    check), then preprocess_midi_files writes the token row."""
+    from midiseq import smf
+    rng = np.random.default_rng(3)
+    notes = []
+    t = 0.0
+    for k in range(250):
+        t += float(rng.choice([0.0, 0.25, 0.5]))
+        notes.append(midi.MIDI_note(pitch=int(rng.integers(30, 90)), time_start=t, time_end=t + 0.25,
+                                    dynamic=int(rng.integers(20, 120)), channel=int(rng.integers(0, 3)), tempo=120.0))
+    src = tmp_path / "midi" / "model" / "Mozart" / "song.mid"
+    src.parent.mkdir(parents=True)
+    smf.note_to_midi(notes, str(src))
+    back = midi.extract_midi(str(src))
+    assert len(back) == len(set(notes))
+    assert all(n.tempo == 120 for n in back)
+    out = midi.preprocess_midi_files(str(tmp_path / "midi"), str(tmp_path / "npy"))
+    assert len(out) == 1 and out[0].endswith("model/Mozart/song.npy")
+    row = np.load(out[0])
+    assert row.dtype == np.int64 and len(row) >= 4 * len(back)
