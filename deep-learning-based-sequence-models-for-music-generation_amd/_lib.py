@@ -39,6 +39,8 @@ SIGNATURES = {
     "msq_dropout_mask_words": (_i64, [_i64, _i64, _i64]),
     "msq_window_gather": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _p, _i64, _i64, _i, _p, _p]),
     "msq_midi_decode": (_i, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "msq_relattn_decode": (_i, [_i, _p, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
+                                _f, _p]),
     "msq_midi_encode": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _p, _i64, _p, _p, _p, _p, _p]),
     "msq_dropout_attn_mask": (_i, [_p, _p, _i64, _i64, _i64, _u32, _u32, _f, _p]),
     "msq_relattn_fwd_dropout": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64, _p, _p,

@@ -11,15 +11,24 @@ k's) and samples on the device by inverse CDF on a uniform per row (replacing
 torch.multinomial). The history stays on the device; the only per-step
 device->host traffic is the B last tokens needed for the host-side k choice.
 
-Cached mode (``mode="cached"``, Mamba only): while the
-window still holds the whole history (prompt + generated <= context_len) every
-Mamba2 mixer is causal and the final LayerNorm / head are per position, so the
-logits of the new last row equal one recurrent step from the mixer states
-after the previous row, and the time-axis log-softmax of filtered_logit only
-needs a running per-vocabulary LSE. The prompt is prefilled by one full
-forward (which also leaves the states); each later step is one
-``MambaEngine.step``. Once the window starts to slide the loop falls back to
-the exact full forward per step.
+Cached mode (``mode="cached"``):
+* Mamba: while the window still holds the whole
+  history (prompt + generated <= context_len) every Mamba2 mixer is causal and
+  the final LayerNorm / head are per position, so the logits of the new last
+  row equal one recurrent step from the mixer states after the previous row,
+  and the time-axis log-softmax of filtered_logit only needs a running
+  per-vocabulary LSE. The prompt is prefilled by one full forward (which also
+  leaves the states); each later step is one ``MambaEngine.step``. EXACT; once
+  the window starts to slide the loop falls back to the exact full forward.
+* Transformer (BASELINE cfg 5 "KV-cache AR decode"): a documented
+  APPROXIMATION (the model is length-anchored). The prompt
+  window is prefilled exactly (its first sampled token equals the exact
+  mode's); every later token is computed once, as the last row of its own
+  window (skew term q . R[j], j = the key's window position), against the
+  cached keys / values of the window, which then slides over a ring of
+  ``context_len`` tokens; filtered_logit's time-axis LSE runs over the
+  window's cached logits rows. oracle/transformer.py CachedTransformer
+  restates these semantics; tests/test_decode_cached_gpu.py pins the build to it.
 """
 import random as _random
 
@@ -76,23 +85,22 @@ def generate(model, context_len, token_ids, meta_ids, num_tokens=1000, device="c
     if mode not in ("exact", "cached"):
         raise ValueError(f"mode must be 'exact' or 'cached', not {mode!r}")
     cached = mode == "cached"
-    if cached and not hasattr(eng, "step"):
-        raise ValueError("cached decode needs a recurrent model (Mamba); the Transformer is length-anchored")
+    slides = cached and getattr(eng, "cache_slides", False)  # Transformer: stays cached past the context
     cache = None
     ldz = (V + 3) // 4 * 4
     z = torch.empty(B, 1, ldz, device=dev, dtype=torch.float32)
     for step in range(num_tokens):
         cur = T0 + step
         W = min(cur, context_len)
-        if cached and cache is not None and cur <= context_len:
+        if cached and cache is not None and (cur <= context_len or slides):
             # one recurrent position: the token sampled last step (out_tok) at row cur-1
             logits = eng.step(out_tok, cache)
             call("msq_filtered_logit_step", ptr(z), ldz, ptr(cache.lse), ptr(logits), dt(logits), cfg.v_pad,
                  ptr(out_tok), ptr(wtab), b[0], b[1], b[2], b[3], B, V, stream())
         else:
             window = hist[:, cur - W:cur].contiguous()
-            if cached and cur <= context_len:  # prefill: the whole prompt, states left in the cache
-                cache = eng.decode_cache(B)
+            if cached and cache is None and (cur <= context_len or slides):  # prefill, states left in the cache
+                cache = eng.decode_cache(B, context_len) if slides else eng.decode_cache(B)
                 logits = eng.forward(window, meta_ids, save=False, cache=cache)
                 col_lse = cache.lse
             else:

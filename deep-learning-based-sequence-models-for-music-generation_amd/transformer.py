@@ -22,6 +22,7 @@ import torch.nn as nn
 
 from . import _lib as L
 from . import ops
+from ._lib import ptr, call, stream, dt
 from .attention import relattn_fwd, relattn_bwd
 from .config import N_META, VOCAB_SIZE, METADATA_VOCAB_SIZE, BLOCK_LEN, DROPOUT
 
@@ -196,8 +197,42 @@ class _Acts:
         return self._bwd
 
 
+class TransformerDecodeCache:
+    """State of the cached decode (generate(mode="cached"); an approximation of
+    scripts/generate.py:26-31, see msq_relattn_decode and oracle/transformer.py
+    CachedTransformer) for B rows and a window of ``context`` tokens:
+    per layer the keys / values of the window (act dtype [L, B, H, 6 + context,
+    hs], a ring: metadata in slots 0..5, sequence position p in slot
+    6 + p % context), the window's logits rows (a ring [B, context, v_pad],
+    empty rows -inf so they drop out of the time-axis LSE) and tokens, and the
+    one-position step buffers."""
+
+    slides = True  # keeps stepping once the window is full (the Mamba cache does not)
+
+    def __init__(self, cfg, B, context, device, act):
+        d, H, hs = cfg.n_embd, cfg.n_heads, cfg.head_size
+        if context + N_META > cfg.s_max:
+            raise ValueError(f"context {context} exceeds block_len {cfg.block_len}")
+        f32 = torch.float32
+        e = lambda *s, dt=act: torch.empty(*s, device=device, dtype=dt)  # noqa: E731
+        self.B, self.ctx, self.S_ring = B, context, context + N_META
+        self.k = torch.zeros(cfg.n_layer, B, H, self.S_ring, hs, device=device, dtype=act)
+        self.v = torch.zeros_like(self.k)
+        self.ring = torch.full((B, context, cfg.v_pad), float("-inf"), device=device, dtype=act)
+        self.tokens = torch.zeros(B, context, device=device, dtype=torch.int64)
+        self.lse = e(B, cfg.vocab_size, dt=f32)
+        self.x, self.xm = e(B, d, dt=f32), e(B, d, dt=f32)
+        self.a, self.c, self.o, self.f = e(B, d), e(B, d), e(B, d), e(B, d)
+        self.qkv, self.h = e(B, 3 * d), e(B, 4 * d)
+        self.st, self.stf = e(2, B, dt=f32), e(2, B, dt=f32)
+        self.logits = e(B, cfg.v_pad)
+        self.length = 0  # tokens absorbed (sequence positions 0 .. length-1)
+
+
 class TransformerEngine:
     """Explicit forward / backward over the libmidiseq kernels."""
+
+    cache_slides = True  # generate(mode="cached") keeps stepping once the window slides
 
     def __init__(self, cfg: TransformerConfig, flat: torch.Tensor):
         if not 0.0 <= cfg.dropout < 1.0:
@@ -239,12 +274,15 @@ class TransformerEngine:
         return self._acts[key]
 
     # ------------------------------------------------------------- forward
-    def forward(self, idx, meta, save=True, train=False, seed=None):
+    def forward(self, idx, meta, save=True, train=False, seed=None, cache=None):
         """save=False (inference): one layer's activation buffers are reused
         and nothing is kept for a backward pass. train=True (nn.Module.train()
         mode, save=True only) applies nn.Dropout(cfg.dropout) at the reference's
         three sites (model_transformer.py:51,80,101) with keep masks drawn from
-        `seed` (default: one draw of torch's CPU generator per step)."""
+        `seed` (default: one draw of torch's CPU generator per step).
+        cache (a TransformerDecodeCache, save=False): the cached decode's
+        prefill — every layer's keys / values, the logits rows and the tokens
+        of the window are left in it."""
         cfg, P, W = self.cfg, self.P, self.W
         if not idx.is_cuda:
             raise RuntimeError("the MI355X engine runs on the GPU only (no CPU fallback)")
@@ -274,6 +312,10 @@ class TransformerEngine:
             x, xo = (A.x[l], A.x[l + 1]) if save else (A.x[l % 2], A.x[(l + 1) % 2])
             ops.layernorm_fwd(x, P[f"{l}.ln1_w"], P[f"{l}.ln1_b"], out=A.a[k], mean=A.st1[k, 0], rstd=A.st1[k, 1])
             ops.gemm(A.a[k], W[f"{l}.wqkv"], out=A.qkv[k])
+            if cache is not None:
+                kv = A.qkv[k].view(B, S, 3, H, hs)
+                cache.k[l][:, :, :S].copy_(kv[:, :, 1].transpose(1, 2))
+                cache.v[l][:, :, :S].copy_(kv[:, :, 2].transpose(1, 2))
             adrop = pdrop = fdrop = None
             if p > 0:
                 ops.dropout_attn_mask(B, H, S, seed, DROP_ATTN + l * 65536, p, self.device, out=masks[k])
@@ -292,7 +334,62 @@ class TransformerEngine:
         V = cfg.vocab_size
         # full V_pad rows (pad rows of lm_w / lm_b are zero): 16-B aligned rows, 256-tile eligible
         ops.gemm(A.f, W["lm_w"], out=A.logits, epilogue=L.EPI_BIAS, bias=P["lm_b"])
+        if cache is not None:
+            if T > cache.ctx:
+                raise ValueError(f"prefill of {T} tokens exceeds the cache context {cache.ctx}")
+            cache.ring.fill_(float("-inf"))
+            cache.ring[:, :T].copy_(A.logits.view(B, T, cfg.v_pad))
+            cache.tokens[:, :T].copy_(idx)
+            cache.length = T
         return A.logits.view(B, T, cfg.v_pad)[:, :, :V]
+
+    def decode_cache(self, B, context=None):
+        return TransformerDecodeCache(self.cfg, B, context or self.cfg.block_len, self.device, self.act)
+
+    @torch.no_grad()
+    def step(self, tok, cache):
+        """One cached decode position for every row: tok int64 [B] (the token
+        at sequence position cache.length) -> its logits row [B, v_pad] (the
+        last row of its window, keys / values of the window from the cache).
+        Leaves cache.lse = the time-axis LSE of the window's OTHER rows (what
+        msq_filtered_logit_step then extends by this row) and writes the row
+        into the window's logits ring."""
+        cfg, P, W = self.cfg, self.P, self.W
+        if not tok.is_cuda:
+            raise RuntimeError("the MI355X engine runs on the GPU only (no CPU fallback)")
+        self.refresh_shadow()
+        B, d, H, hs = cache.B, cfg.n_embd, cfg.n_heads, cfg.head_size
+        ctx, pos = cache.ctx, cache.length
+        n_tok = min(pos + 1, ctx)
+        first = pos + 1 - n_tok
+        slot = pos % ctx
+        s = stream()
+        scale = d ** -0.5
+        tok = tok.contiguous()
+        call("msq_embed_fwd", ptr(cache.x), ptr(P["tok_emb"]), ptr(P["meta_emb"]), ptr(tok), None, B, 1, 0, d, s)
+        x = cache.x
+        for l in range(cfg.n_layer):
+            ops.layernorm_fwd(x, P[f"{l}.ln1_w"], P[f"{l}.ln1_b"], out=cache.a, mean=cache.st[0], rstd=cache.st[1])
+            ops.gemm(cache.a, W[f"{l}.wqkv"], out=cache.qkv)
+            call("msq_relattn_decode", dt(cache.qkv), ptr(cache.o), cache.o.stride(0), ptr(cache.qkv),
+                 cache.qkv.stride(0), ptr(cache.k[l]), ptr(cache.v[l]), ptr(W[f"{l}.R"]), cfg.s_max, B, H, hs,
+                 cache.S_ring, N_META, n_tok, N_META + slot, first % ctx, float(scale), s)
+            ops.gemm(cache.o, W[f"{l}.wproj"], out=cache.xm, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.bproj"], aux=x)
+            ops.layernorm_fwd(cache.xm, P[f"{l}.ln2_w"], P[f"{l}.ln2_b"], out=cache.c, mean=cache.st[0],
+                              rstd=cache.st[1])
+            ops.gemm(cache.c, W[f"{l}.w1"], out=cache.h, epilogue=L.EPI_BIAS_RELU, bias=P[f"{l}.b1"])
+            ops.gemm(cache.h, W[f"{l}.w2"], out=x, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.b2"], aux=cache.xm)
+        ops.layernorm_fwd(x, P["lnf_w"], P["lnf_b"], out=cache.f, mean=cache.stf[0], rstd=cache.stf[1])
+        ops.gemm(cache.f, W["lm_w"], out=cache.logits, epilogue=L.EPI_BIAS, bias=P["lm_b"])
+        # the row leaving the window (or the empty slot) drops out of the LSE
+        cache.ring[:, slot].fill_(float("-inf"))
+        V = cfg.vocab_size
+        ws = ops.workspace(L.lib().msq_filtered_workspace(B, ctx, V), self.device, "loss")
+        call("msq_filtered_colstats", ptr(cache.lse), ptr(cache.ring), dt(cache.ring), cfg.v_pad, B, ctx, V, ptr(ws), s)
+        cache.ring[:, slot].copy_(cache.logits)
+        cache.tokens[:, slot].copy_(tok)
+        cache.length = pos + 1
+        return cache.logits
 
     # ------------------------------------------------------------ backward
     def backward(self, dlogits, grads):

@@ -293,6 +293,23 @@ int msq_midi_decode(const int64_t* rows, int64_t B, int64_t L, int64_t ld, const
                     int64_t cap, int32_t* pitch, int32_t* channel, int32_t* dyn, int32_t* tempo, int64_t* beat_start,
                     int64_t* beat_end, double* t_start, double* t_end, int64_t* count, void* stream);
 
+/* Cached decode step of the relative attention (the Transformer's
+ * generate(mode="cached"), an approximation of scripts/generate.py:26-31's
+ * full forward per token: every row is computed once, as the last row of its
+ * own window, and its keys / values are reused). For each (b, h): the new
+ * token's q, k, v are the head's columns of qkv[b] (bf16 [B, ldq], q | k | v);
+ * k, v are written to cache slot new_slot, then
+ *   out[b, h] = softmax_j((q.k_j + q.R[jw(j)]) * scale) . v_j
+ * over the window's slots j < n_meta + n_tok of kcache / vcache (bf16
+ * [B, H, S_ring, hs]); jw(j) = j for metadata slots, else
+ * n_meta + (j - n_meta - first_mod) mod (S_ring - n_meta) (the key's window
+ * position: HeadRelPos's skew R[S-1-i+j] at the last row i = S-1). R bf16
+ * [H, S_max, hs] (rel_pos_emb of the layer). 8 | hs <= 128; dtype MSQ_BF16 or
+ * MSQ_F32 for every tensor (out [B, ldo] too).                              */
+int msq_relattn_decode(int dtype, void* out, int64_t ldo, const void* qkv, int64_t ldq, void* kcache, void* vcache, const void* R,
+                       int64_t S_max, int64_t B, int64_t H, int64_t hs, int64_t S_ring, int64_t n_meta, int64_t n_tok,
+                       int64_t new_slot, int64_t first_mod, float scale, void* stream);
+
 /* Note -> token encode of a batch of songs (replaces processing/processing.py
  * :129-152 encode + :111-126 adjust_note_time, the preprocessing step of
  * preprocess_midi_files :24-55). Song s = notes [song_off[s], song_off[s+1])

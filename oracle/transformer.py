@@ -141,3 +141,96 @@ def n_flops_fwd_per_seq(n_embd, n_layer, S, V):
 
 
 __all__ = ["forward", "param_shapes", "filled_params", "allowed_mask", "skew_index", "math"]
+
+
+class CachedTransformer:
+    """TEST INFRASTRUCTURE: the semantics of the build's cached Transformer
+    decode (generate(mode="cached")), an APPROXIMATION of scripts/generate.py's
+    full forward per token that the reference itself does not have:
+
+    * the prompt window is prefilled by the exact forward (model_transformer.py
+      :149-165); its per-layer keys / values and logits rows are kept;
+    * every later token is computed ONCE, as the last row of its own window:
+      for the last row i = S-1 the skew term q_i . R[S-1-i+j] is q . R[j]
+      (j = the key's position in the window, metadata 0..5 first) and the row
+      sees every key; its keys / values / logits row are then reused;
+    * the window holds at most ``context`` tokens: the oldest token's keys /
+      values / logits row leave it (metadata stays).
+
+    Called like a model on the sampler's growing window (oracle/sampler.py
+    generate): returns the cached logits rows of the window, so
+    filtered_logit(window, rows)[:, -1] is the cached z."""
+
+    def __init__(self, p, n_layer, n_heads, context):
+        self.p, self.L, self.H, self.ctx = p, n_layer, n_heads, context
+        self.kv = None
+
+    def _prefill(self, idx, meta):
+        p, H = self.p, self.H
+        B, T = idx.shape
+        x = torch.cat([p["metadata_embedding_table.weight"][meta], p["token_embedding_table.weight"][idx]], dim=1)
+        C = x.shape[-1]
+        scale = C ** -0.5
+        self.kv = []
+        for l in range(self.L):
+            pre = f"blocks.{l}."
+            h = F.layer_norm(x, (C,), p[pre + "ln1.weight"], p[pre + "ln1.bias"], 1e-5)
+            heads, ks, vs = [], [], []
+            for hh in range(H):
+                hp = f"{pre}sa.heads.{hh}."
+                q, k, v = h @ p[hp + "query.weight"].t(), h @ p[hp + "key.weight"].t(), h @ p[hp + "value.weight"].t()
+                ks.append(k)
+                vs.append(v)
+                heads.append(rel_attention(q, k, v, p[hp + "rel_pos_emb"], scale))
+            self.kv.append((torch.stack(ks, 1), torch.stack(vs, 1)))  # [B, H, S, hs]
+            x = x + F.linear(torch.cat(heads, -1), p[pre + "sa.proj.weight"], p[pre + "sa.proj.bias"])
+            h = F.layer_norm(x, (C,), p[pre + "ln2.weight"], p[pre + "ln2.bias"], 1e-5)
+            h = torch.relu(F.linear(h, p[pre + "ffwd.net.0.weight"], p[pre + "ffwd.net.0.bias"]))
+            x = x + F.linear(h, p[pre + "ffwd.net.2.weight"], p[pre + "ffwd.net.2.bias"])
+        x = F.layer_norm(x, (C,), p["ln_f.weight"], p["ln_f.bias"], 1e-5)
+        self.rows = F.linear(x, p["lm_head.weight"], p["lm_head.bias"])[:, -T:, :]
+        self.meta = meta
+
+    def _step(self, tok):
+        p, H = self.p, self.H
+        x = p["token_embedding_table.weight"][tok]  # [B, C]
+        C = x.shape[-1]
+        scale = C ** -0.5
+        for l in range(self.L):
+            pre = f"blocks.{l}."
+            h = F.layer_norm(x, (C,), p[pre + "ln1.weight"], p[pre + "ln1.bias"], 1e-5)
+            K, Vv = self.kv[l]
+            nk, nv, heads = [], [], []
+            for hh in range(H):
+                hp = f"{pre}sa.heads.{hh}."
+                q, k, v = h @ p[hp + "query.weight"].t(), h @ p[hp + "key.weight"].t(), h @ p[hp + "value.weight"].t()
+                Kh = torch.cat([K[:, hh], k[:, None]], 1)      # [B, S, hs], window order
+                Vh = torch.cat([Vv[:, hh], v[:, None]], 1)
+                S = Kh.shape[1]
+                s = (torch.einsum("bd,bjd->bj", q, Kh) + q @ p[hp + "rel_pos_emb"][:S].t()) * scale
+                heads.append(torch.einsum("bj,bjd->bd", torch.softmax(s, -1), Vh))
+                nk.append(k)
+                nv.append(v)
+            self.kv[l] = (torch.cat([K, torch.stack(nk, 1)[:, :, None]], 2), torch.cat([Vv, torch.stack(nv, 1)[:, :, None]], 2))
+            x = x + F.linear(torch.cat(heads, -1), p[pre + "sa.proj.weight"], p[pre + "sa.proj.bias"])
+            h = F.layer_norm(x, (C,), p[pre + "ln2.weight"], p[pre + "ln2.bias"], 1e-5)
+            h = torch.relu(F.linear(h, p[pre + "ffwd.net.0.weight"], p[pre + "ffwd.net.0.bias"]))
+            x = x + F.linear(h, p[pre + "ffwd.net.2.weight"], p[pre + "ffwd.net.2.bias"])
+        x = F.layer_norm(x, (C,), p["ln_f.weight"], p["ln_f.bias"], 1e-5)
+        self.rows = torch.cat([self.rows, F.linear(x, p["lm_head.weight"], p["lm_head.bias"])[:, None]], 1)
+
+    def _slide(self):
+        n_meta = self.meta.shape[1]
+        while self.rows.shape[1] > self.ctx:
+            self.rows = self.rows[:, 1:]
+            self.kv = [(torch.cat([K[:, :, :n_meta], K[:, :, n_meta + 1:]], 2),
+                        torch.cat([V[:, :, :n_meta], V[:, :, n_meta + 1:]], 2)) for K, V in self.kv]
+
+    def __call__(self, window, meta):
+        if self.kv is None:
+            self._prefill(window, meta)
+        else:
+            self._step(window[:, -1])
+            self._slide()
+        assert self.rows.shape[1] == window.shape[1]
+        return self.rows
