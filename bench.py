@@ -54,19 +54,6 @@ from midiseq.train_parallel import TrainStep, SyntheticMIDI, setup_distributed  
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 METRIC = "MIDI tokens/sec/GPU (train, seq_len=2048) + AR decode tokens/sec at 1/2/4/8 GPU"
-# HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC
-# passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, KB -> bytes)
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1", "pmc_ffn1_traffic.json")
-
-
-def pmc_traffic():
-    try:
-        with open(PMC_TRAFFIC) as f:
-            return int(json.load(f)["hbm_bytes_per_launch"])
-    except (OSError, KeyError, ValueError):
-        return None
-
-
 def flops_per_token(cfg, T):
     """Algorithmic training FLOPs per MIDI token (SURVEY.md §8(d) cfg 2):
     3 x forward; forward = L (24 S d^2 + 3 d S (S+1)) + 2 T d V per sequence."""
@@ -75,63 +62,151 @@ def flops_per_token(cfg, T):
     return 3.0 * fwd / T
 
 
-class OpTimer:
-    """HIP events around one named op inside the timed region (on the stream
-    it is launched on)."""
-
-    def __init__(self, name):
-        self.name, self.pairs, self.on = name, [], False
-
-    def wrap(self, fn):
-        def inner(*a, **k):
-            if not self.on:
-                return fn(*a, **k)
-            s = torch.cuda.Event(enable_timing=True)
-            e = torch.cuda.Event(enable_timing=True)
-            s.record()
-            r = fn(*a, **k)
-            e.record()
-            self.pairs.append((s, e))
-            return r
-        return inner
-
-    def avg_ms(self):
-        ts = [s.elapsed_time(e) for s, e in self.pairs]
-        return sum(ts) / max(1, len(ts)), len(ts)
+def _gemm_class(a):
+    """msq_gemm / msq_gemm_ex / msq_gemm_dropout args -> (class, FLOPs)."""
+    ta, tb, M, N, K, batch, epi = a[1], a[2], a[3], a[4], a[5], a[16], a[17]
+    cls = "gemm_dW" if epi == L.EPI_ACCUM else ("gemm_dX" if (tb and not ta) else "gemm_fwd")
+    return cls, 2.0 * M * N * K * batch, None
 
 
-def cpu_baseline(seconds_budget=20.0):
-    """The CPU oracle (plain PyTorch fp32 restatement of the reference, the
-    'port') timed on this host: default model, B=1, T=2048, full train step
-    (forward, filtered CE, backward, Adam)."""
+def _attn_flops(B, S, H, hs):
+    """QK^T, q.R^T and PV over the causal triangle (SURVEY.md §8(d) cfg 2)."""
+    return 3 * 2.0 * hs * S * (S + 1) / 2 * B * H
+
+
+CLASSIFY = {
+    "msq_gemm": _gemm_class, "msq_gemm_ex": _gemm_class, "msq_gemm_dropout": _gemm_class,
+    "msq_relattn_fwd_dropout": lambda a: ("attn_fwd", _attn_flops(a[7], a[8], a[9], a[10]), None),
+    # backward = 2 x the forward's products (algorithmic; the recompute of P is not counted)
+    "msq_relattn_bwd_dropout": lambda a: ("attn_bwd", 2 * _attn_flops(a[11], a[12], a[13], a[14]), None),
+    # filtered CE: 3 reads of the logits + 1 write of dlogits ([B, T, ld] of the act dtype)
+    "msq_filtered_ce": lambda a: ("loss", None, 4.0 * a[13] * a[14] * a[5] * (2 if a[4] == L.BF16 else 4)),
+    "msq_layernorm_fwd": lambda a: ("layernorm", None, None),
+    "msq_layernorm_bwd": lambda a: ("layernorm", None, None),
+    "msq_layernorm_bwd_dropout": lambda a: ("layernorm", None, None),
+    "msq_colsum": lambda a: ("colsum", None, None),
+    # 4 fp32 reads (p, g, m, v) + 3 fp32 writes + 1 bf16 shadow write per parameter
+    "msq_adam_step": lambda a: ("adam", None, 30.0 * a[5]),
+    "msq_dropout_attn_mask": lambda a: ("dropout_mask", None, None),
+    "msq_embed_fwd": lambda a: ("embed", None, None), "msq_embed_bwd": lambda a: ("embed", None, None),
+    # SSD scan (SURVEY.md §8(d) cfg 3): bf16 x, B, C, dt in + y out = 8 512 B per token per layer (d_inner 2048)
+    "msq_mamba_ssd_fwd_state": lambda a: ("ssd_fwd", None, (4 * a[14] + 4 * 64 + 2 * a[15]) * float(a[12] * a[13])),
+    "msq_mamba_ssd_bwd": lambda a: ("ssd_bwd", None, None),
+    "msq_mamba_conv_fwd": lambda a: ("mamba_conv", None, None), "msq_mamba_conv_bwd": lambda a: ("mamba_conv", None, None),
+    "msq_mamba_gnorm_fwd": lambda a: ("mamba_gnorm", None, None),
+    "msq_mamba_gnorm_bwd": lambda a: ("mamba_gnorm", None, None),
+}
+
+
+class ClassTimer:
+    """HIP events around every libmidiseq launch (midiseq._lib.TAP), recorded
+    on the stream the launch goes to (torch's current stream at the call:
+    the main stream, or the weight-gradient / side stream inside its
+    `with torch.cuda.stream(...)` block), grouped by kernel class."""
+
+    def __init__(self):
+        self.rec, self.on = [], False
+
+    def __call__(self, name, args, launch):
+        if not self.on:
+            return launch()
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        r = launch()
+        e.record()
+        cls, flops, nbytes = CLASSIFY.get(name, lambda a: ("other:" + name[4:], None, None))(args)
+        self.rec.append((cls, flops, nbytes, s, e))
+        return r
+
+    def table(self, steps):
+        """{class: {launches_per_step, ms_per_step, avg_launch_ms, achieved, peak, unit, frac}}."""
+        agg = {}
+        for cls, flops, nbytes, s, e in self.rec:
+            a = agg.setdefault(cls, {"n": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0, "f": flops is not None,
+                                     "b": nbytes is not None})
+            a["n"] += 1
+            a["ms"] += s.elapsed_time(e)
+            a["flops"] += flops or 0.0
+            a["bytes"] += nbytes or 0.0
+        out = {}
+        for cls, a in sorted(agg.items(), key=lambda kv: -kv[1]["ms"]):
+            row = {"launches_per_step": round(a["n"] / steps, 2), "ms_per_step": round(a["ms"] / steps, 3),
+                   "avg_launch_ms": round(a["ms"] / a["n"], 4)}
+            if a["f"]:
+                ach = a["flops"] / (a["ms"] * 1e-3) / 1e12
+                row.update(bound="mfma", achieved=round(ach, 1), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
+                           frac=round(ach / PEAK_BF16_TFLOPS, 4), work_per_launch=a["flops"] / a["n"])
+            elif a["b"]:
+                ach = a["bytes"] / (a["ms"] * 1e-3) / 1e9
+                row.update(bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBS, unit="GB/s",
+                           frac=round(ach / PEAK_HBM_GBS, 4), work_per_launch=a["bytes"] / a["n"])
+            out[cls] = row
+        return out
+
+
+CALIB = os.path.join(ROOT, "profiles", "r2", "cpu_calibration.json")
+
+
+def _oracle_train_rate(hp, B, T, budget_s, max_steps):
+    """tokens/s of the oracle's fp32 train step (forward, filtered CE,
+    backward, Adam) on this host; one untimed warm-up step."""
     import numpy as np
     from oracle import loss as oloss, transformer as otr
     from oracle.fill import REAL, grammar_tokens
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    hp = dict(n_embd=1024, n_heads=8, n_layer=8, block_len=2048)
-    T = 2048
     shapes = otr.param_shapes(hp["n_embd"], hp["n_heads"], hp["n_layer"], hp["block_len"], REAL.size, 568)
     g = torch.Generator().manual_seed(0)
     p = {k: (torch.randn(s, generator=g) * 0.02).requires_grad_(True) for k, s in shapes.items()}
     opt = torch.optim.Adam(list(p.values()), lr=5e-5)
     rng = np.random.default_rng(0)
-    w = grammar_tokens(rng, REAL, T + 1)[None]
+    w = np.stack([grammar_tokens(rng, REAL, T + 1) for _ in range(B)])
     src, trg = torch.from_numpy(w[:, :-1].copy()), torch.from_numpy(w[:, 1:].copy())
-    meta = torch.tensor([[519, 279, 202, 202, 202, 178]])
-    steps, t0 = 0, time.time()
-    while True:
-        logits = otr.forward(p, src, meta, hp["n_layer"], hp["n_heads"])
-        loss = oloss.loss(src, trg, logits, REAL)
+    meta = torch.tensor([[519, 279, 202, 202, 202, 178]] * B)
+
+    def step():
+        loss = oloss.loss(src, trg, otr.forward(p, src, meta, hp["n_layer"], hp["n_heads"]), REAL)
         opt.zero_grad()
         loss.backward()
         opt.step()
+    step()
+    steps, t0 = 0, time.time()
+    while True:
+        step()
         steps += 1
-        if time.time() - t0 > seconds_budget or steps >= 5:
+        if time.time() - t0 > budget_s or steps >= max_steps:
             break
-    dt = time.time() - t0
-    return {"value": round(steps * T / dt, 2), "unit": "MIDI tokens/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ fp32 train step (fwd+filtered CE+bwd+Adam), default model, B=1, T=2048, {steps} steps"}
+    return steps * B * T / (time.time() - t0), steps
+
+
+def cpu_baseline():
+    """The CPU oracle (plain PyTorch fp32 restatement of the reference's train
+    step, the 'port') timed on this host's cores: cfg 2's model at B=1
+    (headline) and cfg 1 (2 layers, d 128, T 256, B 2). The restatement-to-
+    reference ratio measured in the build container on the same cores for both
+    (tools/calibrate_cpu.py -> profiles/r2/cpu_calibration.json) gives the
+    reference-equivalent rate beside it."""
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    v2, n2 = _oracle_train_rate(dict(n_embd=1024, n_heads=8, n_layer=8, block_len=2048), 1, 2048, 15.0, 3)
+    v1, n1 = _oracle_train_rate(dict(n_embd=128, n_heads=8, n_layer=2, block_len=256), 2, 256, 5.0, 30)
+    out = {"value": round(v2, 2), "unit": "MIDI tokens/s", "cores": threads, "kind": "port",
+           "sample": f"oracle/ fp32 train step (fwd+filtered CE+bwd+Adam), default model, B=1, T=2048, {n2} steps",
+           "cfg1": {"value": round(v1, 1), "unit": "MIDI tokens/s",
+                    "sample": f"oracle/ fp32 train step, 2 layers d=128 h=8, B=2, T=256, {n1} steps"}}
+    try:
+        with open(CALIB) as f:
+            cal = json.load(f)
+        r1, r2 = cal["configs"]["cfg1"], cal["configs"]["cfg2_b1"]
+        out["calibration"] = {
+            "source": "profiles/r2/cpu_calibration.json (build container, same cores for both)",
+            "threads": cal["threads"], "oracle_over_reference_cfg1": r1["oracle_over_reference"],
+            "oracle_over_reference_cfg2": r2["oracle_over_reference"],
+            "reference_s_per_step_cfg1": r1["reference_s_per_step"], "reference_s_per_step_cfg2": r2["reference_s_per_step"],
+            "reference_equiv_value": round(v2 * r2["oracle_over_reference"], 2),
+            "reference_equiv_cfg1": round(v1 * r1["oracle_over_reference"], 1)}
+    except (OSError, KeyError, ValueError):
+        pass
+    return out
 
 
 def timed(fn, steps, warmup, world, dev):
@@ -240,17 +315,56 @@ def midi_decode_leg(dev, rank, world, B=64, L=4048, iters=50, cpu_rows=4):
     return out
 
 
-def mamba_leg(dev, rank, world, steps=3, B=8, T=4096):
+def decode_cached_leg(dev, rank, world, B=64, T=2048, K=32, steps=2):
+    """Config 5, cached mode (a documented approximation, midiseq/generate.py):
+    B=64 prompts of 2048 tokens per GPU (replicas), prefill = one exact
+    forward, then one cached step per new token (KV ring of the 2048-token
+    window, decode attention, skinny GEMMs, time-axis LSE over the window's
+    logits ring). Steady-state rate = K new tokens per row over
+    (prefill + K steps) - (prefill alone)."""
+    import random
+    from midiseq.generate import generate
+    m = Transformer(TransformerConfig(precision="bf16", dropout=0.0)).to(dev).eval()
+    src, _, meta = SyntheticMIDI(B, T, dev, rank, n_batches=1).batches[0]
+    run = lambda n: generate(m, T, src, meta, num_tokens=n, rng=random.Random(rank), device=dev,  # noqa: E731
+                             mode="cached", return_tensor=True)
+    el_pre = timed(lambda: run(1), steps, 1, world, dev)
+    el_all = timed(lambda: run(1 + K), steps, 1, world, dev)
+    del m
+    ms_step = (el_all - el_pre) / (steps * K) * 1e3
+    return {"value": round(world * B / (ms_step * 1e-3), 1), "unit": "new tokens/s",
+            "ms_per_token_step": round(ms_step, 3), "prefill_ms": round(el_pre / steps * 1e3, 2),
+            "config": {"workload": "cfg 5 Transformer cached decode (KV ring, approximation of the exact window)",
+                       "batch_per_gpu": B, "context": T, "new_tokens": K}}
+
+
+def mamba_leg(dev, rank, world, timer, steps=3, B=8, T=4096):
     """Config 3: models/mamba (d=1024, 10 Mamba2 layers) train step at
-    T=4096, B=8 per GPU, bf16."""
+    T=4096, B=8 per GPU, bf16; per-class table (SSD scan on HBM bytes)."""
     from midiseq.mamba import Mamba
     m = Mamba(precision="bf16").to(dev)
     st = TrainStep(m)
     data = iter(SyntheticMIDI(B, T, dev, rank, n_batches=2))
-    el = timed(lambda: st(*next(data)), steps, 1, world, dev)
+    for _ in range(1):
+        st(*next(data))
+    timer.rec.clear()
+    timer.on = True
+    el = timed(lambda: st(*next(data)), steps, 0, world, dev)
+    timer.on = False
+    table = timer.table(steps)
     del st, m
-    return {"value": round(world * B * T * steps / el, 1), "unit": "tokens/s", "ms_per_step": round(el / steps * 1e3, 3),
-            "config": {"workload": "cfg 3 Mamba train step (filtered CE + Adam)", "batch_per_gpu": B, "seq_len": T}}
+    tok_s = world * B * T * steps / el
+    fpt = 3.0 * 174e6  # SURVEY.md §8(d) cfg 3: 174 MFLOP per token forward
+    out = {"value": round(tok_s, 1), "unit": "tokens/s", "ms_per_step": round(el / steps * 1e3, 3),
+           "mfu": round(tok_s / world * fpt / 1e12 / PEAK_BF16_TFLOPS, 4), "classes": table,
+           "config": {"workload": "cfg 3 Mamba train step (filtered CE + Adam)", "batch_per_gpu": B, "seq_len": T}}
+    if "ssd_fwd" in table:
+        r = table["ssd_fwd"]
+        out["roofline"] = {"kernel": "SSD scan forward (msq_mamba_ssd_fwd_state: state + pass + out kernels)",
+                           "bound": "hbm", "achieved": r["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                           "frac": r["frac"], "traffic": None, "avg_launch_ms": r["avg_launch_ms"],
+                           "algorithmic_bytes": int(r["work_per_launch"])}
+    return out
 
 
 def main():
@@ -264,6 +378,8 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.01, help="configs/common/config.yaml values.dropout")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the decode and Mamba legs")
+    ap.add_argument("--serial", action="store_true",
+                    help="weight-gradient GEMMs on the main stream (per-class times then sum to the step)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU check of the launch: init gloo ranks, verify the world size, print, exit")
     args = ap.parse_args()
@@ -284,21 +400,12 @@ def main():
     torch.cuda.set_device(dev)
     cfg = TransformerConfig(n_layer=args.layers, block_len=args.seq, precision="bf16", dropout=args.dropout)
     model = Transformer(cfg).to(dev)
+    model.engine.overlap_dw = not args.serial
     step = TrainStep(model)
     data = iter(SyntheticMIDI(args.batch, args.seq, dev, rank))
 
-    # dominant kernel for the roofline: relative-attention backward pass A
-    # (flash_bwd_a) is timed through the op that launches it
-    timer = OpTimer("ffn1_gemm")
-    import midiseq.transformer as mt
-    orig_gemm = mt.ops.gemm
-
-    def gemm_tap(A, B, **kw):
-        if kw.get("epilogue") == L.EPI_BIAS_RELU:
-            return timer.wrap(orig_gemm)(A, B, **kw)
-        return orig_gemm(A, B, **kw)
-    mt.ops.gemm = gemm_tap
-
+    timer = ClassTimer()
+    L.TAP = timer
     for _ in range(args.warmup):
         step(*next(data))
     torch.cuda.synchronize()
@@ -323,21 +430,26 @@ def main():
     value = tokens / el
     ms_step = el / args.steps * 1e3
     fpt = flops_per_token(cfg, args.seq)
+    classes = timer.table(args.steps)
+    timer.rec.clear()
+    loss_last = round(float(loss.item()), 4)
 
-    ffn_ms, n_launch = timer.avg_ms()
     extra = {}
     if not args.no_extra:
         del step, model
         torch.cuda.empty_cache()
         extra["decode"] = decode_leg(dev, rank, world)
         torch.cuda.empty_cache()
-        extra["mamba_train"] = mamba_leg(dev, rank, world)
+        extra["decode_cached"] = decode_cached_leg(dev, rank, world)
+        torch.cuda.empty_cache()
+        extra["mamba_train"] = mamba_leg(dev, rank, world, timer)
         torch.cuda.empty_cache()
         extra["mamba_decode"] = mamba_decode_leg(dev, rank, world)
         extra["midi_decode"] = midi_decode_leg(dev, rank, world)
-    M = args.batch * (args.seq + 6)
-    ffn_flops = 2.0 * M * (4 * cfg.n_embd) * cfg.n_embd
-    achieved = ffn_flops / (ffn_ms * 1e-3) / 1e12 if ffn_ms > 0 else 0.0
+    L.TAP = None
+    # dominant kernel class of the train step: the largest summed time
+    dom = next(k for k in classes if "frac" in classes[k])
+    r = classes[dom]
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -353,17 +465,19 @@ def main():
             "dtype": "bf16",
             "data": "synthetic grammar-cycled MIDI tokens, random-init weights",
             "config": {"workload": "configs/transformer default (d=1024, h=8, L=8, V=17914) train step, "
-                                   f"filtered CE + Adam, dropout={args.dropout}",
+                                   f"filtered CE + Adam, dropout={args.dropout}"
+                                   + (", weight-gradient GEMMs serial" if args.serial else ""),
                        "model": "Transformer", "global_batch": args.batch * world, "seq_len": args.seq,
                        "parallelism": f"dp{world}"},
             "model_tflops": round(value * fpt / 1e12, 1),
             "mfu": round(value * fpt / 1e12 / (PEAK_BF16_TFLOPS * world), 4),
-            "loss_last": round(float(loss.item()), 4),
-            "roofline": {"kernel": "gemm_bf16 FFN1 (NT, bias+ReLU epilogue) 65728x4096x1024",
-                         "bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(),
-                         "algorithmic_bytes": int(2 * (M * cfg.n_embd + 4 * cfg.n_embd * cfg.n_embd + M * 4 * cfg.n_embd)),
-                         "avg_launch_ms": round(ffn_ms, 4), "launches": n_launch},
+            "loss_last": loss_last,
+            "roofline": {"kernel": f"{dom} (dominant class of the train step: {r['ms_per_step']} ms/step, "
+                                   f"{r['launches_per_step']} launches/step)",
+                         "bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"],
+                         "frac": r["frac"], "traffic": None, "avg_launch_ms": r["avg_launch_ms"],
+                         "algorithmic_work_per_launch": r["work_per_launch"]},
+            "classes": classes,
         }
         out.update(extra)
         if world == 1 and not args.no_cpu_baseline:

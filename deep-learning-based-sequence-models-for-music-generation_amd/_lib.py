@@ -97,7 +97,18 @@ def lib():
     return _lib
 
 
+# optional launch observer (bench.py's per-class HIP-event timing):
+# TAP(name, args, launch) must call launch() and return its result
+TAP = None
+
+
 def call(name, *args):
+    if TAP is not None:
+        return TAP(name, args, lambda: _call(name, args))
+    return _call(name, args)
+
+
+def _call(name, args):
     rc = getattr(lib(), name)(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed ({rc}): {lib().msq_last_error().decode()}")

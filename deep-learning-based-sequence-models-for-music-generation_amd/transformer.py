@@ -414,7 +414,7 @@ class TransformerEngine:
         # side launch waits for the main stream's producer of its inputs; the
         # main stream waits for the side stream before it overwrites a buffer
         # the side still reads (gb / gb2 / dh / dqkv, one layer of slack).
-        ov = Bw["gb2"] is not None
+        ov = Bw["gb2"] is not None and getattr(self, "overlap_dw", True)
         main = torch.cuda.current_stream(self.device)
         if ov and getattr(self, "_dw_stream", None) is None:
             self._dw_stream = torch.cuda.Stream(device=self.device)
