@@ -73,9 +73,13 @@ __global__ __launch_bounds__(NT) void colstats_part_kernel(LossArgs a, float* __
         const f32x4 x = ld4(o + t * a.ld, v, a.V);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+            // -inf rows (the cached decode's empty / leaving ring slots) add
+            // nothing; skipping them also keeps -inf - -inf out of the sum
             const float mn = fmaxf(m[i], x[i]);
-            s[i] = s[i] * expf(m[i] - mn) + expf(x[i] - mn);
-            m[i] = mn;
+            if (mn != -INFINITY) {
+                s[i] = s[i] * expf(m[i] - mn) + expf(x[i] - mn);
+                m[i] = mn;
+            }
         }
     }
     float* pm = part + ((b * TSPLIT + ts) * 2) * a.V;

@@ -118,7 +118,9 @@ __global__ __launch_bounds__(NT) void sample_kernel(int64_t* __restrict__ hist, 
             c += f[q].v / sum;
             if (c > u) { pick = q; break; }
         }
-        const int64_t tok = f[pick].i;
+        // no finite candidate (NaN / -inf row): the reference's
+        // torch.multinomial would raise; never emit an out-of-range id
+        const int64_t tok = f[pick].i < V ? f[pick].i : 0;
         h[cur_len] = tok;
         out_tok[b] = tok;
     }

@@ -219,9 +219,10 @@ class CachedTransformer:
         x = F.layer_norm(x, (C,), p["ln_f.weight"], p["ln_f.bias"], 1e-5)
         self.rows = torch.cat([self.rows, F.linear(x, p["lm_head.weight"], p["lm_head.bias"])[:, None]], 1)
 
-    def _slide(self):
+    def _slide(self, keep):
+        """drop the oldest tokens until ``keep`` remain (metadata stays)"""
         n_meta = self.meta.shape[1]
-        while self.rows.shape[1] > self.ctx:
+        while self.rows.shape[1] > keep:
             self.rows = self.rows[:, 1:]
             self.kv = [(torch.cat([K[:, :, :n_meta], K[:, :, n_meta + 1:]], 2),
                         torch.cat([V[:, :, :n_meta], V[:, :, n_meta + 1:]], 2)) for K, V in self.kv]
@@ -229,8 +230,8 @@ class CachedTransformer:
     def __call__(self, window, meta):
         if self.kv is None:
             self._prefill(window, meta)
-        else:
+        else:  # the new token's window holds at most ctx tokens, itself included
+            self._slide(self.ctx - 1)
             self._step(window[:, -1])
-            self._slide()
         assert self.rows.shape[1] == window.shape[1]
         return self.rows
