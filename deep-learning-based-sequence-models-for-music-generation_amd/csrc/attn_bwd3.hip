@@ -24,7 +24,11 @@ constexpr int KB = 128, QT = 32, NCH = 6, SCR = 36;
 constexpr int O_Q = 0, O_O = 2 * QT * 256, O_L = 4 * QT * 256, O_R = O_L + 2 * 2 * 64 * 4;
 constexpr int O_S = O_R + NCH * 32 * 256, O_M = O_S + 8 * 2 * 16 * SCR * 4;
 constexpr int O_D = O_M + 64 * 4;  // dropout keep words of the block's 128 keys, 2 tiles
-constexpr int LDS_BYTES = O_D + 2 * KB * 4;
+// dS staging for the coalesced stores: 2 tiles x 32 query rows x 128 keys, rows
+// 288 B apart (the four rows one wave writes at a time fall on disjoint banks)
+constexpr int T_PITCH = 288, T_BYTES = QT * T_PITCH;
+constexpr int O_T = O_D + 2 * KB * 4;
+constexpr int LDS_BYTES = O_T + 2 * T_BYTES;
 constexpr uint32_t OOB = 0xFFFF0000u;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
@@ -51,7 +55,9 @@ __device__ __forceinline__ int sw_dual(int row) { return ((row & 3) << 2) | ((ro
 // DROP: attention-probability dropout (model_transformer.py:80); the keep word
 // (key, query tile) of colmask is staged with the tile: dV uses P keep/(1-p),
 // dS = P (dP keep/(1-p) - D) scale
-template <bool DROP>
+// LAB: ablation switches for tools/lab (0 in the library): 1 no dS stores,
+// 2 no MFMA, 4 no skew / softmax, 16 no DMA in the loop
+template <bool DROP, int LAB = 0>
 __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const float* __restrict__ lse,
                                                               const float* __restrict__ Dv,
                                                               const bf16* __restrict__ dout, int64_t ldo,
@@ -170,34 +176,43 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const 
 #pragma unroll
     for (int c = 0; c < NCH - 1; ++c) stage_r(c);
 
-    // dS of a tile is stored at the top of the NEXT iteration, before that
-    // iteration's prefetch: the vmcnt(0) that waits for a tile's DMA then never
-    // waits for fresh stores
-    bf16x8 ds_prev = (bf16x8){};
+    // dS of a tile (j <= i, else 0) is staged in LDS and stored in the NEXT
+    // iteration, right AFTER that iteration's prefetch, as whole rows: thread t
+    // writes 8 keys of query row t/16, once j-indexed (dSj, aligned 16-B
+    // chunks of 256-B row runs) and once r-indexed (dQR, r = S-1-i+j: the
+    // row's 128 values start 2-byte aligned, stored as unaligned 16-B chunks;
+    // entries j > i land at r >= S, in the row padding (ldr >= S + 128) that no
+    // reader touches). The 2 stores per thread are then the youngest vector
+    // memory ops at the following tile's wait (vmcnt(2) leaves them in flight);
+    // invalid rows use the out-of-range offset, so the count is exact.
     int i0_prev = -1;
-    // dS twice: r-indexed (dQR, j <= i only) for the R products and j-indexed
-    // (dSj, 0 for j > i) for dq's K product (attn_dq.hip)
-    auto store_ds = [&](const bf16x8& v, int ip) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int i = ip + 16 * (e >> 2) + 4 * g + (e & 3);
-            if (i < S && jk < S) {
-                if (jk <= i) qr_rows[(int64_t)i * ldr + (S - 1 - i + jk)] = v[e];
-                sj_rows[(int64_t)i * ldr + jk] = jk <= i ? v[e] : (bf16)0.f;
-            }
-        }
+    const __amdgpu_buffer_rsrc_t rqr = make_rsrc(qr_rows, (uint32_t)min<int64_t>((int64_t)S * ldr * 2, OOB - 1));
+    const __amdgpu_buffer_rsrc_t rsj = make_rsrc(sj_rows, (uint32_t)min<int64_t>((int64_t)S * ldr * 2, OOB - 1));
+    auto store_ds = [&](int ip, int sbuf) {
+        const int row = tid >> 4, ch = tid & 15;
+        const u32x4 v = *(const u32x4*)(smem + O_T + sbuf * T_BYTES + row * T_PITCH + ch * 16);
+        const int i = ip + row, j = j0 + 8 * ch;
+        const bool in = i < S;
+        const uint32_t os = in ? (uint32_t)(((int64_t)i * ldr + j) * 2) : OOB;
+        const uint32_t oq = in ? (uint32_t)(((int64_t)i * ldr + (S - 1 - i + j)) * 2) : OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(v, rsj, os, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rqr, oq, 0, 0);
     };
 
     for (int t = 0; t < nqt; ++t) {
         const int i0 = it0 + QT * t, buf = t & 1;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        bar();  // tile t landed everywhere; tile t-1's buffers are free
-        if (i0_prev >= 0) store_ds(ds_prev, i0_prev);
-        if (t + 1 < nqt) {
+        // tile t's DMA (issued in iteration t-1, or the prologue) is older than
+        // the 2 dS stores of iteration t-1 (present from t = 2 on)
+        if (t >= 2 && !(LAB & 1)) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();  // tile t landed everywhere; tile t-1's buffers (and dS staging) are free / published
+        if (t + 1 < nqt && !(LAB & 16)) {
             stage_q(t + 1);
             stage_r(t + NCH - 1);
             stage_m(t + 1);
         }
+        asm volatile("" ::: "memory");
+        if (i0_prev >= 0 && !(LAB & 1)) store_ds(i0_prev, buf ^ 1);
         const char* cQ = smem + O_Q + buf * QT * 256;
         const char* cO = smem + O_O + buf * QT * 256;
         const float* cL = (const float*)(smem + O_L + buf * 512);
@@ -217,17 +232,30 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const 
             for (int ks = 0; ks < 4; ++ks) {
                 const bf16x8 qx = *(const bf16x8*)(cQ + s * 4096 + rowo[ks]);
                 const bf16x8 ox = *(const bf16x8*)(cO + s * 4096 + rowo[ks]);
-                sacc = mfma(qx, kf[ks], sacc);
-                dpacc = mfma(ox, vf[ks], dpacc);
+                if (LAB & 2) {
+                    asm volatile("" ::"v"(qx), "v"(ox));
+                } else {
+                    sacc = mfma(qx, kf[ks], sacc);
+                    dpacc = mfma(ox, vf[ks], dpacc);
+                }
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     const int wr = rb_a + 16 * u;  // window row of the block (multiple of 16)
                     const int c = t + 4 - (wr >> 5);
                     const int ringrow = (c % NCH) * 32 + (wr & 31);
                     const bf16x8 rx = *(const bf16x8*)(sR + ringrow * 256 + ro_R[ks]);
-                    if (u == 0) qa = mfma(qx, rx, qa);
+                    if (LAB & 2) asm volatile("" ::"v"(rx));
+                    else if (u == 0) qa = mfma(qx, rx, qa);
                     else qb2 = mfma(qx, rx, qb2);
                 }
+            }
+            if (LAB & 4) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    pa[4 * s + r] = (bf16)(sacc[r] + qa[r]);
+                    da[4 * s + r] = (bf16)(dpacc[r] + qb2[r]);
+                }
+                continue;
             }
             // skew: QR[i = 4g+r][wl = il (+16)] -> BD[i][j = il], wl = j - i + 15
             float* sc = scw + s * 16 * SCR;
@@ -268,13 +296,28 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv3_kernel(AttnArgs a, const 
         for (int n = 0; n < 8; ++n) {
             const bf16x8 ofr = cat8(tr_read(cO, quado[n]), tr_read(cO, 4096 + quado[n]));
             const bf16x8 qfr = cat8(tr_read(cQ, quado[n]), tr_read(cQ, 4096 + quado[n]));
-            dv[n] = mfma(ofr, pa, dv[n]);
-            dk[n] = mfma(qfr, da, dk[n]);
+            if (LAB & 2) {
+                asm volatile("" ::"v"(ofr), "v"(qfr), "v"(pa), "v"(da));
+            } else {
+                dv[n] = mfma(ofr, pa, dv[n]);
+                dk[n] = mfma(qfr, da, dk[n]);
+            }
         }
-        ds_prev = da;
+        {  // stage this tile's dS rows (0 above the diagonal) for the next iteration's stores
+            char* st = smem + O_T + buf * T_BYTES + (16 * w + il) * 2;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int row = 16 * (e >> 2) + 4 * g + (e & 3);
+                *(bf16*)(st + row * T_PITCH) = jk <= i0 + row ? da[e] : (bf16)0.f;
+            }
+        }
         i0_prev = i0;
     }
-    if (i0_prev >= 0) store_ds(ds_prev, i0_prev);
+    if (i0_prev >= 0 && !(LAB & 1)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        bar();
+        store_ds(i0_prev, (nqt - 1) & 1);
+    }
     // lane holds dK^T / dV^T [d = 16n + 4g + r][key il]
     if (jk < S) {
         bf16* dkp = dqkv + ((int64_t)b * S + jk) * ldd + (H + h) * HS;

@@ -117,8 +117,8 @@ def test_generate_cached_matches_exact(T0, ctx, n):
     np.testing.assert_array_equal(np.array(out["cached"]), np.array(out["exact"]))
 
 
-def test_cached_mode_rejects_transformer():
+def test_unknown_mode_rejected():
     from midiseq.transformer import Transformer, TransformerConfig
     m = Transformer(TransformerConfig(n_embd=64, n_heads=4, n_layer=1, block_len=16, precision="fp32")).to("cuda")
     with pytest.raises(ValueError):
-        generate(m, 16, tokens(1, 8, 0), META[:1], num_tokens=2, mode="cached")
+        generate(m, 16, tokens(1, 8, 0), META[:1], num_tokens=2, mode="kv")
