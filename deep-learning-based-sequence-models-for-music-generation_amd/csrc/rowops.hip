@@ -114,17 +114,22 @@ struct CopyDrop {
     int on;
 };
 
-// dx_acc += rstd*(dyg - mean(dyg) - xhat*mean(dyg*xhat)); per-block dgamma/dbeta partials
-template <typename TD, typename TO, int MAXC>
+// dx_acc += rstd*(dyg - mean(dyg) - xhat*mean(dyg*xhat)); per-block dgamma/dbeta
+// partials, and (BIAS) the column sums of the written gradient rows (the copy
+// after its dropout mask, else the updated dx_acc): the bias gradient of the
+// residual branch that produced this LayerNorm's input (model_transformer.py
+// :51,101 proj / FFN output biases), which would otherwise be a separate
+// column-sum pass over the same rows
+template <typename TD, typename TO, int MAXC, bool BIAS>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO* __restrict__ dcopy,
                                                      float* __restrict__ part, const TD* __restrict__ dy,
                                                      const float* __restrict__ x, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                      int64_t rows, int d, int64_t seg, int64_t skip, CopyDrop cd) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    f32x4 pg[MAXC], pb[MAXC];
+    f32x4 pg[MAXC], pb[MAXC], pc[MAXC];
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) pg[c] = pb[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < MAXC; ++c) pg[c] = pb[c] = pc[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
     for (int64_t row = blockIdx.x * 4LL + wid; row < rows; row += (int64_t)gridDim.x * 4) {
         const float mu = mean[row], rs = rstd[row];
         const int64_t xrow = map_row(row, seg, skip);
@@ -169,6 +174,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
                     }
                     store4(dcopy + xrow * d + col, o);
                 }
+                if (BIAS) pc[c] += o;
             }
         }
     }
@@ -182,7 +188,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
         for (int c = 0; c < MAXC; ++c) {
             const int col = (c * 64 + lane) * 4;
             f32x4 t = red[0][c * 64 + lane] + red[1][c * 64 + lane] + red[2][c * 64 + lane] + red[3][c * 64 + lane];
-            if (col < d) *(f32x4*)(part + (int64_t)blockIdx.x * 2 * d + col) = t;
+            if (col < d) *(f32x4*)(part + (int64_t)blockIdx.x * 3 * d + col) = t;
         }
     }
     __syncthreads();
@@ -194,35 +200,51 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
         for (int c = 0; c < MAXC; ++c) {
             const int col = (c * 64 + lane) * 4;
             f32x4 t = red[0][c * 64 + lane] + red[1][c * 64 + lane] + red[2][c * 64 + lane] + red[3][c * 64 + lane];
-            if (col < d) *(f32x4*)(part + (int64_t)blockIdx.x * 2 * d + d + col) = t;
+            if (col < d) *(f32x4*)(part + (int64_t)blockIdx.x * 3 * d + d + col) = t;
+        }
+    }
+    if (BIAS) {
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) red[wid][c * 64 + lane] = pc[c];
+        __syncthreads();
+        if (wid == 0) {
+#pragma unroll
+            for (int c = 0; c < MAXC; ++c) {
+                const int col = (c * 64 + lane) * 4;
+                f32x4 t = red[0][c * 64 + lane] + red[1][c * 64 + lane] + red[2][c * 64 + lane] + red[3][c * 64 + lane];
+                if (col < d) *(f32x4*)(part + (int64_t)blockIdx.x * 3 * d + 2 * d + col) = t;
+            }
         }
     }
 }
 
-// out[c] += sum_p part[p, c] for c < 2d (dgamma | dbeta)
+// out[c] += sum_p part[p, c] for c < nout (dgamma | dbeta | dbias), partial rows 3d apart
 // block = 64 columns x 4 waves; each wave sums every 4th partial row
 __global__ __launch_bounds__(256) void ln_reduce_kernel(float* __restrict__ dg, float* __restrict__ db,
-                                                        const float* __restrict__ part, int nparts, int d) {
+                                                        float* __restrict__ dbias, const float* __restrict__ part,
+                                                        int nparts, int d, int nout) {
     __shared__ float red[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + lane;
     float s = 0.f;
-    if (c < 2 * d) {
+    if (c < nout) {
 #pragma unroll 8
-        for (int p = w; p < nparts; p += 4) s += part[(int64_t)p * 2 * d + c];
+        for (int p = w; p < nparts; p += 4) s += part[(int64_t)p * 3 * d + c];
     }
     red[w][lane] = s;
     __syncthreads();
-    if (w == 0 && c < 2 * d) {
+    if (w == 0 && c < nout) {
         s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
         if (c < d) dg[c] += s;
-        else db[c - d] += s;
+        else if (c < 2 * d) db[c - d] += s;
+        else dbias[c - 2 * d] += s;
     }
 }
 
 extern "C" size_t msq_layernorm_bwd_workspace(int64_t rows, int64_t d) {
     (void)rows;
-    return (size_t)LN_BWD_BLOCKS * 2 * d * sizeof(float);
+    return (size_t)LN_BWD_BLOCKS * 3 * d * sizeof(float);
 }
 
 template <typename TY>
@@ -246,14 +268,21 @@ extern "C" int msq_layernorm_fwd(void* y, int y_dtype, float* mean, float* rstd,
     return MSQ_OK;
 }
 
+template <typename TD, typename TO, bool BIAS>
+static void ln_bwd_launch_b(float* dxa, TO* dcopy, float* part, const TD* dy, const float* x, const float* mean,
+                            const float* rstd, const float* gamma, int64_t rows, int d, int64_t seg, int64_t skip,
+                            CopyDrop cd, hipStream_t s) {
+    const dim3 grid(LN_BWD_BLOCKS);
+    if (d <= 256) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 1, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
+    else if (d <= 1024) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
+    else hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 8, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
+}
 template <typename TD, typename TO>
 static void ln_bwd_launch(float* dxa, TO* dcopy, float* part, const TD* dy, const float* x, const float* mean,
                           const float* rstd, const float* gamma, int64_t rows, int d, int64_t seg, int64_t skip,
-                          CopyDrop cd, hipStream_t s) {
-    const dim3 grid(LN_BWD_BLOCKS);
-    if (d <= 256) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 1>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
-    else if (d <= 1024) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
-    else hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 8>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
+                          CopyDrop cd, bool bias, hipStream_t s) {
+    if (bias) ln_bwd_launch_b<TD, TO, true>(dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd, s);
+    else ln_bwd_launch_b<TD, TO, false>(dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd, s);
 }
 
 extern "C" int msq_layernorm_bwd(float* dx_acc, void* dx_copy, int copy_dtype, float* dgamma, float* dbeta,
@@ -269,6 +298,15 @@ extern "C" int msq_layernorm_bwd_dropout(float* dx_acc, void* dx_copy, int copy_
                                          const float* rstd, const float* gamma, int64_t rows, int64_t d,
                                          int64_t seg_len, int64_t seg_skip, uint32_t seed, uint32_t site, float p,
                                          void* workspace, void* stream) {
+    return msq_layernorm_bwd_bias(dx_acc, dx_copy, copy_dtype, dgamma, dbeta, nullptr, dy, dy_dtype, x, mean, rstd,
+                                  gamma, rows, d, seg_len, seg_skip, seed, site, p, workspace, stream);
+}
+
+extern "C" int msq_layernorm_bwd_bias(float* dx_acc, void* dx_copy, int copy_dtype, float* dgamma, float* dbeta,
+                                      float* dbias, const void* dy, int dy_dtype, const float* x, const float* mean,
+                                      const float* rstd, const float* gamma, int64_t rows, int64_t d, int64_t seg_len,
+                                      int64_t seg_skip, uint32_t seed, uint32_t site, float p, void* workspace,
+                                      void* stream) {
     MSQ_CHECK_ARG(d % 4 == 0 && d <= 2048 && rows > 0 && workspace, "msq_layernorm_bwd: bad args");
     MSQ_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || dx_copy), "msq_layernorm_bwd: dropout needs dx_copy");
     CopyDrop cd{drop_base(seed, site), drop_threshold(p), 1.f / (1.f - p), p > 0.f ? 1 : 0};
@@ -276,15 +314,17 @@ extern "C" int msq_layernorm_bwd_dropout(float* dx_acc, void* dx_copy, int copy_
     hipStream_t s = (hipStream_t)stream;
     float* part = (float*)workspace;
     const int di = (int)d;
+    const bool bias = dbias != nullptr;
     if (dy_dtype == MSQ_BF16) {
-        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, s);
-        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, s);
+        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, bias, s);
+        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, bias, s);
     } else {
-        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, s);
-        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, s);
+        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, bias, s);
+        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, bias, s);
     }
-    hipLaunchKernelGGL(ln_reduce_kernel, dim3((unsigned)((2 * d + 63) / 64)), dim3(256), 0, s, dgamma, dbeta, part,
-                       LN_BWD_BLOCKS, di);
+    const int nout = (bias ? 3 : 2) * di;
+    hipLaunchKernelGGL(ln_reduce_kernel, dim3((unsigned)((nout + 63) / 64)), dim3(256), 0, s, dgamma, dbeta, dbias,
+                       part, LN_BWD_BLOCKS, di, nout);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }

@@ -466,19 +466,19 @@ class TransformerEngine:
         # dropout: gb is the gradient INTO the dropped branch (gres masked by the
         # keep mask of the site whose output was added to the residual there);
         # the bias gradients then sum gb instead of gres
-        side_bias = p > 0  # bias sums of gres (fp32, updated in place) stay on the main stream
+        # the proj / FFN output bias gradients (column sums of the gradient into
+        # each residual branch) are fused into the LayerNorm backward that
+        # writes those rows (dbias): lnf / ln1 of layer l+1 -> b2 of layer l,
+        # ln2 of layer l -> bproj of layer l
         ops.layernorm_bwd(gres, Bw["df"], A.x[cfg.n_layer], A.stf[0], A.stf[1], P["lnf_w"], G["lnf_w"], G["lnf_b"],
-                          dx_copy=Bw["gb"], seg=(T, N_META), drop=dsite(DROP_FFN + cfg.n_layer - 1))
+                          dx_copy=Bw["gb"], seg=(T, N_META), drop=dsite(DROP_FFN + cfg.n_layer - 1),
+                          dbias=G[f"{cfg.n_layer - 1}.b2"])
         layer_done("head")
         for l in reversed(range(cfg.n_layer)):
             # FFN (model_transformer.py:92-105,120)
             def ffn2_w(l=l):
                 ops.gemm(gb, A.h[l], ta=True, tb=True, out=G[f"{l}.w2"], epilogue=L.EPI_ACCUM)
-                if side_bias:
-                    ops.colsum(gb, G[f"{l}.b2"], accumulate=True)
             on_side("gb", ffn2_w)
-            if not side_bias:
-                ops.colsum(gres, G[f"{l}.b2"], accumulate=True)
             before_write("dh")
             ops.gemm(gb, W[f"{l}.w2"], tb=True, out=Bw["dh"], epilogue=L.EPI_RELU_MASK, aux=A.h[l])
 
@@ -490,16 +490,12 @@ class TransformerEngine:
             before_write("gb2")
             ops.layernorm_bwd(gres, Bw["dtmp"], A.xm[l], A.st2[l, 0], A.st2[l, 1], P[f"{l}.ln2_w"], G[f"{l}.ln2_w"],
                               G[f"{l}.ln2_b"], dx_copy=gb2 if Bw["gb"] is not None else None,
-                              drop=dsite(DROP_PROJ + l))
+                              drop=dsite(DROP_PROJ + l), dbias=G[f"{l}.bproj"])
             # attention (model_transformer.py:41-90,119)
 
             def proj_w(l=l):
                 ops.gemm(gb2, A.o[l], ta=True, tb=True, out=G[f"{l}.wproj"], epilogue=L.EPI_ACCUM)
-                if side_bias:
-                    ops.colsum(gb2, G[f"{l}.bproj"], accumulate=True)
             on_side("gb2", proj_w)
-            if not side_bias:
-                ops.colsum(gres, G[f"{l}.bproj"], accumulate=True)
             ops.gemm(gb2, W[f"{l}.wproj"], tb=True, out=Bw["dtmp"])
             before_write("dqkv")
             relattn_bwd(Bw["dtmp"], A.o[l], A.lse[l], A.qkv[l], W[f"{l}.R"], B, S, H, hs, scale, dqkv=Bw["dqkv"],
@@ -511,7 +507,8 @@ class TransformerEngine:
             ops.gemm(Bw["dqkv"], W[f"{l}.wqkv"], tb=True, out=Bw["dtmp"])
             before_write("gb")
             ops.layernorm_bwd(gres, Bw["dtmp"], A.x[l], A.st1[l, 0], A.st1[l, 1], P[f"{l}.ln1_w"], G[f"{l}.ln1_w"],
-                              G[f"{l}.ln1_b"], dx_copy=Bw["gb"], drop=dsite(DROP_FFN + l - 1) if l > 0 else None)
+                              G[f"{l}.ln1_b"], dx_copy=Bw["gb"], drop=dsite(DROP_FFN + l - 1) if l > 0 else None,
+                              dbias=G[f"{l - 1}.b2"] if l > 0 else None)
             layer_done(l)
         ops.embed_bwd(G["tok_emb"], G["meta_emb"], gres, idx, meta)
         layer_done(-1)
