@@ -81,6 +81,7 @@ CLASSIFY = {
     "msq_relattn_bwd_dropout": lambda a: ("attn_bwd", 2 * _attn_flops(a[11], a[12], a[13], a[14]), None),
     # filtered CE: 3 reads of the logits + 1 write of dlogits ([B, T, ld] of the act dtype)
     "msq_filtered_ce": lambda a: ("loss", None, 4.0 * a[13] * a[14] * a[5] * (2 if a[4] == L.BF16 else 4)),
+    "msq_filtered_ce_bias": lambda a: ("loss", None, 4.0 * a[14] * a[15] * a[6] * (2 if a[5] == L.BF16 else 4)),
     "msq_layernorm_fwd": lambda a: ("layernorm", None, None),
     "msq_layernorm_bwd": lambda a: ("layernorm", None, None),
     "msq_layernorm_bwd_dropout": lambda a: ("layernorm", None, None),

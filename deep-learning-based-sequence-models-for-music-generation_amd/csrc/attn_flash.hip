@@ -194,6 +194,29 @@ __global__ void flash_bwd_pre_kernel(AttnArgs a, const bf16* __restrict__ dout, 
     if (lane == 0) Dv[(b * a.H + h) * a.S + i] = s;
 }
 
+// same, 16 lanes x 8 elements (one 16-B load of dO and of O each) per
+// (row, head): 4 head-rows per wave
+__global__ __launch_bounds__(256) void flash_bwd_pre_vec_kernel(AttnArgs a, const bf16* __restrict__ dout,
+                                                                int64_t ldo, const bf16* __restrict__ out,
+                                                                float* __restrict__ Dv) {
+    const int64_t row = blockIdx.x * 16LL + (threadIdx.x >> 4);  // over B*S*H
+    const int l = threadIdx.x & 15;
+    const bool ok = row < a.B * a.S * a.H;
+    const int64_t r = ok ? row : 0;
+    const int64_t h = r % a.H, bi = r / a.H;
+    const bf16x8 x = *(const bf16x8*)(dout + bi * ldo + h * HS + 8 * l);
+    const bf16x8 y = *(const bf16x8*)(out + bi * ldo + h * HS + 8 * l);
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += (float)x[e] * (float)y[e];
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (ok && l == 0) {
+        const int64_t b = bi / a.S, i = bi % a.S;
+        Dv[(b * a.H + h) * a.S + i] = s;
+    }
+}
+
 // ------------------------------------------------------------ backward: fix-up
 // metadata prefix, j > i (only i < n_meta - 1): dS_ij was written to meta_ds.
 //   dq_i     += dS_ij k_j            (AC term; pass B only sees j <= i)
@@ -234,15 +257,27 @@ namespace {
 // and the row pad [S, ldr); and the row pad of dSj. The dq kernel and the dR
 // product never read further below the band.
 constexpr int DQR_BAND = 256;
+// one wave per row; ldr % 8 == 0 (flash_dqr_ld), so the row starts are 16-B
+// aligned: ragged ends with 2-B stores, the body with 16-B stores
+__device__ __forceinline__ void zero_span(bf16* __restrict__ p, int64_t lo, int64_t hi, int lane) {
+    if (lo >= hi) return;
+    const int64_t a = min(hi, (lo + 7) & ~(int64_t)7), e = max(a, hi & ~(int64_t)7);
+    if (lane < a - lo) p[lo + lane] = (bf16)0.f;
+    if (lane < hi - e) p[e + lane] = (bf16)0.f;
+    const u32x4 z = (u32x4){0u, 0u, 0u, 0u};
+    for (int64_t r = a + 8 * lane; r < e; r += 512) *(u32x4*)(p + r) = z;
+}
+
 __global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, bf16* __restrict__ dsj, int64_t ldr, int64_t S,
                                      int64_t rows) {
     const int64_t row = blockIdx.x * 4LL + (threadIdx.x >> 6);  // (h, b, i) flattened
     if (row >= rows) return;
+    const int lane = threadIdx.x & 63;
     const int64_t i = row % S;
     bf16* p = dqr + row * ldr;
-    const int64_t lo = max<int64_t>(0, S - 1 - i - DQR_BAND), hi = S - 1 - i;
-    for (int64_t r = lo + (threadIdx.x & 63); r < hi; r += 64) p[r] = (bf16)0.f;
-    for (int64_t r = S + (threadIdx.x & 63); r < ldr; r += 64) p[r] = dsj[row * ldr + r] = (bf16)0.f;
+    zero_span(p, max<int64_t>(0, S - 1 - i - DQR_BAND), S - 1 - i, lane);
+    zero_span(p, S, ldr, lane);
+    zero_span(dsj + row * ldr, S, ldr, lane);
 }
 }  // namespace
 
@@ -287,7 +322,12 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     hipLaunchKernelGGL(dqr_band_zero_kernel, dim3((unsigned)((H * B * S + 3) / 4)), dim3(256), 0, s, dqr, dsj, ldr,
                        S, H * B * S);
     hipMemsetAsync(meta_ds, 0, (size_t)B * H * 64 * 4, s);
-    hipLaunchKernelGGL(flash_bwd_pre_kernel, dim3((unsigned)((B * S * H + 3) / 4)), dim3(256), 0, s, a, dout, ldo, out, Dv);
+    if (ldo % 8 == 0 && ((uintptr_t)dout % 16) == 0 && ((uintptr_t)out % 16) == 0)
+        hipLaunchKernelGGL(flash_bwd_pre_vec_kernel, dim3((unsigned)((B * S * H + 15) / 16)), dim3(256), 0, s, a, dout,
+                           ldo, out, Dv);
+    else
+        hipLaunchKernelGGL(flash_bwd_pre_kernel, dim3((unsigned)((B * S * H + 3) / 4)), dim3(256), 0, s, a, dout, ldo,
+                           out, Dv);
     // key/value pass: dK, dV, and dS in both layouts
     if (flash_bwd_kv3(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s))
         return msq_set_error(MSQ_ERR_UNSUPPORTED, "flash_bwd: shape outside the key/value pass (n_meta > 8 or > 4 GB)");

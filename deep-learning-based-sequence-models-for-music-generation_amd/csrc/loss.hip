@@ -11,6 +11,7 @@
 // registers; the column sums of W*dZ are accumulated in registers over the 32
 // rows and flushed with one atomic per column), and an elementwise finisher.
 #include "common.h"
+#include <type_traits>
 #include <stdlib.h>
 
 namespace {
@@ -284,8 +285,6 @@ __device__ __forceinline__ void stv(T* p, const float (&x)[N]) {
 __device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 
 constexpr int TS2 = 32;    // time splits of colstats2 / finish2
-constexpr int ROWS2 = 64;  // rows per workgroup of rowstats2
-constexpr int NT2 = 512;   // rowstats2: 8 waves, a whole row of V columns in registers
 
 // Padded layouts (Vp = V rounded up to 16): col_lse copy, colsum and the 5-row
 // weight table live in the workspace with zero pads, so every 16-B access is
@@ -307,10 +306,29 @@ __global__ __launch_bounds__(NT) void colstats2_kernel(LossArgs a, float* __rest
     const int64_t t0 = ts * per, t1 = min(a.T, t0 + per);
     if (v >= a.V) return;
     const T* o = (const T*)a.o + b * a.T * a.ld + v;
+    constexpr float L2E = 1.4426950408889634f;
     float m[N], s[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) m[i] = -INFINITY, s[i] = 0.f;
-    for (int64_t t = t0; t < t1; ++t) {
+    // 4 rows per online-softmax update: 5 exponentials per 4 elements, 4 loads in flight
+    constexpr int U = 4;
+    int64_t t = t0;
+    for (; t + U <= t1; t += U) {
+        float x[U][N];
+#pragma unroll
+        for (int u = 0; u < U; ++u) ldv<T, N>(o + (t + u) * a.ld, x[u]);
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const float mn = fmaxf(fmaxf(m[i], fmaxf(x[0][i], x[1][i])), fmaxf(x[2][i], x[3][i]));
+            const float ml = mn * L2E;
+            float e = s[i] * __builtin_amdgcn_exp2f(__builtin_fmaf(m[i], L2E, -ml));
+#pragma unroll
+            for (int u = 0; u < U; ++u) e += __builtin_amdgcn_exp2f(__builtin_fmaf(x[u][i], L2E, -ml));
+            s[i] = e;
+            m[i] = mn;
+        }
+    }
+    for (; t < t1; ++t) {
         float x[N];
         ldv<T, N>(o + t * a.ld, x);
 #pragma unroll
@@ -370,111 +388,271 @@ __device__ __forceinline__ float block8_sum(float v, float* red) {
     return ((red[0] + red[1]) + (red[2] + red[3])) + ((red[4] + red[5]) + (red[6] + red[7]));
 }
 
-// NC = column chunks of NT2*N: chunks 0..NC-2 are full for every thread
-template <typename T, int NC>
-__global__ __launch_bounds__(NT2) void rowstats2_kernel(LossArgs a, const float* __restrict__ clp,
-                                                        const float* __restrict__ wtp, int Vp,
-                                                        float* __restrict__ loss_rows, float* __restrict__ row_lse,
-                                                        float* __restrict__ colsum, float gs) {
-    constexpr int N = VecOf<T>::N, CH = NT2 * N;
-    __shared__ float red[8];
-    const int blocks_per_b = (int)((a.T + ROWS2 - 1) / ROWS2);
-    const int b = blockIdx.x / blocks_per_b;
-    const int r0 = (blockIdx.x % blocks_per_b) * ROWS2, r1 = min((int)a.T, r0 + ROWS2);
-    const int tid = threadIdx.x, V = (int)a.V;
-    const int v0 = tid * N;
-    const bool last_ok = v0 + (NC - 1) * CH < V;  // this thread's part of the last chunk
-    float cl[NC][N], cs[NC][N];
+// nonzero column range [lo, hi) of every weight-table row (lo = hi = 0 for an
+// all-zero row): rowstats2 reads only the logits of those columns, since
+// Z = -(o - col_lse) W is exactly 0 wherever W is 0
+__global__ void wrange_kernel(const float* __restrict__ wtp, int64_t Vp, int64_t V, int* __restrict__ range) {
+    __shared__ int red[2][4];
+    const int k = blockIdx.x, tid = threadIdx.x;
+    int lo = INT32_MAX, hi = -1;
+    for (int64_t v = tid; v < V; v += 256)
+        if (wtp[k * Vp + v] != 0.f) lo = min(lo, (int)v), hi = max(hi, (int)v);
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-#pragma unroll
-        for (int i = 0; i < N; ++i) cs[c][i] = 0.f, cl[c][i] = 0.f;
-        if (c < NC - 1 || last_ok) ldf<N>(clp + (int64_t)b * Vp + v0 + c * CH, cl[c]);
-    }
-    for (int t = r0; t < r1; ++t) {
-        const int64_t row = (int64_t)b * a.T + t;
-        const T* o = (const T*)a.o + row * a.ld + v0;
-        const float* w = wtp + (int64_t)bucket_of(a, a.src[row]) * Vp + v0;
-        const int y = (int)a.trg[row];
-        float z[NC][N];
-        float mx = -INFINITY;
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            if (c < NC - 1 || last_ok) {
-                float ov[N], wv[N];
-                ldv<T, N>(o + c * CH, ov);
-                ldf<N>(w + c * CH, wv);
-#pragma unroll
-                for (int i = 0; i < N; ++i) {
-                    const bool in = c < NC - 1 || v0 + c * CH + i < V;
-                    z[c][i] = in ? -(ov[i] - cl[c][i]) * wv[i] : -INFINITY;
-                    mx = fmaxf(mx, z[c][i]);
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < N; ++i) z[c][i] = -INFINITY;
-            }
-        }
-        mx = block8_max(mx, red);
-        float se = 0.f;
-#pragma unroll
-        for (int c = 0; c < NC; ++c)
-#pragma unroll
-            for (int i = 0; i < N; ++i) se += fexp(z[c][i] - mx);
-        const float lse = mx + logf(block8_sum(se, red));
-        if (tid == 0) {
-            const float zy = -((float)((const T*)a.o)[row * a.ld + y] - clp[(int64_t)b * Vp + y]) *
-                             wtp[(int64_t)bucket_of(a, a.src[row]) * Vp + y];
-            loss_rows[row] = lse - zy;
-            row_lse[row] = lse;
-        }
-        // colsum_t(W dZ), dZ = (softmax_v Z - onehot y) gs   (pads: W = 0)
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            if (c < NC - 1 || last_ok) {
-                float wv[N];
-                ldf<N>(w + c * CH, wv);
-                const int vb = v0 + c * CH;
-#pragma unroll
-                for (int i = 0; i < N; ++i) cs[c][i] += wv[i] * (fexp(z[c][i] - lse) - (vb + i == y ? 1.f : 0.f)) * gs;
-            }
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-        const int vb = v0 + c * CH;
-#pragma unroll
-        for (int i = 0; i < N; ++i)
-            if (vb + i < V) atomicAdd(colsum + (int64_t)b * Vp + vb + i, cs[c][i]);
+    for (int o = 32; o > 0; o >>= 1) lo = min(lo, __shfl_xor(lo, o, 64)), hi = max(hi, __shfl_xor(hi, o, 64));
+    if ((tid & 63) == 0) red[0][tid >> 6] = lo, red[1][tid >> 6] = hi;
+    __syncthreads();
+    if (tid == 0) {
+        lo = min(min(red[0][0], red[0][1]), min(red[0][2], red[0][3]));
+        hi = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
+        range[2 * k] = hi < 0 ? 0 : lo;
+        range[2 * k + 1] = hi + 1;
     }
 }
 
+// Per row, one wave (log2 domain, z = Z log2 e = (cl - o) W log2 e):
+//   row_lse = logsumexp_v Z,  loss_row = row_lse - Z[y]
+// Only the bucket's nonzero weight range [lo, hi) is read; the V - (hi - lo)
+// columns outside it have Z = 0 exactly and enter the sum analytically.
+template <typename T>
+__global__ __launch_bounds__(256) void rowlse_kernel(LossArgs a, const float* __restrict__ clp,
+                                                     const float* __restrict__ wtp, int Vp,
+                                                     const int* __restrict__ wrange, float* __restrict__ loss_rows,
+                                                     float* __restrict__ row_lse) {
+    constexpr int N = VecOf<T>::N;
+    constexpr float L2E = 1.4426950408889634f;
+    const int lane = threadIdx.x & 63;
+    const int64_t row = blockIdx.x * 4LL + (threadIdx.x >> 6);
+    if (row >= a.B * a.T) return;  // whole waves; no block-level sync below
+    const int64_t b = row / a.T;
+    const int bk = bucket_of(a, a.src[row]);
+    const int lo = wrange[2 * bk], hi = wrange[2 * bk + 1];
+    const T* o = (const T*)a.o + row * a.ld;
+    const float* cl = clp + b * Vp;
+    const float* w = wtp + (int64_t)bk * Vp;
+    float m = -INFINITY, s = 0.f;
+    for (int v = (lo & ~(N - 1)) + lane * N; v < hi; v += 64 * N) {
+        float x[N], c[N], ww[N], z[N];
+        ldv<T, N>(o + v, x);
+        ldf<N>(cl + v, c);
+        ldf<N>(w + v, ww);
+        float mm = m;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            z[i] = (v + i >= lo && v + i < hi) ? (c[i] - x[i]) * ww[i] * L2E : -INFINITY;
+            mm = fmaxf(mm, z[i]);
+        }
+        if (mm != -INFINITY) {
+            float e = m == -INFINITY ? 0.f : s * __builtin_amdgcn_exp2f(m - mm);
+#pragma unroll
+            for (int i = 0; i < N; ++i) e += __builtin_amdgcn_exp2f(z[i] - mm);
+            s = e;
+            m = mm;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float m2 = __shfl_xor(m, off, 64), s2 = __shfl_xor(s, off, 64);
+        const float mn = fmaxf(m, m2);
+        s = (mn == -INFINITY) ? 0.f
+                              : (m == -INFINITY ? 0.f : s * __builtin_amdgcn_exp2f(m - mn)) +
+                                    (m2 == -INFINITY ? 0.f : s2 * __builtin_amdgcn_exp2f(m2 - mn));
+        m = mn;
+    }
+    if (lane == 0) {
+        const int inact = (int)a.V - (hi - lo);  // columns with Z = 0 outside the range
+        if (inact > 0) {
+            const float mn = fmaxf(m, 0.f);
+            s = (m == -INFINITY ? 0.f : s * __builtin_amdgcn_exp2f(m - mn)) + (float)inact * __builtin_amdgcn_exp2f(-mn);
+            m = mn;
+        }
+        const float lse2 = m + __builtin_log2f(s);
+        const int y = (int)a.trg[row];
+        const float zy = (y >= lo && y < hi) ? (cl[y] - (float)o[y]) * w[y] * L2E : 0.f;
+        loss_rows[row] = (lse2 - zy) / L2E;
+        row_lse[row] = lse2 / L2E;
+    }
+}
+
+// colsum_t(W dZ) partials per (batch, time split): thread-owned columns as in
+// finish2, W dZ = W gs (softmax_v Z - onehot y); rows whose bucket has zero
+// weight on the thread's columns contribute 0 and are not read.
+template <typename T>
+__global__ __launch_bounds__(NT) void cspart_kernel(LossArgs a, const float* __restrict__ clp,
+                                                    const float* __restrict__ wtp, int Vp,
+                                                    const float* __restrict__ row_lse, float gs,
+                                                    float* __restrict__ part) {
+    constexpr int N = VecOf<T>::N;
+    constexpr float L2E = 1.4426950408889634f;
+    __shared__ f32x4 wl[5][NT * N / 4];
+    const int tid = threadIdx.x;
+    const int v = (blockIdx.x * NT + tid) * N;
+    const int64_t b = blockIdx.y, ts = blockIdx.z;
+    const int64_t per = (a.T + TS2 - 1) / TS2;
+    const int64_t t0 = ts * per, t1 = min(a.T, t0 + per);
+    if (v >= a.V) return;  // only this thread's own LDS slots are read
+    float cl2[N], cs[N];
+    ldf<N>(clp + b * Vp + v, cl2);
+#pragma unroll
+    for (int i = 0; i < N; ++i) cl2[i] *= L2E, cs[i] = 0.f;
+    unsigned nzb = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        float w[N];
+        ldf<N>(wtp + (int64_t)k * Vp + v, w);
+        bool nz = false;
+#pragma unroll
+        for (int i = 0; i < N; i += 4) {
+            wl[k][tid * (N / 4) + i / 4] = (f32x4){w[i], w[i + 1], w[i + 2], w[i + 3]};
+            nz |= (w[i] != 0.f) | (w[i + 1] != 0.f) | (w[i + 2] != 0.f) | (w[i + 3] != 0.f);
+        }
+        nzb |= (unsigned)nz << k;
+    }
+    auto one = [&](const float (&ov)[N], int bk, int y, float lse) {
+        float w[N];
+#pragma unroll
+        for (int i = 0; i < N; i += 4) {
+            const f32x4 u = wl[bk][tid * (N / 4) + i / 4];
+            w[i] = u[0], w[i + 1] = u[1], w[i + 2] = u[2], w[i + 3] = u[3];
+        }
+        const float l2 = lse * L2E;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const float av = __builtin_fmaf(ov[i], L2E, -cl2[i]);
+            const float sv = __builtin_amdgcn_exp2f(__builtin_fmaf(-av, w[i], -l2));
+            cs[i] = __builtin_fmaf(w[i] * gs, sv, cs[i]);
+        }
+        if ((unsigned)(y - v) < (unsigned)N) {
+#pragma unroll
+            for (int i = 0; i < N; ++i)
+                if (v + i == y) cs[i] -= w[i] * gs;
+        }
+    };
+    constexpr int U = 4;
+    int64_t t = t0;
+    for (; t + U <= t1; t += U) {
+        float ov[U][N];
+        int bk[U], y[U];
+        float lse[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t row = b * a.T + t + u;
+            bk[u] = bucket_of(a, a.src[row]);
+            y[u] = (int)a.trg[row];
+            lse[u] = row_lse[row];
+            if ((nzb >> bk[u]) & 1) ldv<T, N>((const T*)a.o + row * a.ld + v, ov[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if ((nzb >> bk[u]) & 1) one(ov[u], bk[u], y[u], lse[u]);
+    }
+    for (; t < t1; ++t) {
+        const int64_t row = b * a.T + t;
+        const int bk = bucket_of(a, a.src[row]);
+        if ((nzb >> bk) & 1) {
+            float ov[N];
+            ldv<T, N>((const T*)a.o + row * a.ld + v, ov);
+            one(ov, bk, (int)a.trg[row], row_lse[row]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) part[(b * TS2 + ts) * Vp + v + i] = v + i < a.V ? cs[i] : 0.f;
+}
+
+// colsum[b][v] = sum over the TS2 partials in a fixed order (pads -> 0)
+__global__ void cs_reduce_kernel(const float* __restrict__ part, int64_t B, int64_t V, int64_t Vp,
+                                 float* __restrict__ colsum) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= B * Vp) return;
+    const int64_t b = e / Vp, v = e % Vp;
+    float s = 0.f;
+    if (v < V) {
+        const float* p = part + b * TS2 * Vp + v;
+#pragma unroll 8
+        for (int ts = 0; ts < TS2; ++ts) s += p[ts * Vp];
+    }
+    colsum[e] = s;
+}
+
+// dO[t,v] = -W[v] dZ[t,v] + softmax_t(o)[t,v] colsum_t(W dZ)[v], in the log2
+// domain (a = (o - col_lse) log2 e):
+//   softmax_t(o) = 2^a,  softmax_v(Z) = 2^(-a W - row_lse log2 e)
+// A thread's 5 weight rows sit in LDS (indexed by the row's bucket, no
+// register select chains); a bucket whose weights are all 0 on the thread's
+// columns (most columns of the sparse grammar rows) skips the dZ term.
 template <typename T, typename TD>
 __global__ __launch_bounds__(NT) void finish2_kernel(LossArgs a, const float* __restrict__ clp,
                                                      const float* __restrict__ wtp, int Vp,
                                                      const float* __restrict__ row_lse,
                                                      const float* __restrict__ colsum, TD* __restrict__ dout,
-                                                     int64_t ldd, float gs) {
+                                                     int64_t ldd, float gs, float* __restrict__ dbias) {
     constexpr int N = VecOf<T>::N;
-    const int v = (blockIdx.x * NT + threadIdx.x) * N;
+    constexpr float L2E = 1.4426950408889634f;
+    __shared__ f32x4 wl[5][NT * N / 4];
+    const int tid = threadIdx.x;
+    const int v = (blockIdx.x * NT + tid) * N;
     const int64_t b = blockIdx.y, ts = blockIdx.z;
     const int64_t per = (a.T + TS2 - 1) / TS2;
     const int64_t t0 = ts * per, t1 = min(a.T, t0 + per);
-    if (v >= a.V) return;
-    float cl[N], cs[N], wt[5][N];
-    ldf<N>(clp + b * Vp + v, cl);
+    if (v >= a.V) return;  // only this thread's own LDS slots are ever read: no barrier needed
+    float cl2[N], cs[N];
+    ldf<N>(clp + b * Vp + v, cl2);
     ldf<N>(colsum + b * Vp + v, cs);
 #pragma unroll
-    for (int k = 0; k < 5; ++k) ldf<N>(wtp + (int64_t)k * Vp + v, wt[k]);
+    for (int i = 0; i < N; ++i) cl2[i] *= L2E;
+    unsigned nzb = 0;  // bit k: bucket k has a nonzero weight on this thread's columns
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        float w[N];
+        ldf<N>(wtp + (int64_t)k * Vp + v, w);
+        bool nz = false;
+#pragma unroll
+        for (int i = 0; i < N; i += 4) {
+            wl[k][tid * (N / 4) + i / 4] = (f32x4){w[i], w[i + 1], w[i + 2], w[i + 3]};
+            nz |= (w[i] != 0.f) | (w[i + 1] != 0.f) | (w[i + 2] != 0.f) | (w[i + 3] != 0.f);
+        }
+        nzb |= (unsigned)nz << k;
+    }
+    const bool edge = v + N > a.V;  // the one thread holding pad columns
+    float bs[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) bs[i] = 0.f;
     auto one = [&](int64_t row, const float (&ov)[N], int bk, int y, float lse) {
-        float d[N];
+        float d[N], ea[N];
 #pragma unroll
         for (int i = 0; i < N; ++i) {
-            const float wv = bk == 0 ? wt[0][i] : bk == 1 ? wt[1][i] : bk == 2 ? wt[2][i] : bk == 3 ? wt[3][i] : wt[4][i];
-            const float oc = ov[i] - cl[i];
-            const float dz = (fexp(-oc * wv - lse) - (v + i == y ? 1.f : 0.f)) * gs;
-            d[i] = (v + i < a.V) ? -wv * dz + fexp(oc) * cs[i] : 0.f;  // pad columns stay 0
+            const float av = __builtin_fmaf(ov[i], L2E, -cl2[i]);
+            ea[i] = __builtin_amdgcn_exp2f(av);
+            d[i] = av;
         }
+        if ((nzb >> bk) & 1) {
+            float w[N];
+#pragma unroll
+            for (int i = 0; i < N; i += 4) {
+                const f32x4 u = wl[bk][tid * (N / 4) + i / 4];
+                w[i] = u[0], w[i + 1] = u[1], w[i + 2] = u[2], w[i + 3] = u[3];
+            }
+            const float l2 = lse * L2E;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const float sv = __builtin_amdgcn_exp2f(__builtin_fmaf(-d[i], w[i], -l2));  // softmax_v Z
+                d[i] = __builtin_fmaf(ea[i], cs[i], -w[i] * sv * gs);
+            }
+            if ((unsigned)(y - v) < (unsigned)N) {
+#pragma unroll
+                for (int i = 0; i < N; ++i)
+                    if (v + i == y) d[i] += w[i] * gs;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < N; ++i) d[i] = ea[i] * cs[i];
+        }
+        if (edge) {
+#pragma unroll
+            for (int i = 0; i < N; ++i)
+                if (v + i >= a.V) d[i] = 0.f;  // pad columns stay 0
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) bs[i] += d[i];
         stv<TD, N>(dout + row * ldd + v, d);
     };
     // 4 rows per step: their loads are all in flight before the first use
@@ -501,6 +679,52 @@ __global__ __launch_bounds__(NT) void finish2_kernel(LossArgs a, const float* __
         ldv<T, N>((const T*)a.o + row * a.ld + v, ov);
         one(row, ov, bucket_of(a, a.src[row]), (int)a.trg[row], row_lse[row]);
     }
+    // dbias partials: column sums of this thread's dlogits rows (the output bias
+    // gradient), written per (batch, time split) and reduced in a fixed order by
+    // dbias_reduce_kernel, so the bias gradient is bitwise reproducible
+    if (dbias) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) dbias[(b * TS2 + ts) * Vp + v + i] = bs[i];
+    }
+}
+
+// 1024 threads = 64 columns x 16 partial groups (partials g, g+16, ...), the
+// 16 group sums added in a fixed order through LDS: deterministic, and 16
+// waves per CU keep enough loads in flight for the [B*TS2][Vp] partials
+__global__ __launch_bounds__(1024) void dbias_reduce_kernel(const float* __restrict__ part, int64_t nparts, int Vp,
+                                                            int64_t V, float* __restrict__ dbias) {
+    __shared__ float red[16][64];
+    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int64_t v = (int64_t)blockIdx.x * 64 + c;
+    float s = 0.f;
+    if (v < V) {
+        int64_t p = g;
+        for (; p + 48 < nparts; p += 64) {
+            const float x0 = part[p * Vp + v], x1 = part[(p + 16) * Vp + v];
+            const float x2 = part[(p + 32) * Vp + v], x3 = part[(p + 48) * Vp + v];
+            s += x0; s += x1; s += x2; s += x3;
+        }
+        for (; p < nparts; p += 16) s += part[p * Vp + v];
+    }
+    red[g][c] = s;
+    __syncthreads();
+    if (g == 0 && v < V) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) t += red[k][c];
+        dbias[v] += t;
+    }
+}
+
+// fallback for dbias where finish2 does not run: column sums of dlogits rows
+template <typename TD>
+__global__ void dlogit_colsum_kernel(const TD* __restrict__ d, int64_t ldd, int64_t rows, int64_t V,
+                                     float* __restrict__ dbias) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    float s = 0.f;
+    for (int64_t r = 0; r < rows; ++r) s += (float)d[r * ldd + v];
+    dbias[v] += s;
 }
 
 LossArgs mk(const void* o, int64_t ld, const int64_t* src, const int64_t* trg, const float* wtab, int64_t b0,
@@ -528,7 +752,7 @@ extern "C" size_t msq_filtered_workspace(int64_t B, int64_t T, int64_t V) {
     // | row_lse [B*T] | colstats2 partials [B][TS2][2][V] | clp, colsum [B][Vp] | wtab [5][Vp]
     const size_t Vp = (V + 15) / 16 * 16;
     return (size_t)B * TSPLIT * 2 * V * 4 + (size_t)B * V * 4 + (size_t)B * T * 4 * 2 + 256 +
-           (size_t)B * 32 * 2 * V * 4 + (2 * (size_t)B + 5) * Vp * 4 + 256;
+           (size_t)B * 32 * 2 * V * 4 + (2 * (size_t)B + 5) * Vp * 4 + 64 + 256;
 }
 
 #define LOSS_CHECK()                                                                                  \
@@ -550,7 +774,16 @@ extern "C" int msq_filtered_ce(float* loss, void* dlogits, int64_t ldd, const vo
                                const int64_t* src, const int64_t* trg, const float* wtab, int64_t b0, int64_t b1,
                                int64_t b2, int64_t b3, int64_t B, int64_t T, int64_t V, float grad_scale,
                                float* col_lse, void* workspace, void* stream) {
+    return msq_filtered_ce_bias(loss, dlogits, ldd, nullptr, logits, dtype, ld, src, trg, wtab, b0, b1, b2, b3, B, T, V,
+                                grad_scale, col_lse, workspace, stream);
+}
+
+extern "C" int msq_filtered_ce_bias(float* loss, void* dlogits, int64_t ldd, float* dbias, const void* logits,
+                                    int dtype, int64_t ld, const int64_t* src, const int64_t* trg, const float* wtab,
+                                    int64_t b0, int64_t b1, int64_t b2, int64_t b3, int64_t B, int64_t T, int64_t V,
+                                    float grad_scale, float* col_lse, void* workspace, void* stream) {
     LOSS_CHECK();
+    MSQ_CHECK_ARG(!dbias || dlogits, "msq_filtered_ce_bias: dbias needs dlogits");
     MSQ_CHECK_ARG(!dlogits || ldd % 4 == 0, "msq_filtered_ce: ldd %% 4 != 0");
     const LossArgs a = mk(logits, ld, src, trg, wtab, b0, b1, b2, b3, B, T, V);
     hipStream_t s = (hipStream_t)stream;
@@ -561,8 +794,7 @@ extern "C" int msq_filtered_ce(float* loss, void* dlogits, int64_t ldd, const vo
     float* part2 = (float*)(ws + (size_t)B * TSPLIT * 2 * V * 4 + (size_t)B * V * 4 + (size_t)B * T * 4 * 2 + 256);
     const bool bfl = dtype == MSQ_BF16;
     const bool stream2 = dlogits && ld % 8 == 0 && ldd % 8 == 0 && ((uintptr_t)logits % 16) == 0 &&
-                         ((uintptr_t)dlogits % 16) == 0 &&
-                         (V + (bfl ? 4095 : 2047)) / (bfl ? 4096 : 2048) <= (bfl ? 5 : 9) && !getenv("MSQ_CE_V1");
+                         ((uintptr_t)dlogits % 16) == 0 && !getenv("MSQ_CE_V1");
     if (!stream2) {
         if (bfl) colstats_launch<bf16>(a, col_lse, part, s);
         else colstats_launch<float>(a, col_lse, part, s);
@@ -572,49 +804,39 @@ extern "C" int msq_filtered_ce(float* loss, void* dlogits, int64_t ldd, const vo
         if (bfl) hipLaunchKernelGGL((row_kernel<0, bf16, float>), dim3(nblk), dim3(NT), 0, s, a, col_lse, rows, (float*)nullptr, 0, nullptr, 0, nullptr, 0.f, 0);
         else hipLaunchKernelGGL((row_kernel<0, float, float>), dim3(nblk), dim3(NT), 0, s, a, col_lse, rows, (float*)nullptr, 0, nullptr, 0, nullptr, 0.f, 0);
     } else if (stream2) {
-        // streaming path: colstats2 -> rowstats2 -> finish2 on zero-padded copies
+        // streaming path: colstats2 -> rowlse -> cspart -> finish2 on zero-padded copies
         const int64_t Vp = (V + 15) / 16 * 16;
         float* clp = part2 + (size_t)B * TS2 * 2 * V;
         float* csp = clp + B * Vp;
         float* wtp = csp + B * Vp;
         float* row_lse = rows + B * T;
-        hipMemsetAsync(csp, 0, (size_t)B * Vp * 4, s);
         hipLaunchKernelGGL(pad_table_kernel, dim3((unsigned)((5 * Vp + 255) / 256)), dim3(256), 0, s, wtab, wtp,
                            (int64_t)5, V, Vp);
         const int N = bfl ? 8 : 4;
         const dim3 gc((unsigned)((V + NT * N - 1) / (NT * N)), (unsigned)B, TS2);
-        const unsigned nb2 = (unsigned)(B * ((T + ROWS2 - 1) / ROWS2));
-        const int nc = (int)((V + NT2 * N - 1) / (NT2 * N));
         const dim3 gm((unsigned)((B * Vp + 255) / 256));
-#define ROWSTATS(TT, NCV) hipLaunchKernelGGL((rowstats2_kernel<TT, NCV>), dim3(nb2), dim3(NT2), 0, s, a, clp, wtp, (int)Vp, rows, row_lse, csp, grad_scale)
+        const dim3 gr((unsigned)((B * T + 3) / 4));
+        int* wrange = (int*)(wtp + 5 * Vp);
+        hipLaunchKernelGGL(wrange_kernel, dim3(5), dim3(256), 0, s, wtp, Vp, V, wrange);
+        // part2 carries, in turn: colstats2 partials, colsum partials, dbias partials
         if (bfl) {
             hipLaunchKernelGGL(colstats2_kernel<bf16>, gc, dim3(NT), 0, s, a, part2);
             hipLaunchKernelGGL(colstats2_merge_kernel, gm, dim3(256), 0, s, a, part2, col_lse, clp, Vp);
-            switch (nc) {
-                case 1: ROWSTATS(bf16, 1); break;
-                case 2: ROWSTATS(bf16, 2); break;
-                case 3: ROWSTATS(bf16, 3); break;
-                case 4: ROWSTATS(bf16, 4); break;
-                default: ROWSTATS(bf16, 5); break;
-            }
-            hipLaunchKernelGGL((finish2_kernel<bf16, bf16>), gc, dim3(NT), 0, s, a, clp, wtp, (int)Vp, row_lse, csp, (bf16*)dlogits, ldd, grad_scale);
+            hipLaunchKernelGGL(rowlse_kernel<bf16>, gr, dim3(256), 0, s, a, clp, wtp, (int)Vp, wrange, rows, row_lse);
+            hipLaunchKernelGGL(cspart_kernel<bf16>, gc, dim3(NT), 0, s, a, clp, wtp, (int)Vp, row_lse, grad_scale, part2);
+            hipLaunchKernelGGL(cs_reduce_kernel, gm, dim3(256), 0, s, part2, B, V, Vp, csp);
+            hipLaunchKernelGGL((finish2_kernel<bf16, bf16>), gc, dim3(NT), 0, s, a, clp, wtp, (int)Vp, row_lse, csp, (bf16*)dlogits, ldd, grad_scale, dbias ? part2 : nullptr);
         } else {
             hipLaunchKernelGGL(colstats2_kernel<float>, gc, dim3(NT), 0, s, a, part2);
             hipLaunchKernelGGL(colstats2_merge_kernel, gm, dim3(256), 0, s, a, part2, col_lse, clp, Vp);
-            switch (nc) {
-                case 1: ROWSTATS(float, 1); break;
-                case 2: ROWSTATS(float, 2); break;
-                case 3: ROWSTATS(float, 3); break;
-                case 4: ROWSTATS(float, 4); break;
-                case 5: ROWSTATS(float, 5); break;
-                case 6: ROWSTATS(float, 6); break;
-                case 7: ROWSTATS(float, 7); break;
-                case 8: ROWSTATS(float, 8); break;
-                default: ROWSTATS(float, 9); break;
-            }
-            hipLaunchKernelGGL((finish2_kernel<float, float>), gc, dim3(NT), 0, s, a, clp, wtp, (int)Vp, row_lse, csp, (float*)dlogits, ldd, grad_scale);
+            hipLaunchKernelGGL(rowlse_kernel<float>, gr, dim3(256), 0, s, a, clp, wtp, (int)Vp, wrange, rows, row_lse);
+            hipLaunchKernelGGL(cspart_kernel<float>, gc, dim3(NT), 0, s, a, clp, wtp, (int)Vp, row_lse, grad_scale, part2);
+            hipLaunchKernelGGL(cs_reduce_kernel, gm, dim3(256), 0, s, part2, B, V, Vp, csp);
+            hipLaunchKernelGGL((finish2_kernel<float, float>), gc, dim3(NT), 0, s, a, clp, wtp, (int)Vp, row_lse, csp, (float*)dlogits, ldd, grad_scale, dbias ? part2 : nullptr);
         }
-#undef ROWSTATS
+        if (dbias)  // part2 is free after colstats2_merge: finish2 left [B*TS2][Vp] partials in it
+            hipLaunchKernelGGL(dbias_reduce_kernel, dim3((unsigned)((V + 63) / 64)), dim3(1024), 0, s, part2,
+                               B * TS2, (int)Vp, V, dbias);
     } else {
         hipMemsetAsync(colsum, 0, (size_t)B * V * 4, s);
         const unsigned gf = (unsigned)std::min<int64_t>(B * T * ((V + 3) / 4) / 256 + 1, 16384);
@@ -624,6 +846,11 @@ extern "C" int msq_filtered_ce(float* loss, void* dlogits, int64_t ldd, const vo
         } else {
             hipLaunchKernelGGL((row_kernel<1, float, float>), dim3(nblk), dim3(NT), 0, s, a, col_lse, rows, (float*)dlogits, ldd, nullptr, 0, colsum, grad_scale, 0);
             hipLaunchKernelGGL((finish_kernel<float, float>), dim3(gf), dim3(256), 0, s, a, col_lse, colsum, (float*)dlogits, ldd);
+        }
+        if (dbias) {
+            const dim3 gb((unsigned)((V + 255) / 256));
+            if (bfl) hipLaunchKernelGGL(dlogit_colsum_kernel<bf16>, gb, dim3(256), 0, s, (const bf16*)dlogits, ldd, B * T, V, dbias);
+            else hipLaunchKernelGGL(dlogit_colsum_kernel<float>, gb, dim3(256), 0, s, (const float*)dlogits, ldd, B * T, V, dbias);
         }
     }
     hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(NT), 0, s, rows, B * T, loss);

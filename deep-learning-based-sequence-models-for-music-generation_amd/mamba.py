@@ -285,7 +285,7 @@ class MambaEngine:
         cache.length += 1
         return cache.logits
 
-    def backward(self, dlogits, grads):
+    def backward(self, dlogits, grads, head_bias_done=False):
         cfg, P, W = self.cfg, self.P, self.W
         G = self.layout.views(grads)
         idx, meta = self._idx, self._meta
@@ -299,7 +299,8 @@ class MambaEngine:
         hook = self.layer_grad_ready
         dl = dlogits[:, :V]
         ops.gemm(dlogits, A.f, ta=True, tb=True, out=G["lm_w"], epilogue=L.EPI_ACCUM)  # pad columns are 0
-        ops.colsum(dl, G["lm_b"][:V], accumulate=True)
+        if not head_bias_done:
+            ops.colsum(dl, G["lm_b"][:V], accumulate=True)
         ops.gemm(dlogits, W["lm_w"], tb=True, out=Bw["df"])
         gx, gxb = Bw["gx"], Bw["gxb"]
         gx.zero_()

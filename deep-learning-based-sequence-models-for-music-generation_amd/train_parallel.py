@@ -35,6 +35,7 @@ class TrainStep:
         self.v = torch.zeros_like(flat)
         self.lr, self.betas, self.eps = lr, betas, eps
         self.grammar = grammar or Grammar()
+        self.lm_bias_grad = self.eng.layout.views(self.grads)["lm_b"][:self.eng.cfg.vocab_size]
         self.step_no = 0
         self.buckets = None
         if dist.is_initialized() and dist.get_world_size(group) > 1:
@@ -51,10 +52,11 @@ class TrainStep:
         eng.forward(src, meta, train=self.model.training)
         A = eng.acts(B, T)
         dl = eng.dlogits_buffer(B, T)
-        loss, _ = ce_forward_backward(src, A.logits.view(B, T, cfg.v_pad), trg, cfg.vocab_size, self.grammar,
-                                      dlogits=dl.view(B, T, cfg.v_pad))
         self.grads.zero_()
-        eng.backward(dl, self.grads)
+        # the output-bias gradient (column sums of dlogits) comes out of the loss pass
+        loss, _ = ce_forward_backward(src, A.logits.view(B, T, cfg.v_pad), trg, cfg.vocab_size, self.grammar,
+                                      dlogits=dl.view(B, T, cfg.v_pad), dbias=self.lm_bias_grad)
+        eng.backward(dl, self.grads, head_bias_done=True)
         scale = self.buckets.finish() if self.buckets is not None else 1.0
         self.step_no += 1
         ops.adam_step(self.model.flat.data, self.grads, self.m, self.v, self.step_no, self.lr, self.betas[0],

@@ -392,9 +392,10 @@ class TransformerEngine:
         return cache.logits
 
     # ------------------------------------------------------------ backward
-    def backward(self, dlogits, grads):
+    def backward(self, dlogits, grads, head_bias_done=False):
         """dlogits: [B*T, ld] (act dtype) whose first V columns are dL/dlogits;
-        grads: flat fp32 buffer (accumulated)."""
+        grads: flat fp32 buffer (accumulated). head_bias_done: the lm_head
+        bias gradient was already accumulated (msq_filtered_ce_bias)."""
         cfg, P, W = self.cfg, self.P, self.W
         G = self.layout.views(grads)
         idx, meta = self._idx, self._meta
@@ -454,7 +455,8 @@ class TransformerEngine:
         # lm_head (model_transformer.py:147,161)
         def lm_w():
             ops.gemm(dlogits, A.f, ta=True, tb=True, out=G["lm_w"], epilogue=L.EPI_ACCUM)  # pad columns are 0
-            ops.colsum(dl, G["lm_b"][:V], accumulate=True)
+            if not head_bias_done:
+                ops.colsum(dl, G["lm_b"][:V], accumulate=True)
         on_side("dlogits", lm_w)
         ops.gemm(dlogits, W["lm_w"], tb=True, out=Bw["df"])
         gres = Bw["gres"]

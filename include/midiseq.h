@@ -193,6 +193,13 @@ int msq_filtered_ce(float* loss, void* dlogits, int64_t ldd, const void* logits,
                     const int64_t* src, const int64_t* trg, const float* wtab, int64_t b0, int64_t b1, int64_t b2,
                     int64_t b3, int64_t B, int64_t T, int64_t V, float grad_scale, float* col_lse, void* workspace,
                     void* stream);
+/* msq_filtered_ce that also accumulates (+=) into dbias (fp32 [V]) the column
+ * sums of dlogits over the B*T rows: the gradient of the output layer's bias
+ * (lm_head.bias / output_layer.bias), fused into the pass that writes dlogits. */
+int msq_filtered_ce_bias(float* loss, void* dlogits, int64_t ldd, float* dbias, const void* logits, int dtype,
+                         int64_t ld, const int64_t* src, const int64_t* trg, const float* wtab, int64_t b0, int64_t b1,
+                         int64_t b2, int64_t b3, int64_t B, int64_t T, int64_t V, float grad_scale, float* col_lse,
+                         void* workspace, void* stream);
 /* Z rows t_begin..T-1 (fp32, [B, T-t_begin, ldz]) = filtered_logit(src, logits). */
 int msq_filtered_logit(float* z, int64_t ldz, const void* logits, int dtype, int64_t ld, const int64_t* src,
                        const float* wtab, int64_t b0, int64_t b1, int64_t b2, int64_t b3, int64_t B, int64_t T,
