@@ -56,6 +56,7 @@ SIGNATURES = {
     "msq_relattn_fwd": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64, _p]),
     "msq_filtered_workspace": (_sz, [_i64, _i64, _i64]),
     "msq_filtered_colstats": (_i, [_p, _p, _i, _i64, _i64, _i64, _i64, _p, _p]),
+    "msq_ring_lse": (_i, [_p, _p, _p, _i, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p]),
     "msq_filtered_ce_bias": (_i, [_p, _p, _i64, _p, _p, _i, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
                                   _f, _p, _p, _p]),
     "msq_filtered_ce": (_i, [_p, _p, _i64, _p, _i, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _f,

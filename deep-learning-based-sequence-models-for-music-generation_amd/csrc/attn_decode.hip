@@ -51,7 +51,21 @@ __device__ __forceinline__ f32x2 load2(const bf16* p) {
 }
 __device__ __forceinline__ f32x2 load2(const float* p) { return *(const f32x2*)p; }
 
-// T = bf16 (the MFMA engine) or float (the exact fp32 engine)
+__device__ __forceinline__ void load8(const bf16* p, float (&x)[8]) {
+    const bf16x8 a = *(const bf16x8*)p;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = (float)a[e];
+}
+__device__ __forceinline__ void load8(const float* p, float (&x)[8]) {
+    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = a[e], x[4 + e] = b[e];
+}
+
+// T = bf16 (the MFMA engine) or float (the exact fp32 engine). A key's row
+// (hs <= 128 values) is spread over a 16-lane group, 8 values per lane, so a
+// wave reads 4 whole rows per load instruction (coalesced) and keeps 4 row
+// loads of every kind in flight per unrolled step.
 template <typename T>
 __global__ __launch_bounds__(NT) void relattn_decode_kernel(T* __restrict__ out, int64_t ldo,
                                                             const T* __restrict__ qkv, int64_t ldq,
@@ -64,6 +78,7 @@ __global__ __launch_bounds__(NT) void relattn_decode_kernel(T* __restrict__ out,
     __shared__ float red[NT / 64];
     __shared__ float part[4][HS];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int l16 = lane & 15, grp = w * 4 + (lane >> 4);  // 16 key groups per block
     const int h = blockIdx.x, b = blockIdx.y;
     const int ctx = S_ring - n_meta;
     const int S = n_meta + n_tok;
@@ -80,18 +95,32 @@ __global__ __launch_bounds__(NT) void relattn_decode_kernel(T* __restrict__ out,
         copy8(vcb + (int64_t)new_slot * hs + tid * 8, vnew + tid * 8);
     }
     __syncthreads();
+    const int d0 = 8 * l16;
+    const bool dok = d0 < hs;
+    float q[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q[e] = dok ? q_s[d0 + e] : 0.f;
 
-    // scores: thread t takes slots t, t + 256, ...
+    // scores: group g takes slots g, g + 16, ...; lane l16 the dims 8 l16 ..
     float mx = -INFINITY;
-    for (int s = tid; s < S; s += NT) {
+#pragma unroll 4
+    for (int s = grp; s < S; s += 16) {
         const int jw = s < n_meta ? s : n_meta + (s - n_meta - first_mod + ctx) % ctx;
         const T* kr = s == new_slot ? knew : kcb + (int64_t)s * hs;
-        const T* rr = Rh + (int64_t)jw * hs;
+        float kx[8], rx[8];
+        if (dok) {
+            load8(kr + d0, kx);
+            load8(Rh + (int64_t)jw * hs + d0, rx);
+        }
         float acc = 0.f;
-#pragma unroll 4
-        for (int c = 0; c < hs / 8; ++c) acc += dot8(kr + c * 8, q_s + c * 8) + dot8(rr + c * 8, q_s + c * 8);
+        if (dok) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc = fmaf(kx[e] + rx[e], q[e], acc);
+        }
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
         acc *= scale;
-        p_s[s] = acc;
+        if (l16 == 0) p_s[s] = acc;
         mx = fmaxf(mx, acc);
     }
     mx = wave_max(mx);
@@ -110,25 +139,35 @@ __global__ __launch_bounds__(NT) void relattn_decode_kernel(T* __restrict__ out,
     __syncthreads();
     const float inv = 1.f / (red[0] + red[1] + red[2] + red[3]);
 
-    // P.V: wave w takes slots s = w (mod 4), lane owns dims 2 lane, 2 lane + 1
-    float o0 = 0.f, o1 = 0.f;
-    const bool own = 2 * lane < hs;
+    // P.V: group g takes slots g, g + 16, ...; lane l16 accumulates dims 8 l16 ..
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.f;
 #pragma unroll 4
-    for (int s = w; s < S; s += 4) {
+    for (int s = grp; s < S; s += 16) {
         const T* vr = s == new_slot ? vnew : vcb + (int64_t)s * hs;
-        const f32x2 v = own ? load2(vr + 2 * lane) : (f32x2){0.f, 0.f};
-        const float p = p_s[s];
-        o0 = fmaf(p, (float)v[0], o0);
-        o1 = fmaf(p, (float)v[1], o1);
+        if (dok) {
+            float vx[8];
+            load8(vr + d0, vx);
+            const float p = p_s[s];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = fmaf(p, vx[e], o[e]);
+        }
     }
-    if (own) {
-        part[w][2 * lane] = o0;
-        part[w][2 * lane + 1] = o1;
+    // the 4 groups of the wave, then the 4 waves
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        o[e] += __shfl_xor(o[e], 16, 64);
+        o[e] += __shfl_xor(o[e], 32, 64);
+    }
+    if (lane < 16 && dok) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) part[w][d0 + e] = o[e];
     }
     __syncthreads();
     if (tid < hs) {
-        const float o = (part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]) * inv;
-        out[(int64_t)b * ldo + (int64_t)h * hs + tid] = (T)o;
+        const float r = (part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]) * inv;
+        out[(int64_t)b * ldo + (int64_t)h * hs + tid] = (T)r;
     }
 }
 

@@ -64,10 +64,22 @@ __device__ __forceinline__ f32x4 epi_load(const T* p, int nv) {
     return x;
 }
 
-// Applies the epilogue to one lane's 4 consecutive outputs C[m][n..n+3].
+// epilogues that read the aux operand (their loads can be issued ahead of the stores)
+template <int EPI>
+constexpr bool epi_reads_aux() {
+    return EPI == MSQ_EPI_RELU_MASK || EPI == MSQ_EPI_BIAS_RESID || EPI == MSQ_EPI_BIAS_DROP_RESID;
+}
+template <typename TX>
+__device__ __forceinline__ f32x4 epi_aux_load(const GemmArgs& g, const TX* X, int64_t m, int64_t n) {
+    const int nv = g.vec ? (int)min<int64_t>(4, g.N - n) : -(int)min<int64_t>(4, g.N - n);
+    return epi_load(X + m * g.ldx + n, nv);
+}
+
+// Applies the epilogue to one lane's 4 consecutive outputs C[m][n..n+3]
+// (xpre: the aux vector, already loaded).
 template <int EPI, typename TC, typename TX>
 __device__ __forceinline__ void epi_apply(const GemmArgs& g, TC* C, const TX* X, int64_t m, int64_t n, f32x4 v,
-                                          float* wsp = nullptr) {
+                                          float* wsp = nullptr, const f32x4* xpre = nullptr) {
     if (EPI == MSQ_EPI_ACCUM && wsp) {  // split-K partial, reduced by splitk_reduce
         store4(wsp + m * g.N + n, v);
         return;
@@ -76,14 +88,14 @@ __device__ __forceinline__ void epi_apply(const GemmArgs& g, TC* C, const TX* X,
     if ((EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID ||
          EPI == MSQ_EPI_BIAS_DROP_RESID) && g.bias)
         v += epi_load(g.bias + n, nv);
-    if (EPI == MSQ_EPI_BIAS_DROP_RESID) v = epi_drop(g, m, n, v) + epi_load(X + m * g.ldx + n, nv);
+    if (EPI == MSQ_EPI_BIAS_DROP_RESID) v = epi_drop(g, m, n, v) + (xpre ? *xpre : epi_load(X + m * g.ldx + n, nv));
     if (EPI == MSQ_EPI_BIAS_RELU) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);
     }
-    if (EPI == MSQ_EPI_BIAS_RESID) v += epi_load(X + m * g.ldx + n, nv);
+    if (EPI == MSQ_EPI_BIAS_RESID) v += xpre ? *xpre : epi_load(X + m * g.ldx + n, nv);
     if (EPI == MSQ_EPI_RELU_MASK) {
-        const f32x4 x = epi_load(X + m * g.ldx + n, nv);
+        const f32x4 x = xpre ? *xpre : epi_load(X + m * g.ldx + n, nv);
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = x[t] > 0.f ? v[t] : 0.f;
     }
@@ -101,6 +113,9 @@ __device__ __forceinline__ void epi_apply(const GemmArgs& g, TC* C, const TX* X,
 // preconditions (the caller then uses the 128x128 kernel).
 bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, size_t ws_bytes,
                     hipStream_t s);
+// skinny-M weight-streaming kernel of the decode steps (gemm_skinny.hip):
+// false when the problem is not M <= 64 / ta = tb = 0 / a forward epilogue
+bool gemm_skinny_launch(const GemmArgs& g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s);
 // fills tiles / ksplit / kper (and descriptor extents) of the 256 tile; false if it does not apply
 bool gemm256_plan(GemmArgs& g, int ta, int tb, int epi);
 

@@ -528,6 +528,11 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
     plan128_ksplit(g, dtype, epilogue);
     g.ws = (float*)ws;
     hipStream_t s = (hipStream_t)stream;
+    if (dtype == MSQ_BF16 && M <= 64 && !getenv("MSQ_GEMM_NOSKINNY") &&
+        gemm_skinny_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, s)) {
+        MSQ_LAUNCH_CHECK();
+        return MSQ_OK;
+    }
     if (dtype == MSQ_BF16 && !getenv("MSQ_GEMM128")) {
         // wave quantisation: M = B*S rows rarely divide by 256 (32 x 2054 =
         // 256.75 tiles), and the partial last row of 256 tiles alone would

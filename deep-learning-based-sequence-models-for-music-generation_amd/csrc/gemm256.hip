@@ -298,8 +298,24 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(GemmArgs g) {
     const TX* X = (const TX*)g.aux + (g.aux ? bz * g.sX : 0);
     float* wsp = (EPI == MSQ_EPI_ACCUM && g.ksplit > 1 && g.ws) ? g.ws + ((int64_t)kslice * g.batch + bz) * g.M * g.N
                                                                  : nullptr;
+    // per half-tile, the aux vectors the epilogue reads are all loaded before
+    // its first store (C stores could alias them, so the compiler would
+    // otherwise issue each load only after the previous store)
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 2; ++a) {
+        f32x4 xp[4][2][2];
+        if (epi_reads_aux<EPI>()) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int64_t m = m0 + a * 128 + wr * 64 + i * 16 + (lane & 15);
+                        const int64_t n = n0 + b * 128 + wc * 32 + j * 16 + 4 * (lane >> 4);
+                        xp[i][b][j] = (m < g.M && n < g.N) ? epi_aux_load(g, X, m, n) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                    }
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int64_t m = m0 + a * 128 + wr * 64 + i * 16 + (lane & 15);
@@ -311,9 +327,11 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(GemmArgs g) {
                     const int64_t n = n0 + b * 128 + wc * 32 + j * 16 + 4 * (lane >> 4);
                     if (n >= g.N) continue;
                     if ((LAB & 16) && acc[a][b][i][j][0] != 12345.f) continue;
-                    epi_apply<EPI, TC, TX>(g, C, X, m, n, acc[a][b][i][j], wsp);
+                    epi_apply<EPI, TC, TX>(g, C, X, m, n, acc[a][b][i][j], wsp,
+                                           epi_reads_aux<EPI>() ? &xp[i][b][j] : nullptr);
                 }
         }
+    }
 }
 
 template <int TA, int TB, int EPI, typename TC, typename TX>

@@ -1,0 +1,199 @@
+// Skinny-M bf16 GEMM for the decode steps (M = batch rows <= 64):
+//   C[M][N] = A[M][K] . W[N][K]^T  (+ the msq_gemm epilogues)
+// The weight W (nn.Linear layout, K contiguous) is the only large operand: it
+// is streamed from HBM exactly once, straight into MFMA B-fragments (no LDS
+// staging), while the <= 64 activation rows (<= 128 KiB) come from L2.
+//   * block = 1024 threads = 16 waves on one 16-row slice of W; the waves split
+//     K (16 x 1-4 k-steps at K = 1024-2048: every W load of a wave is issued
+//     at once, 32-64 KiB in flight per CU) and their partial accumulators are
+//     summed through LDS;
+//   * per k-step of 32 a wave issues one 16-B W load and MT 16-B A loads per
+//     lane, U k-steps ahead, then U*MT v_mfma_f32_16x16x32_bf16;
+//   * MFMA roles: W rows are the MFMA A-operand (output rows), activation rows
+//     the B-operand, so a lane ends with C[m][n..n+3] (4 consecutive n of one
+//     row m), the layout epi_apply takes.
+// Bound: HBM bytes of W (2 N K) per launch; grid = N / 16 blocks.
+#include "gemm.h"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace {
+
+constexpr int SK_WAVES = 16, SK_U = 4;
+
+template <int EPI, typename TC, typename TX, int MT>
+__global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(GemmArgs g) {
+    __shared__ f32x4 red[SK_WAVES - 1][MT][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t n0 = (int64_t)blockIdx.x * 16;
+    const bf16* W = (const bf16*)g.B;
+    const bf16* A = (const bf16*)g.A;
+    const int64_t kper = (g.K + SK_WAVES * 32 - 1) / (SK_WAVES * 32) * 32;
+    const int64_t kb = w * kper, ke = min<int64_t>(g.K, kb + kper);
+    const int64_t wn = n0 + (lane & 15);
+    const bool wok = wn < g.N;
+    const bf16* wrow = W + (wok ? wn : 0) * g.ldb;
+    const int kq = 8 * (lane >> 4);
+    const bf16* arow[MT];
+    bool aok[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int64_t m = mt * 16 + (lane & 15);
+        aok[mt] = m < g.M;
+        arow[mt] = A + (aok[mt] ? m : 0) * g.lda;
+    }
+    f32x4 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const bf16x8 z = (bf16x8){};
+    for (int64_t k = kb; k < ke; k += 32 * SK_U) {
+        bf16x8 wf[SK_U], af[SK_U][MT];
+#pragma unroll
+        for (int u = 0; u < SK_U; ++u) {
+            const int64_t kk = k + 32 * u + kq;  // K % 8 == 0: a chunk of 8 is wholly in or out
+            const bool kin = kk < ke;
+            wf[u] = (wok && kin) ? *(const bf16x8*)(wrow + kk) : z;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) af[u][mt] = (aok[mt] && kin) ? *(const bf16x8*)(arow[mt] + kk) : z;
+        }
+#pragma unroll
+        for (int u = 0; u < SK_U; ++u)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[u], af[u][mt], acc[mt], 0, 0, 0);
+    }
+    if (w > 0) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) red[w - 1][mt][lane] = acc[mt];
+    }
+    __syncthreads();
+    if (w != 0) return;
+    TC* C = (TC*)g.C;
+    const TX* X = (const TX*)g.aux;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        f32x4 v = acc[mt];
+#pragma unroll
+        for (int q = 0; q < SK_WAVES - 1; ++q) v += red[q][mt][lane];
+        const int64_t m = mt * 16 + (lane & 15), n = n0 + 4 * (lane >> 4);
+        if (m < g.M && n < g.N) epi_apply<EPI, TC, TX>(g, C, X, m, n, v);
+    }
+}
+
+// Persistent variant for K <= SK_WAVES * 2 * 32 = 1024: a wave's K slice of
+// the activation rows (KS k-steps x MT fragments) is loaded ONCE into
+// registers and serves every 16-row W slice the block visits; the block walks
+// W slices blockIdx.x, + gridDim.x, ... with the next slice's W fragments
+// loaded before the current slice's MFMAs, reduction and epilogue, so each
+// CU keeps streaming W without launch rounds.
+template <int EPI, typename TC, typename TX, int MT, int KS>
+__global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_pk_kernel(GemmArgs g, int64_t ntiles) {
+    __shared__ f32x4 red[SK_WAVES][MT][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const bf16* W = (const bf16*)g.B;
+    const bf16* A = (const bf16*)g.A;
+    const int kq = 8 * (lane >> 4);
+    const int64_t kb = (int64_t)w * KS * 32;
+    const bf16x8 z = (bf16x8){};
+    bf16x8 af[KS][MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int64_t m = mt * 16 + (lane & 15);
+        const bf16* arow = A + (m < g.M ? m : 0) * g.lda;
+#pragma unroll
+        for (int u = 0; u < KS; ++u) {
+            const int64_t kk = kb + 32 * u + kq;
+            af[u][mt] = (m < g.M && kk < g.K) ? *(const bf16x8*)(arow + kk) : z;
+        }
+    }
+    auto load_w = [&](int64_t tile, bf16x8 (&wf)[KS]) {
+        const int64_t n = tile * 16 + (lane & 15);
+        const bf16* wrow = W + (n < g.N ? n : 0) * g.ldb;
+#pragma unroll
+        for (int u = 0; u < KS; ++u) {
+            const int64_t kk = kb + 32 * u + kq;
+            wf[u] = (n < g.N && kk < g.K) ? *(const bf16x8*)(wrow + kk) : z;
+        }
+    };
+    TC* C = (TC*)g.C;
+    const TX* X = (const TX*)g.aux;
+    bf16x8 wc[KS], wn[KS];
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) load_w(tile, wc);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int64_t nxt = tile + gridDim.x;
+        if (nxt < ntiles) load_w(nxt, wn);
+        f32x4 acc[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < KS; ++u)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wc[u], af[u][mt], acc[mt], 0, 0, 0);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) red[w][mt][lane] = acc[mt];
+        __syncthreads();
+        if (w < MT) {  // wave q sums fragment q over the 16 K slices and applies the epilogue
+            f32x4 v = red[0][w][lane];
+#pragma unroll
+            for (int q = 1; q < SK_WAVES; ++q) v += red[q][w][lane];
+            const int64_t m = w * 16 + (lane & 15), n = tile * 16 + 4 * (lane >> 4);
+            if (m < g.M && n < g.N) epi_apply<EPI, TC, TX>(g, C, X, m, n, v);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < KS; ++u) wc[u] = wn[u];
+    }
+}
+
+template <int EPI, typename TC, typename TX, int MT>
+void launch_pk(const GemmArgs& g, hipStream_t s) {
+    const int64_t ntiles = (g.N + 15) / 16;
+    const dim3 grid((unsigned)std::min<int64_t>(ntiles, 256));
+    const int64_t ks = (g.K + SK_WAVES * 32 - 1) / (SK_WAVES * 32);
+    // (KS = 4 would not fit the activation fragments in 128 VGPRs at MT = 4)
+    if (ks <= 1) hipLaunchKernelGGL((gemm_skinny_pk_kernel<EPI, TC, TX, MT, 1>), grid, dim3(64 * SK_WAVES), 0, s, g, ntiles);
+    else hipLaunchKernelGGL((gemm_skinny_pk_kernel<EPI, TC, TX, MT, 2>), grid, dim3(64 * SK_WAVES), 0, s, g, ntiles);
+}
+
+template <int EPI, typename TC, typename TX>
+void launch_mt(const GemmArgs& g, hipStream_t s) {
+    const int mt = (int)((g.M + 15) / 16);
+    if (g.K <= SK_WAVES * 2 * 32 && !getenv("MSQ_SKINNY_NOPK")) {
+        if (mt == 1) launch_pk<EPI, TC, TX, 1>(g, s);
+        else if (mt == 2) launch_pk<EPI, TC, TX, 2>(g, s);
+        else if (mt == 3) launch_pk<EPI, TC, TX, 3>(g, s);
+        else launch_pk<EPI, TC, TX, 4>(g, s);
+        return;
+    }
+    const dim3 grid((unsigned)((g.N + 15) / 16));
+    if (mt == 1) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TC, TX, 1>), grid, dim3(64 * SK_WAVES), 0, s, g);
+    else if (mt == 2) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TC, TX, 2>), grid, dim3(64 * SK_WAVES), 0, s, g);
+    else if (mt == 3) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TC, TX, 3>), grid, dim3(64 * SK_WAVES), 0, s, g);
+    else hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TC, TX, 4>), grid, dim3(64 * SK_WAVES), 0, s, g);
+}
+
+template <typename TC>
+bool launch_epi(const GemmArgs& g, int epi, int aux_dtype, hipStream_t s) {
+    switch (epi) {
+        case MSQ_EPI_NONE: launch_mt<MSQ_EPI_NONE, TC, float>(g, s); return true;
+        case MSQ_EPI_BIAS: launch_mt<MSQ_EPI_BIAS, TC, float>(g, s); return true;
+        case MSQ_EPI_BIAS_RELU: launch_mt<MSQ_EPI_BIAS_RELU, TC, float>(g, s); return true;
+        case MSQ_EPI_BIAS_RESID:
+            if (aux_dtype == MSQ_BF16) launch_mt<MSQ_EPI_BIAS_RESID, TC, bf16>(g, s);
+            else launch_mt<MSQ_EPI_BIAS_RESID, TC, float>(g, s);
+            return true;
+        default: return false;  // ACCUM / RELU_MASK / dropout: not decode shapes
+    }
+}
+
+}  // namespace
+
+// M <= 64, A [M][K] and W [N][K] bf16 (ta = tb = 0), one batch; false when
+// the problem is outside these conditions (the caller then uses the tiles)
+bool gemm_skinny_launch(const GemmArgs& g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s) {
+    if (ta || tb || g.batch != 1 || g.M > 64 || g.K % 8 || g.lda % 8 || g.ldb % 8) return false;
+    if (epi != MSQ_EPI_NONE && epi != MSQ_EPI_BIAS && epi != MSQ_EPI_BIAS_RELU && epi != MSQ_EPI_BIAS_RESID)
+        return false;
+    return c_dtype == MSQ_BF16 ? launch_epi<bf16>(g, epi, aux_dtype, s) : launch_epi<float>(g, epi, aux_dtype, s);
+}

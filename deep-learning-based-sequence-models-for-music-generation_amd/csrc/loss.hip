@@ -744,6 +744,58 @@ void colstats_launch(const LossArgs& a, float* col_lse, float* part, hipStream_t
                        col_lse);
 }
 
+// ---- cached decode (TransformerEngine.step): time-axis LSE over a ring of
+// logits rows [B][ctx][ld], kept as per-block partials lse_blk[b][blk][v] over
+// RB-row blocks, so a step re-reads one or two blocks instead of the window.
+template <typename T>
+__global__ __launch_bounds__(NT) void ring_block_lse_kernel(const T* __restrict__ ring, int64_t ld, int64_t ctx,
+                                                            int64_t V, int64_t rb, int64_t blk0, int64_t skip,
+                                                            float* __restrict__ part, int64_t nblk) {
+    constexpr int N = VecOf<T>::N;
+    constexpr float L2E = 1.4426950408889634f;
+    const int64_t v = ((int64_t)blockIdx.x * NT + threadIdx.x) * N;
+    const int64_t b = blockIdx.y, blk = blk0 + blockIdx.z;
+    if (v >= V) return;
+    const int64_t t0 = blk * rb, t1 = min(ctx, t0 + rb);
+    float m[N], sm[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) m[i] = -INFINITY, sm[i] = 0.f;
+    for (int64_t t = t0; t < t1; ++t) {
+        if (t == skip) continue;
+        float x[N];
+        ldv<T, N>(ring + (b * ctx + t) * ld + v, x);
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            if (x[i] == -INFINITY) continue;  // empty ring rows
+            const float mn = fmaxf(m[i], x[i]);
+            sm[i] = (m[i] == -INFINITY ? 0.f : sm[i] * __builtin_amdgcn_exp2f((m[i] - mn) * L2E)) +
+                    __builtin_amdgcn_exp2f((x[i] - mn) * L2E);
+            m[i] = mn;
+        }
+    }
+    float* pp = part + (b * nblk + blk) * V;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (v + i < V) pp[v + i] = m[i] == -INFINITY ? -INFINITY : m[i] + logf(sm[i]);
+}
+
+__global__ void ring_lse_merge_kernel(const float* __restrict__ part, int64_t B, int64_t nblk, int64_t V,
+                                      float* __restrict__ col_lse) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= B * V) return;
+    const int64_t b = e / V, v = e % V;
+    const float* p = part + b * nblk * V + v;
+    float m = -INFINITY;
+    for (int64_t k = 0; k < nblk; ++k) m = fmaxf(m, p[k * V]);
+    float sm = 0.f;
+    if (m != -INFINITY)
+        for (int64_t k = 0; k < nblk; ++k) {
+            const float x = p[k * V];
+            if (x != -INFINITY) sm += expf(x - m);
+        }
+    col_lse[e] = m == -INFINITY ? -INFINITY : m + logf(sm);
+}
+
 }  // namespace
 
 extern "C" size_t msq_filtered_workspace(int64_t B, int64_t T, int64_t V) {
@@ -896,6 +948,31 @@ extern "C" int msq_filtered_logit_bwd(void* dlogits, int64_t ldd, const float* d
         hipLaunchKernelGGL((row_kernel<2, float, float>), dim3(nblk), dim3(NT), 0, s, a, col_lse, nullptr, (float*)dlogits, ldd, dz, ldz, colsum, 1.f, 0);
         hipLaunchKernelGGL((finish_kernel<float, float>), dim3(gf), dim3(256), 0, s, a, col_lse, colsum, (float*)dlogits, ldd);
     }
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
+extern "C" int msq_ring_lse(float* col_lse, float* part, const void* ring, int dtype, int64_t ld, int64_t B,
+                            int64_t ctx, int64_t V, int64_t rows_per_block, int64_t blk_lo, int64_t blk_hi,
+                            int64_t skip_row, int64_t blk_extra, void* stream) {
+    const int64_t nblk = rows_per_block > 0 ? (ctx + rows_per_block - 1) / rows_per_block : 0;
+    MSQ_CHECK_ARG(B > 0 && ctx > 0 && V > 0 && ld >= V && ld % 8 == 0 && rows_per_block > 0 && ((uintptr_t)ring % 16) == 0,
+                  "msq_ring_lse: bad sizes (ld %% 8 == 0, 16-B aligned ring)");
+    MSQ_CHECK_ARG(0 <= blk_lo && blk_lo <= blk_hi && blk_hi <= nblk && blk_extra < nblk, "msq_ring_lse: bad block range");
+    hipStream_t s = (hipStream_t)stream;
+    const bool bfl = dtype == MSQ_BF16;
+    const int N = bfl ? 8 : 4;
+    const unsigned gx = (unsigned)((V + NT * N - 1) / (NT * N));
+    auto blocks = [&](int64_t lo, int64_t n, int64_t skip) {
+        if (n <= 0) return;
+        const dim3 g(gx, (unsigned)B, (unsigned)n);
+        if (bfl) hipLaunchKernelGGL(ring_block_lse_kernel<bf16>, g, dim3(NT), 0, s, (const bf16*)ring, ld, ctx, V, rows_per_block, lo, skip, part, nblk);
+        else hipLaunchKernelGGL(ring_block_lse_kernel<float>, g, dim3(NT), 0, s, (const float*)ring, ld, ctx, V, rows_per_block, lo, skip, part, nblk);
+    };
+    blocks(blk_lo, blk_hi - blk_lo, skip_row);
+    if (blk_extra >= 0 && (blk_extra < blk_lo || blk_extra >= blk_hi)) blocks(blk_extra, 1, -1);
+    hipLaunchKernelGGL(ring_lse_merge_kernel, dim3((unsigned)((B * V + 255) / 256)), dim3(256), 0, s, part, B, nblk, V,
+                       col_lse);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }

@@ -619,6 +619,46 @@ __global__ __launch_bounds__(256) void gnorm_fwd_kernel(const float* __restrict_
     }
 }
 
+// decode rows (few rows): one 256-thread block per row, the row in registers
+// (NK = ceil(dn / 1024) <= 4 float4 per thread), one block reduction
+template <typename TZ, typename TO, int NK>
+__global__ __launch_bounds__(256) void gnorm_fwd_row_kernel(const float* __restrict__ y, int64_t ldy,
+                                                            const TZ* __restrict__ z, int64_t ldz,
+                                                            const float* __restrict__ w, TO* __restrict__ out,
+                                                            int64_t ldo, float* __restrict__ rstd, int dn, float eps) {
+    __shared__ float red[4];
+    const int tid = threadIdx.x;
+    const int64_t row = blockIdx.x;
+    f32x4 gv[NK];
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+        const int c = tid * 4 + k * 1024;
+        if (c < dn) {
+            const f32x4 yv = *(const f32x4*)(y + row * ldy + c);
+            const f32x4 zv = load4(z + row * ldz + c);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) { gv[k][t] = yv[t] * silu(zv[t]); ss += gv[k][t] * gv[k][t]; }
+        }
+    }
+    ss = wave_sum(ss);
+    if ((tid & 63) == 0) red[tid >> 6] = ss;
+    __syncthreads();
+    const float r = rsqrtf(((red[0] + red[1]) + (red[2] + red[3])) / dn + eps);
+    if (tid == 0) rstd[row] = r;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+        const int c = tid * 4 + k * 1024;
+        if (c < dn) {
+            const f32x4 wv = *(const f32x4*)(w + c);
+            f32x4 o;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) o[t] = gv[k][t] * r * wv[t];
+            store4(out + row * ldo + c, o);
+        }
+    }
+}
+
 // dn = dout*w ; dg = r (dn - n mean(dn n)) ; dy = dg silu(z) ; dz = dg y silu'(z) ; dw += dout n
 // One wave per row, the row's y / z / dout held in registers (one HBM pass):
 // lane owns columns 4 lane + 256 k, k < NK (NK = ceil(d_inner / 256), compile time).
@@ -1367,6 +1407,16 @@ extern "C" int msq_mamba_gnorm_fwd(void* out, int64_t ldo, float* rstd, const fl
                                    int64_t d_inner, float eps, void* stream) {
     MSQ_CHECK_ARG(rows > 0 && d_inner % 4 == 0 && d_inner <= 4096, "mamba gnorm: bad sizes");
     hipStream_t s = (hipStream_t)stream;
+    if (rows <= 1024) {  // decode steps: a block per row
+        const int nk = (int)((d_inner + 1023) / 1024);
+#define GN_ROW(NK)                                                                                                     \
+    if (dtype == MSQ_BF16) hipLaunchKernelGGL((gnorm_fwd_row_kernel<bf16, bf16, NK>), dim3((unsigned)rows), dim3(256), 0, s, y, ldy, (const bf16*)zxbcdt, ldz, w, (bf16*)out, ldo, rstd, (int)d_inner, eps); \
+    else hipLaunchKernelGGL((gnorm_fwd_row_kernel<float, float, NK>), dim3((unsigned)rows), dim3(256), 0, s, y, ldy, (const float*)zxbcdt, ldz, w, (float*)out, ldo, rstd, (int)d_inner, eps);
+        if (nk == 1) { GN_ROW(1) } else if (nk == 2) { GN_ROW(2) } else if (nk == 3) { GN_ROW(3) } else { GN_ROW(4) }
+#undef GN_ROW
+        MSQ_LAUNCH_CHECK();
+        return MSQ_OK;
+    }
     const dim3 grid((unsigned)((rows + 3) / 4));
     if (dtype == MSQ_BF16) hipLaunchKernelGGL((gnorm_fwd_kernel<bf16, bf16>), grid, dim3(256), 0, s, y, ldy, (const bf16*)zxbcdt, ldz, w, (bf16*)out, ldo, rstd, rows, (int)d_inner, eps);
     else hipLaunchKernelGGL((gnorm_fwd_kernel<float, float>), grid, dim3(256), 0, s, y, ldy, (const float*)zxbcdt, ldz, w, (float*)out, ldo, rstd, rows, (int)d_inner, eps);

@@ -10,6 +10,7 @@
 //     torch.multinomial, :76-80), append to the history.
 // Ties in top-k prefer the lower vocabulary index.
 #include "common.h"
+#include <cmath>
 
 namespace {
 
@@ -17,6 +18,11 @@ constexpr int NT = 256;
 constexpr int MAXPEN = 16640;  // pitch + dyn token ids that can be penalised (default vocab)
 
 struct Cand { float v; int i; };
+
+// (float)min(base ** c, 1.2) for c < PEN_C, built on the host with libm's pow
+// (what Python's ** calls), so the device needs no double-precision pow
+constexpr int PEN_C = 32;
+struct PenTab { float p[2][PEN_C]; };
 
 __device__ __forceinline__ bool better(const Cand& a, const Cand& b) {
     return a.v > b.v || (a.v == b.v && a.i < b.i);
@@ -38,7 +44,8 @@ __global__ __launch_bounds__(NT) void sample_kernel(int64_t* __restrict__ hist, 
                                                     float* __restrict__ z, int64_t ldz, int64_t V,
                                                     const int* __restrict__ ks, const float* __restrict__ us,
                                                     int64_t* __restrict__ out_tok, int64_t time_start,
-                                                    int64_t tempo_start, int64_t dyn_start, int64_t len_start) {
+                                                    int64_t tempo_start, int64_t dyn_start, int64_t len_start,
+                                                    PenTab pt) {
     __shared__ unsigned short cnt[MAXPEN];
     __shared__ int s_j;
     __shared__ Cand red[NT / 64][3];
@@ -84,8 +91,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(int64_t* __restrict__ hist, 
     for (int64_t v = tid; v < npen; v += NT) {
         const int c = cnt[v];
         if (c > 0) {
-            const double base = v >= dyn_start ? 1.02 : 1.01;
-            const float pen = (float)fmin(pow(base, (double)c), 1.2);
+            const float pen = c < PEN_C ? pt.p[v >= dyn_start][c] : 1.2f;
             zr[v] = zr[v] / pen;
         }
     }
@@ -134,8 +140,16 @@ extern "C" int msq_decode_sample(int64_t* hist, int64_t ld_hist, int64_t cur_len
                                  void* stream) {
     MSQ_CHECK_ARG(B > 0 && V > 0 && cur_len > 0 && cur_len < ld_hist, "msq_decode_sample: bad sizes");
     MSQ_CHECK_ARG(length_start <= MAXPEN, "msq_decode_sample: vocabulary layout too large (pitch+dyn > %d)", MAXPEN);
+    static const PenTab pt = [] {
+        PenTab t;
+        for (int c = 0; c < PEN_C; ++c) {
+            t.p[0][c] = (float)std::fmin(std::pow(1.01, (double)c), 1.2);
+            t.p[1][c] = (float)std::fmin(std::pow(1.02, (double)c), 1.2);
+        }
+        return t;
+    }();
     hipLaunchKernelGGL(sample_kernel, dim3((unsigned)B), dim3(NT), 0, (hipStream_t)stream, hist, ld_hist, cur_len,
-                       z_last, ld_z, V, ks, uniforms, out_tok, time_start, tempo_start, dyn_start, length_start);
+                       z_last, ld_z, V, ks, uniforms, out_tok, time_start, tempo_start, dyn_start, length_start, pt);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }

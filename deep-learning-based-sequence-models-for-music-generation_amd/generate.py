@@ -95,7 +95,7 @@ def generate(model, context_len, token_ids, meta_ids, num_tokens=1000, device="c
         if cached and cache is not None and (cur <= context_len or slides):
             # one recurrent position: the token sampled last step (out_tok) at row cur-1
             logits = eng.step(out_tok, cache)
-            call("msq_filtered_logit_step", ptr(z), ldz, ptr(cache.lse), ptr(logits), dt(logits), cfg.v_pad,
+            call("msq_filtered_logit_step", ptr(z), ldz, ptr(cache.lse), ptr(logits), dt(logits), logits.stride(0),
                  ptr(out_tok), ptr(wtab), b[0], b[1], b[2], b[3], B, V, stream())
         else:
             window = hist[:, cur - W:cur].contiguous()

@@ -7,6 +7,7 @@ Same engine structure as the Transformer: one flat fp32 parameter buffer
 GEMMs (in_proj 1024->4256, out_proj 2048->1024, the 17 914-way head), the SSD
 scan in fp32 from chunk-entry states kept in HBM for the backward."""
 import math
+import os
 from collections import OrderedDict
 from dataclasses import dataclass
 
@@ -162,9 +163,15 @@ class DecodeCache:
         self.stf = e(2, B, dt=f32)
         self.logits = e(B, cfg.v_pad)
         self.length = 0  # positions absorbed (metadata excluded)
+        # the step as one HIP graph (captured on the second step; the first
+        # runs eagerly and allocates the step's workspaces)
+        self.graph, self.graph_tok, self.eager_steps = None, None, 0
 
 
 class MambaEngine:
+    # decode steps replay a captured HIP graph (MSQ_NO_STEP_GRAPH=1: eager launches)
+    step_graphs = not os.environ.get("MSQ_NO_STEP_GRAPH")
+
     def __init__(self, cfg: MambaConfig, flat):
         self.cfg = cfg
         self.layout = MambaLayout(cfg)
@@ -261,10 +268,28 @@ class MambaEngine:
         """One recurrent position for every row: tok int64 [B] (contiguous) ->
         logits [B, v_pad] (cache.logits) of that position; the cache advances.
         Equal to the last row of forward() over the grown sequence."""
-        cfg, P, W = self.cfg, self.P, self.W
         if not tok.is_cuda:
             raise RuntimeError("the MI355X engine runs on the GPU only (no CPU fallback)")
         self.refresh_shadow()
+        # every launch of a step has fixed pointers and sizes (the recurrent
+        # state lives in the cache): replay one captured HIP graph instead of
+        # ~7 launches per layer from the host
+        if self.step_graphs and tok.data_ptr() == cache.graph_tok and cache.graph is not None:
+            cache.graph.replay()
+        elif self.step_graphs and cache.eager_steps >= 1 and tok.is_contiguous():
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._step_body(tok, cache)
+            cache.graph, cache.graph_tok = g, tok.data_ptr()
+            g.replay()
+        else:
+            self._step_body(tok, cache)
+            cache.eager_steps += 1
+        cache.length += 1
+        return cache.logits
+
+    def _step_body(self, tok, cache):
+        cfg, P, W = self.cfg, self.P, self.W
         B, d, di, H = cache.B, cfg.d_model, cfg.d_inner, cfg.nheads
         dtc = L.BF16 if self.act == torch.bfloat16 else L.F32
         s = stream()
@@ -278,12 +303,15 @@ class MambaEngine:
                  cfg.d_in_proj, dtc, ptr(P[f"{l}.dt_bias"]), ptr(P[f"{l}.A_log"]), ptr(P[f"{l}.D"]), B, di, H, s)
             call("msq_mamba_gnorm_fwd", ptr(cache.yn), di, ptr(cache.rstd), ptr(cache.y), di, ptr(cache.zx),
                  cfg.d_in_proj, dtc, ptr(P[f"{l}.norm_w"]), B, di, float(cfg.norm_eps), s)
-            ops.gemm(cache.yn, W[f"{l}.out_w"], out=cache.x)
-            ops.cast(cache.xa, cache.x)
+            if l < cfg.n_layers - 1 and cache.xa.dtype != torch.float32:
+                # the next layer's bf16 input straight from the fp32 accumulator
+                # (the same rounding as forward()'s fp32 row + cast)
+                ops.gemm(cache.yn, W[f"{l}.out_w"], out=cache.xa)
+            else:
+                ops.gemm(cache.yn, W[f"{l}.out_w"], out=cache.x)
+                ops.cast(cache.xa, cache.x)
         ops.layernorm_fwd(cache.x, P["lnf_w"], P["lnf_b"], out=cache.f, mean=cache.stf[0], rstd=cache.stf[1])
         ops.gemm(cache.f, W["lm_w"], out=cache.logits, epilogue=L.EPI_BIAS, bias=P["lm_b"])
-        cache.length += 1
-        return cache.logits
 
     def backward(self, dlogits, grads, head_bias_done=False):
         cfg, P, W = self.cfg, self.P, self.W

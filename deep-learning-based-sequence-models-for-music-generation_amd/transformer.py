@@ -226,6 +226,11 @@ class TransformerDecodeCache:
         self.qkv, self.h = e(B, 3 * d), e(B, 4 * d)
         self.st, self.stf = e(2, B, dt=f32), e(2, B, dt=f32)
         self.logits = e(B, cfg.v_pad)
+        # time-axis LSE of the ring kept as per-block partials (msq_ring_lse)
+        self.RB = 64
+        self.nblk = (context + self.RB - 1) // self.RB
+        self.part = e(B, self.nblk, cfg.vocab_size, dt=f32)
+        self.part_valid = False
         self.length = 0  # tokens absorbed (sequence positions 0 .. length-1)
 
 
@@ -338,6 +343,7 @@ class TransformerEngine:
             if T > cache.ctx:
                 raise ValueError(f"prefill of {T} tokens exceeds the cache context {cache.ctx}")
             cache.ring.fill_(float("-inf"))
+            cache.part_valid = False
             cache.ring[:, :T].copy_(A.logits.view(B, T, cfg.v_pad))
             cache.tokens[:, :T].copy_(idx)
             cache.length = T
@@ -380,16 +386,24 @@ class TransformerEngine:
             ops.gemm(cache.c, W[f"{l}.w1"], out=cache.h, epilogue=L.EPI_BIAS_RELU, bias=P[f"{l}.b1"])
             ops.gemm(cache.h, W[f"{l}.w2"], out=x, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.b2"], aux=cache.xm)
         ops.layernorm_fwd(x, P["lnf_w"], P["lnf_b"], out=cache.f, mean=cache.stf[0], rstd=cache.stf[1])
-        ops.gemm(cache.f, W["lm_w"], out=cache.logits, epilogue=L.EPI_BIAS, bias=P["lm_b"])
-        # the row leaving the window (or the empty slot) drops out of the LSE
-        cache.ring[:, slot].fill_(float("-inf"))
-        V = cfg.vocab_size
-        ws = ops.workspace(L.lib().msq_filtered_workspace(B, ctx, V), self.device, "loss")
-        call("msq_filtered_colstats", ptr(cache.lse), ptr(cache.ring), dt(cache.ring), cfg.v_pad, B, ctx, V, ptr(ws), s)
-        cache.ring[:, slot].copy_(cache.logits)
+        # the new row goes straight into its ring slot, over the row that leaves
+        # the window (or the empty slot); the LSE below leaves that slot out
+        row = cache.ring[:, slot]
+        ops.gemm(cache.f, W["lm_w"], out=row, epilogue=L.EPI_BIAS, bias=P["lm_b"])
+        V, rb = cfg.vocab_size, cache.RB
+        blk = slot // rb
+        if not cache.part_valid:  # first step: every block of the prefilled window
+            lo, hi, extra = 0, cache.nblk, -1
+            cache.part_valid = True
+        else:  # this slot's block, and the block holding the previous step's row
+            prev_blk = ((pos - 1) % ctx) // rb
+            lo, hi, extra = blk, blk + 1, (prev_blk if prev_blk != blk else -1)
+        call("msq_ring_lse", ptr(cache.lse), ptr(cache.part), ptr(cache.ring), dt(cache.ring), cfg.v_pad, B, ctx, V,
+             rb, lo, hi, slot, extra, s)
         cache.tokens[:, slot].copy_(tok)
         cache.length = pos + 1
-        return cache.logits
+        cache.logits = row
+        return row
 
     # ------------------------------------------------------------ backward
     def backward(self, dlogits, grads, head_bias_done=False):

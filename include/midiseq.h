@@ -186,6 +186,18 @@ int msq_relattn_bwd_dropout(int dtype, void* dqkv, int64_t ld_dqkv, float* dR, c
 size_t msq_filtered_workspace(int64_t B, int64_t T, int64_t V);
 int msq_filtered_colstats(float* col_lse, const void* logits, int dtype, int64_t ld, int64_t B, int64_t T, int64_t V,
                           void* workspace, void* stream);
+
+/* Cached decode (generate mode="cached", TransformerEngine.step): column
+ * log-sum-exp over the time axis of a ring of logits rows ring [B][ctx][ld]
+ * (-inf rows are empty), kept as per-block partials part f32 [B][nblk][V]
+ * over blocks of rows_per_block rows. Recomputes blocks [blk_lo, blk_hi)
+ * leaving out row skip_row (-1: none), and block blk_extra (-1: none) whole,
+ * then col_lse[b][v] = logsumexp over the blocks. Replaces the per-step
+ * torch.logsumexp(out, dim=1) of train.py:133-138 as applied by
+ * scripts/generate.py:33 to the sliding window. */
+int msq_ring_lse(float* col_lse, float* part, const void* ring, int dtype, int64_t ld, int64_t B, int64_t ctx,
+                 int64_t V, int64_t rows_per_block, int64_t blk_lo, int64_t blk_hi, int64_t skip_row,
+                 int64_t blk_extra, void* stream);
 /* loss (fp32 scalar, device) = mean over B*T of the row CE of Z. If dlogits
  * != NULL also writes grad_scale * d(sum of row CE)/dlogits (so grad_scale =
  * 1/(B*T) gives the gradient of the mean).                                  */

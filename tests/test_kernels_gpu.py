@@ -62,6 +62,32 @@ def test_gemm_epilogues(dtype):
     assert _rel(ob.float(), base + bias) < 1e-2
 
 
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 64])
+@pytest.mark.parametrize("N,K", [(17, 64), (1024, 1032), (4384, 1024), (1024, 2048)])
+def test_gemm_skinny_decode_shapes(M, N, K):
+    """M <= 64 rows (decode steps) take the weight-streaming kernel
+    (gemm_skinny.hip): row / column / K edges and every forward epilogue,
+    A with a padded leading dimension, fp32 and bf16 outputs."""
+    g = torch.Generator().manual_seed(M * 31 + N + K)
+    a = torch.randn(M, K, generator=g).bfloat16()
+    w = torch.randn(N, K, generator=g).bfloat16()
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g)
+    base = a.float() @ w.float().t()
+    A = torch.zeros(M, K + 8, device=dev, dtype=torch.bfloat16)[:, :K]  # lda = K + 8
+    A.copy_(a)
+    W, bi, R = w.to(dev), bias.to(dev), res.to(dev)
+    assert A.stride(0) == K + 8
+    assert _rel(ops.gemm(A, W, out_dtype=torch.float32), base) < 2e-3
+    assert _rel(ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_BIAS, bias=bi), base + bias) < 2e-3
+    assert _rel(ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_BIAS_RELU, bias=bi),
+                torch.relu(base + bias)) < 2e-3
+    assert _rel(ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_BIAS_RESID, bias=bi, aux=R),
+                base + bias + res) < 2e-3
+    ob = ops.gemm(A, W, out_dtype=torch.bfloat16, epilogue=L.EPI_BIAS, bias=bi)
+    assert _rel(ob.float(), base + bias) < 1e-2
+
+
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 1), (1, 0)])
 @pytest.mark.parametrize("M,N,K", [(4104, 2056, 1000), (2304, 4096, 512)])
 def test_gemm256_layouts_and_edges(ta, tb, M, N, K):

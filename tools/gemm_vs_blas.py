@@ -48,6 +48,18 @@ def main():
             ("dW", lambda: ops.gemm(dy, x, ta=True, tb=True, out=dw, epilogue=L.EPI_ACCUM),
              lambda: torch.matmul(dy.t(), x, out=dwb)),
         ]
+        if name == "ffn2":  # the fused epilogues of the train step on this shape
+            h = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
+            res = torch.randn(M, N, device=dev, dtype=torch.float32, generator=g)
+            bias = torch.randn(N, device=dev, dtype=torch.float32, generator=g)
+            yf = torch.empty(M, N, device=dev, dtype=torch.float32)
+            cases += [
+                ("dXrm", lambda: ops.gemm(dy, w, tb=True, out=dx, epilogue=L.EPI_RELU_MASK, aux=h),
+                 lambda: torch.matmul(dy, w, out=dx)),
+                ("fwdd", lambda: ops.gemm(x, w, out=yf, epilogue=L.EPI_BIAS_RESID, bias=bias, aux=res,
+                                          drop=(1, 2, 0.01)),
+                 lambda: torch.matmul(x, w.t(), out=y)),
+            ]
         for kind, a, b in cases:
             ta_ = timeit(a)
             tb_ = timeit(b)
