@@ -50,12 +50,15 @@ SIGNATURES = {
     "msq_relattn_bwd_dropout": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64,
                                      _f, _i64, _p, _p, _f, _p, _p]),
     "msq_colsum_workspace": (_sz, [_i64, _i64]),
+    "msq_gemm_colsum_workspace": (_sz, [_i64, _i64]),
     "msq_colsum": (_i, [_p, _i, _p, _i, _i64, _i64, _i64, _p, _p]),
     "msq_cast": (_i, [_p, _i, _p, _i, _i64, _p]),
     "msq_adam_step": (_i, [_p, _p, _p, _p, _p, _i64, _f, _f, _f, _f, _i64, _f, _p]),
     "msq_relattn_fwd": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64, _p]),
     "msq_filtered_workspace": (_sz, [_i64, _i64, _i64]),
     "msq_filtered_colstats": (_i, [_p, _p, _i, _i64, _i64, _i64, _i64, _p, _p]),
+    "msq_gemm_colsum": (_i, [_i, _i, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _i64, _i, _p, _i, _i64, _p, _i, _p,
+                             _i64, _p]),
     "msq_ring_lse": (_i, [_p, _p, _p, _i, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p]),
     "msq_filtered_ce_bias": (_i, [_p, _p, _i64, _p, _p, _i, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
                                   _f, _p, _p, _p]),

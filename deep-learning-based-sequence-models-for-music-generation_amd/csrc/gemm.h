@@ -28,6 +28,9 @@ struct GemmArgs {
     float* ws;
     // global row of local row 0 (the dropout hash is keyed by the global row)
     int64_t m_off;
+    // column sums of the written C (msq_gemm_colsum): per-(M-tile, wave-row)
+    // partials [tiles_m * 2][N], reduced in a fixed order afterwards
+    float* cs_ws;
 };
 
 // bytes of the split-K partial workspace an ACCUM product with this split needs
@@ -78,11 +81,11 @@ __device__ __forceinline__ f32x4 epi_aux_load(const GemmArgs& g, const TX* X, in
 // Applies the epilogue to one lane's 4 consecutive outputs C[m][n..n+3]
 // (xpre: the aux vector, already loaded).
 template <int EPI, typename TC, typename TX>
-__device__ __forceinline__ void epi_apply(const GemmArgs& g, TC* C, const TX* X, int64_t m, int64_t n, f32x4 v,
-                                          float* wsp = nullptr, const f32x4* xpre = nullptr) {
+__device__ __forceinline__ f32x4 epi_apply(const GemmArgs& g, TC* C, const TX* X, int64_t m, int64_t n, f32x4 v,
+                                           float* wsp = nullptr, const f32x4* xpre = nullptr) {
     if (EPI == MSQ_EPI_ACCUM && wsp) {  // split-K partial, reduced by splitk_reduce
         store4(wsp + m * g.N + n, v);
-        return;
+        return v;
     }
     const int nv = g.vec ? (int)min<int64_t>(4, g.N - n) : -(int)min<int64_t>(4, g.N - n);
     if ((EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID ||
@@ -103,10 +106,11 @@ __device__ __forceinline__ void epi_apply(const GemmArgs& g, TC* C, const TX* X,
     if (EPI == MSQ_EPI_ACCUM && g.ksplit > 1) {
         const int na = nv < 0 ? -nv : nv;
         for (int t = 0; t < na; ++t) atomicAdd((float*)cp + t, v[t]);
-        return;
+        return v;
     }
     if (EPI == MSQ_EPI_ACCUM) v += epi_load(cp, nv);
     epi_store(cp, v, nv);
+    return v;  // the value written (before its rounding to TC)
 }
 
 // 256x256 kernel family: returns false when the problem does not fit its
@@ -116,6 +120,12 @@ bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dt
 // skinny-M weight-streaming kernel of the decode steps (gemm_skinny.hip):
 // false when the problem is not M <= 64 / ta = tb = 0 / a forward epilogue
 bool gemm_skinny_launch(const GemmArgs& g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s);
+// 256 tile with the column sums of C (epilogue NONE / RELU_MASK, C bf16,
+// N % 4 == 0): dbias[n] (+)= sum_m C[m][n] (fp32, before C's rounding);
+// ws >= gemm256_colsum_ws_bytes(M, N); false when the 256 tile does not apply
+bool gemm256_colsum_launch(GemmArgs g, int ta, int tb, int epi, int aux_dtype, float* dbias, int accumulate,
+                           float* ws, size_t ws_bytes, hipStream_t s);
+inline size_t gemm256_colsum_ws_bytes(int64_t M, int64_t N) { return (size_t)((M + 255) / 256) * 2 * N * 4; }
 // fills tiles / ksplit / kper (and descriptor extents) of the 256 tile; false if it does not apply
 bool gemm256_plan(GemmArgs& g, int ta, int tb, int epi);
 

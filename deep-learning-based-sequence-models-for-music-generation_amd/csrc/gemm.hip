@@ -14,6 +14,10 @@
 //
 // fp32 exact path: plain LDS-tiled FMA kernel, fp32 end to end (parity mode).
 #include "gemm.h"
+
+extern "C" size_t msq_colsum_workspace(int64_t rows, int64_t cols);
+extern "C" int msq_colsum(float* out, int accumulate, const void* x, int dtype, int64_t rows, int64_t cols,
+                          int64_t ld, void* workspace, void* stream);
 #include <stdlib.h>
 
 namespace {
@@ -580,4 +584,49 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
     if (g.ws) splitk_reduce(g, s);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
+}
+
+// C = epi(op(A) op(B)) (bf16, epilogue NONE / RELU_MASK) and dbias[n] (+)=
+// sum_m C[m][n]: the bias gradient of the layer whose output gradient C is
+// (model_transformer.py:95 FFN first Linear), fused into the 256 tile's
+// epilogue (fp32 sums before C's rounding, fixed-order reduction); other
+// shapes run msq_gemm_ex + msq_colsum.
+extern "C" size_t msq_gemm_colsum_workspace(int64_t M, int64_t N) {
+    return std::max(gemm256_colsum_ws_bytes(M, N), msq_colsum_workspace(M, N));
+}
+
+extern "C" int msq_gemm_colsum(int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                               const void* B, int64_t ldb, void* C, int64_t ldc, int epilogue, const void* aux,
+                               int aux_dtype, int64_t ld_aux, float* dbias, int accumulate, void* ws,
+                               int64_t ws_bytes, void* stream) {
+    MSQ_CHECK_ARG(dbias && ws && ws_bytes >= (int64_t)msq_gemm_colsum_workspace(M, N),
+                  "msq_gemm_colsum: dbias / workspace (msq_gemm_colsum_workspace) missing");
+    MSQ_CHECK_ARG(epilogue == MSQ_EPI_NONE || epilogue == MSQ_EPI_RELU_MASK, "msq_gemm_colsum: epilogue NONE / RELU_MASK");
+    MSQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && N % 4 == 0 && ldc % 8 == 0 && ((uintptr_t)C % 16) == 0,
+                  "msq_gemm_colsum: N %% 4, ldc %% 8, 16-B aligned C");
+    MSQ_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? N : K) && ldc >= N && lda % 8 == 0 && ldb % 8 == 0 &&
+                      ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0,
+                  "msq_gemm_colsum: leading dims / alignment (bf16 needs ld %% 8 == 0, 16-B aligned)");
+    MSQ_CHECK_ARG(aux || epilogue == MSQ_EPI_NONE, "msq_gemm_colsum: RELU_MASK needs aux");
+    hipStream_t s = (hipStream_t)stream;
+    if (!getenv("MSQ_GEMM128")) {
+        GemmArgs g{};
+        g.M = M; g.N = N; g.K = K;
+        g.A = A; g.lda = lda;
+        g.B = B; g.ldb = ldb;
+        g.C = C; g.ldc = ldc;
+        g.aux = aux; g.ldx = ld_aux;
+        g.batch = 1;
+        const int xsz = aux_dtype == MSQ_BF16 ? 2 : 4;
+        g.vec = (ldc % 4 == 0) && ((uintptr_t)C % 8 == 0) &&
+                (!aux || ((ld_aux % 4 == 0) && ((uintptr_t)aux % (4 * xsz) == 0)));
+        if (gemm256_colsum_launch(g, ta, tb, epilogue, aux_dtype, dbias, accumulate, (float*)ws, (size_t)ws_bytes, s)) {
+            MSQ_LAUNCH_CHECK();
+            return MSQ_OK;
+        }
+    }
+    int rc = msq_gemm_ex(MSQ_BF16, ta, tb, M, N, K, A, lda, 0, B, ldb, 0, C, MSQ_BF16, ldc, 0, 1, epilogue, nullptr, aux,
+                         aux_dtype, ld_aux, 0, 0u, 0u, 0.f, nullptr, 0, stream);
+    if (rc) return rc;
+    return msq_colsum(dbias, accumulate, C, MSQ_BF16, M, N, ldc, ws, stream);
 }

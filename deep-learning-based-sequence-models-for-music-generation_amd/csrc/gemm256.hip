@@ -128,7 +128,8 @@ __device__ __forceinline__ void read_set(bf16x8 (&f)[2][NF], const lds_t* slot, 
 // LAB: ablation switches for tools/gemm256_lab.hip only (0 in the library):
 // 1 = no LDS-DMA in the K loop, 2 = no MFMA, 4 = no ping-pong stagger,
 // 8 = K slice innermost in the block order, 16 = no epilogue stores
-template <int TA, int TB, int EPI, typename TC, typename TX, int LAB = 0>
+// CS: also the column sums of the written C, per (M-tile, wave-row) into g.cs_ws
+template <int TA, int TB, int EPI, typename TC, typename TX, int LAB = 0, bool CS = false>
 __global__ __launch_bounds__(NT, 1) void gemm256_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     lds_t* smem = (lds_t*)smem_raw;
@@ -301,6 +302,11 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(GemmArgs g) {
     // per half-tile, the aux vectors the epilogue reads are all loaded before
     // its first store (C stores could alias them, so the compiler would
     // otherwise issue each load only after the previous store)
+    f32x4 csum[2][2];  // CS: this lane's column sums over its 8 rows, [b][j]
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) csum[b][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
         f32x4 xp[4][2][2];
@@ -327,10 +333,46 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(GemmArgs g) {
                     const int64_t n = n0 + b * 128 + wc * 32 + j * 16 + 4 * (lane >> 4);
                     if (n >= g.N) continue;
                     if ((LAB & 16) && acc[a][b][i][j][0] != 12345.f) continue;
-                    epi_apply<EPI, TC, TX>(g, C, X, m, n, acc[a][b][i][j], wsp,
-                                           epi_reads_aux<EPI>() ? &xp[i][b][j] : nullptr);
+                    const f32x4 v = epi_apply<EPI, TC, TX>(g, C, X, m, n, acc[a][b][i][j], wsp,
+                                                           epi_reads_aux<EPI>() ? &xp[i][b][j] : nullptr);
+                    if (CS) csum[b][j] += v;
                 }
         }
+    }
+    if (CS) {
+        // sum over the 16 row-lanes (lane & 15) of each column group, then one
+        // partial row per (M-tile, wave-row): cs_ws[(tm * 2 + wr)][n]
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f32x4 v = csum[b][j];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) v[t] += __shfl_xor(v[t], o, 64);
+                const int64_t n = n0 + b * 128 + wc * 32 + j * 16 + 4 * (lane >> 4);
+                if ((lane & 15) == 0 && n < g.N) *(f32x4*)(g.cs_ws + ((int64_t)tm * 2 + wr) * g.N + n) = v;
+            }
+    }
+}
+
+// dbias[n] (+)= sum_p part[p][n], fixed order: 64 columns x 16 partial groups
+__global__ __launch_bounds__(1024) void colsum_partials_kernel(const float* __restrict__ part, int64_t nparts,
+                                                               int64_t N, float* __restrict__ dbias, int accumulate) {
+    __shared__ float red[16][64];
+    const int c = threadIdx.x & 63, gq = threadIdx.x >> 6;
+    const int64_t n = (int64_t)blockIdx.x * 64 + c;
+    float s = 0.f;
+    if (n < N)
+        for (int64_t p = gq; p < nparts; p += 16) s += part[p * N + n];
+    red[gq][c] = s;
+    __syncthreads();
+    if (gq == 0 && n < N) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) t += red[k][c];
+        dbias[n] = accumulate ? dbias[n] + t : t;
     }
 }
 
@@ -408,6 +450,33 @@ bool gemm256_plan(GemmArgs& g, int ta, int tb, int epi) {
     if (tiles * g.ksplit < 128) return false;
     g.a_ext = (uint32_t)(aext * 2);
     g.b_ext = (uint32_t)(bext * 2);
+    return true;
+}
+
+bool gemm256_colsum_launch(GemmArgs g, int ta, int tb, int epi, int aux_dtype, float* dbias, int accumulate,
+                           float* ws, size_t ws_bytes, hipStream_t s) {
+    if (epi != MSQ_EPI_NONE && epi != MSQ_EPI_RELU_MASK) return false;
+    if (g.N % 4 || g.batch != 1 || ws_bytes < gemm256_colsum_ws_bytes(g.M, g.N) || !gemm256_plan(g, ta, tb, epi))
+        return false;
+    g.cs_ws = ws;
+    auto go = [&](auto kern) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * HALF);
+        hipLaunchKernelGGL(kern, dim3(g.tiles_m * g.tiles_n), dim3(NT), 8 * HALF, s, g);
+    };
+    const bool bx = aux_dtype == MSQ_BF16;
+    if (ta == 0 && tb == 1) {
+        if (epi == MSQ_EPI_NONE) go(gemm256_kernel<0, 1, MSQ_EPI_NONE, bf16, float, 0, true>);
+        else if (bx) go(gemm256_kernel<0, 1, MSQ_EPI_RELU_MASK, bf16, bf16, 0, true>);
+        else go(gemm256_kernel<0, 1, MSQ_EPI_RELU_MASK, bf16, float, 0, true>);
+    } else if (ta == 0 && tb == 0) {
+        if (epi == MSQ_EPI_NONE) go(gemm256_kernel<0, 0, MSQ_EPI_NONE, bf16, float, 0, true>);
+        else if (bx) go(gemm256_kernel<0, 0, MSQ_EPI_RELU_MASK, bf16, bf16, 0, true>);
+        else go(gemm256_kernel<0, 0, MSQ_EPI_RELU_MASK, bf16, float, 0, true>);
+    } else {
+        return false;
+    }
+    hipLaunchKernelGGL(colsum_partials_kernel, dim3((unsigned)((g.N + 63) / 64)), dim3(1024), 0, s, ws,
+                       (int64_t)g.tiles_m * 2, g.N, dbias, accumulate);
     return true;
 }
 

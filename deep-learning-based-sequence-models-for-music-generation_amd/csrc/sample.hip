@@ -14,7 +14,7 @@
 
 namespace {
 
-constexpr int NT = 256;
+constexpr int NT = 1024;  // one workgroup per row: the V-long passes take 18 iterations
 constexpr int MAXPEN = 16640;  // pitch + dyn token ids that can be penalised (default vocab)
 
 struct Cand { float v; int i; };

@@ -58,6 +58,25 @@ def gemm(A, B, *, ta=False, tb=False, out=None, out_dtype=None, epilogue=L.EPI_N
     return out
 
 
+def gemm_colsum(A, B, out, dbias, *, ta=False, tb=False, epilogue=L.EPI_NONE, aux=None, accumulate=False):
+    """out = epi(op(A) . op(B)) (bf16, epilogue NONE / RELU_MASK) and
+    dbias (+)= its column sums (fp32, fused into the GEMM epilogue)."""
+    if A.dtype != torch.bfloat16:  # fp32 engine: the unfused pair
+        gemm(A, B, ta=ta, tb=tb, out=out, epilogue=epilogue, aux=aux)
+        return colsum(out, dbias, accumulate=accumulate)
+    ar, ac, lda, _, _ = _mat(A, ta)
+    br, bc, ldb, _, _ = _mat(B, tb)
+    M, K = (ac, ar) if ta else (ar, ac)
+    N = bc if tb else br
+    assert out.shape == (M, N) and out.dtype == torch.bfloat16 and B.dtype == torch.bfloat16
+    ws = workspace(L.lib().msq_gemm_colsum_workspace(M, N), A.device, "gemm_colsum")
+    ldx = aux.stride(0) if aux is not None else 0
+    call("msq_gemm_colsum", int(ta), int(tb), M, N, K, ptr(A), lda, ptr(B), ldb, ptr(out), out.stride(0), epilogue,
+         ptr(aux), dt(aux) if aux is not None else L.F32, ldx, ptr(dbias), int(accumulate), ptr(ws), ws.numel(),
+         stream())
+    return out
+
+
 _WS = {}
 
 

@@ -496,11 +496,12 @@ class TransformerEngine:
                 ops.gemm(gb, A.h[l], ta=True, tb=True, out=G[f"{l}.w2"], epilogue=L.EPI_ACCUM)
             on_side("gb", ffn2_w)
             before_write("dh")
-            ops.gemm(gb, W[f"{l}.w2"], tb=True, out=Bw["dh"], epilogue=L.EPI_RELU_MASK, aux=A.h[l])
+            # dh = ReLU-masked FFN2 dX; the FFN1 bias gradient (its column sums) in the same epilogue
+            ops.gemm_colsum(gb, W[f"{l}.w2"], Bw["dh"], G[f"{l}.b1"], tb=True, epilogue=L.EPI_RELU_MASK, aux=A.h[l],
+                            accumulate=True)
 
             def ffn1_w(l=l):
                 ops.gemm(Bw["dh"], A.c[l], ta=True, tb=True, out=G[f"{l}.w1"], epilogue=L.EPI_ACCUM)
-                ops.colsum(Bw["dh"], G[f"{l}.b1"], accumulate=True)
             on_side("dh", ffn1_w)
             ops.gemm(Bw["dh"], W[f"{l}.w1"], tb=True, out=Bw["dtmp"])
             before_write("gb2")

@@ -124,6 +124,16 @@ int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, cons
                 int64_t ld_aux, int64_t stride_aux, uint32_t seed, uint32_t site, float p, void* ws,
                 int64_t ws_bytes, void* stream);
 /* column sums (bias gradients): out[c] (+)= sum_r x[r, c]                      */
+/* C = epi(op(A) op(B)) in bf16 (epilogue NONE or RELU_MASK with aux, no
+ * batch) and dbias[n] = (accumulate ? dbias[n] : 0) + sum_m C[m][n] in fp32:
+ * the FFN dX product of the backward with the gradient of the first
+ * Linear's bias (model_transformer.py:95) fused into its epilogue. ws of
+ * msq_gemm_colsum_workspace(M, N) bytes. Replaces the per-step bias
+ * gradient of FeedFoward's nn.Linear (autograd's sum over rows). */
+size_t msq_gemm_colsum_workspace(int64_t M, int64_t N);
+int msq_gemm_colsum(int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
+                    int64_t ldb, void* C, int64_t ldc, int epilogue, const void* aux, int aux_dtype, int64_t ld_aux,
+                    float* dbias, int accumulate, void* ws, int64_t ws_bytes, void* stream);
 size_t msq_colsum_workspace(int64_t rows, int64_t cols);
 int msq_colsum(float* out, int accumulate, const void* x, int dtype, int64_t rows, int64_t cols, int64_t ld,
                void* workspace, void* stream);

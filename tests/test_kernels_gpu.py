@@ -62,6 +62,40 @@ def test_gemm_epilogues(dtype):
     assert _rel(ob.float(), base + bias) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(3000, 4096, 1024), (65728 // 8, 1024, 512), (100, 256, 64)])
+@pytest.mark.parametrize("epi", ["relu_mask", "none"])
+def test_gemm_colsum_bias_grad(M, N, K, epi):
+    """msq_gemm_colsum: the FFN dX product (dY . W) with the column sums of its
+    bf16 output fused into the 256 tile's epilogue (fp32 sums before rounding,
+    fixed-order reduction; small shapes: msq_gemm_ex + msq_colsum), with and
+    without accumulation into the bias gradient."""
+    g = torch.Generator().manual_seed(M + N + K)
+    dy = torch.randn(M, K, generator=g).bfloat16()
+    w = torch.randn(K, N, generator=g).bfloat16()  # [K][N]: tb
+    h = torch.randn(M, N, generator=g).bfloat16()
+    base = dy.float() @ w.float()
+    if epi == "relu_mask":
+        base = base * (h.float() > 0)
+    Dy, Wd, Hd = dy.to(dev), w.to(dev), h.to(dev)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    db = torch.full((N,), 0.5, device=dev)
+    e = L.EPI_RELU_MASK if epi == "relu_mask" else L.EPI_NONE
+    ops.gemm_colsum(Dy, Wd, out, db, tb=True, epilogue=e, aux=Hd if epi == "relu_mask" else None, accumulate=True)
+    torch.cuda.synchronize()
+    assert _rel(out.float(), base) < 1e-2
+    # fused: fp32 sums before rounding; the small-shape fallback sums the bf16 C
+    tol = 2e-3 if M >= 256 else 1e-2
+    assert _rel(db - 0.5, base.sum(0)) < tol
+    db2 = torch.empty(N, device=dev)
+    ops.gemm_colsum(Dy, Wd, out, db2, tb=True, epilogue=e, aux=Hd if epi == "relu_mask" else None)
+    torch.cuda.synchronize()
+    assert torch.equal(db2, db - 0.5) or _rel(db2, base.sum(0)) < tol
+    db3 = torch.empty(N, device=dev)  # bitwise reproducible (no atomics)
+    ops.gemm_colsum(Dy, Wd, out, db3, tb=True, epilogue=e, aux=Hd if epi == "relu_mask" else None)
+    torch.cuda.synchronize()
+    assert torch.equal(db2, db3)
+
+
 @pytest.mark.parametrize("M", [1, 5, 16, 33, 64])
 @pytest.mark.parametrize("N,K", [(17, 64), (1024, 1032), (4384, 1024), (1024, 2048)])
 def test_gemm_skinny_decode_shapes(M, N, K):
