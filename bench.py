@@ -79,6 +79,9 @@ CLASSIFY = {
     "msq_relattn_fwd_dropout": lambda a: ("attn_fwd", _attn_flops(a[7], a[8], a[9], a[10]), None),
     # backward = 2 x the forward's products (algorithmic; the recompute of P is not counted)
     "msq_relattn_bwd_dropout": lambda a: ("attn_bwd", 2 * _attn_flops(a[11], a[12], a[13], a[14]), None),
+    "msq_relattn_bwd_ws": lambda a: ("attn_bwd", 2 * _attn_flops(a[11], a[12], a[13], a[14]), None),
+    # FFN dX with the FFN1 bias gradient in its epilogue
+    "msq_gemm_colsum": lambda a: ("gemm_dX", 2.0 * a[2] * a[3] * a[4], None),
     # filtered CE: 3 reads of the logits + 1 write of dlogits ([B, T, ld] of the act dtype)
     "msq_filtered_ce": lambda a: ("loss", None, 4.0 * a[13] * a[14] * a[5] * (2 if a[4] == L.BF16 else 4)),
     "msq_filtered_ce_bias": lambda a: ("loss", None, 4.0 * a[14] * a[15] * a[6] * (2 if a[5] == L.BF16 else 4)),

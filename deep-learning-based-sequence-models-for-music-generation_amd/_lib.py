@@ -49,6 +49,8 @@ SIGNATURES = {
                                      _f, _p]),
     "msq_relattn_bwd_dropout": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64,
                                      _f, _i64, _p, _p, _f, _p, _p]),
+    "msq_relattn_bwd_ws": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64,
+                                     _f, _i64, _p, _p, _f, _p, _i, _p]),
     "msq_colsum_workspace": (_sz, [_i64, _i64]),
     "msq_gemm_colsum_workspace": (_sz, [_i64, _i64]),
     "msq_colsum": (_i, [_p, _i, _p, _i, _i64, _i64, _i64, _p, _p]),

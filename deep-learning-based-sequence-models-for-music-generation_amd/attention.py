@@ -24,6 +24,11 @@ def relattn_fwd(qkv, R, B, S, H, hs, scale, out=None, lse=None, n_meta=N_META, d
     return out, lse
 
 
+# workspace pointer -> (dtype, B, S, H) of the backward it last served (its zero
+# bands stay valid for the next backward of the same shape: msq_relattn_bwd_ws)
+_ws_served = {}
+
+
 def relattn_bwd(dout, out, lse, qkv, R, B, S, H, hs, scale, dqkv=None, dR=None, n_meta=N_META, drop=None):
     """Returns (dqkv [B*S, 3*H*hs] (overwritten), dR fp32 [H, S_max, hs] (accumulated))."""
     if dqkv is None:
@@ -33,8 +38,11 @@ def relattn_bwd(dout, out, lse, qkv, R, B, S, H, hs, scale, dqkv=None, dR=None, 
     nbytes = L.lib().msq_relattn_bwd_workspace(dt(qkv), B, S, H)
     ws = workspace(nbytes, qkv.device, "attn")
     masks, p = drop if drop is not None else (None, 0.0)
-    call("msq_relattn_bwd_dropout", dt(qkv), ptr(dqkv), dqkv.stride(0), ptr(dR), ptr(dout), dout.stride(0), ptr(out),
+    key = (dt(qkv), B, S, H)
+    ready = int(_ws_served.get(ws.data_ptr()) == key)  # the "attn" workspace serves only this op
+    call("msq_relattn_bwd_ws", dt(qkv), ptr(dqkv), dqkv.stride(0), ptr(dR), ptr(dout), dout.stride(0), ptr(out),
          ptr(lse), ptr(qkv), qkv.stride(0), ptr(R), B, S, H, hs, R.shape[1], float(scale), n_meta,
          ptr(masks[0]) if masks is not None else None, ptr(masks[1]) if masks is not None else None, float(p),
-         ptr(ws), stream())
+         ptr(ws), ready, stream())
+    _ws_served[ws.data_ptr()] = key
     return dqkv, dR

@@ -55,4 +55,4 @@ void flash_bwd_dq(const AttnArgs& a, const bf16* dsj, const bf16* dqr, int64_t l
 // v3 forward (attn_fwd3.hip): 8 waves x 32 queries, 32-key tiles; -1 if unsupported
 int flash_fwd3(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s);
 int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo, const bf16* out, bf16* dqkv,
-              int64_t ldd, float* dR, void* ws, hipStream_t s);
+              int64_t ldd, float* dR, void* ws, bool ws_ready, hipStream_t s);

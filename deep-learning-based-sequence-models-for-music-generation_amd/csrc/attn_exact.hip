@@ -261,14 +261,16 @@ extern "C" int msq_relattn_fwd_dropout(int dtype, void* out, int64_t ld_out, flo
 }
 
 static int relattn_bwd(int dtype, void* dqkv, int64_t ld_dqkv, float* dR, const void* dout, int64_t ld_dout,
-                       const void* out, const float* lse, const AttnArgs& a, void* workspace, void* stream) {
+                       const void* out, const float* lse, const AttnArgs& a, void* workspace, int ws_ready,
+                       void* stream) {
     hipStream_t s = (hipStream_t)stream;
     if (dtype == MSQ_F32) {
         exact_bwd(a, lse, (const float*)dout, ld_dout, (float*)dqkv, ld_dqkv, dR, workspace, s);
     } else {
         MSQ_CHECK_ARG(a.hs == 128 && a.ldq % 8 == 0 && ld_dout % 8 == 0 && ld_dqkv % 8 == 0,
                       "msq_relattn_bwd: bf16 path needs hs == 128, ld %% 8 == 0");
-        int rc = flash_bwd(a, lse, (const bf16*)dout, ld_dout, (const bf16*)out, (bf16*)dqkv, ld_dqkv, dR, workspace, s);
+        int rc = flash_bwd(a, lse, (const bf16*)dout, ld_dout, (const bf16*)out, (bf16*)dqkv, ld_dqkv, dR, workspace,
+                           ws_ready != 0, s);
         if (rc) return rc;
     }
     MSQ_LAUNCH_CHECK();
@@ -288,10 +290,19 @@ extern "C" int msq_relattn_bwd_dropout(int dtype, void* dqkv, int64_t ld_dqkv, f
                                        int64_t ld_qkv, const void* R, int64_t B, int64_t S, int64_t H, int64_t hs,
                                        int64_t S_max, float scale, int64_t n_meta, const uint32_t* rowmask,
                                        const uint32_t* colmask, float p, void* workspace, void* stream) {
+    return msq_relattn_bwd_ws(dtype, dqkv, ld_dqkv, dR, dout, ld_dout, out, lse, qkv, ld_qkv, R, B, S, H, hs, S_max,
+                              scale, n_meta, rowmask, colmask, p, workspace, 0, stream);
+}
+
+extern "C" int msq_relattn_bwd_ws(int dtype, void* dqkv, int64_t ld_dqkv, float* dR, const void* dout,
+                                  int64_t ld_dout, const void* out, const float* lse, const void* qkv, int64_t ld_qkv,
+                                  const void* R, int64_t B, int64_t S, int64_t H, int64_t hs, int64_t S_max,
+                                  float scale, int64_t n_meta, const uint32_t* rowmask, const uint32_t* colmask,
+                                  float p, void* workspace, int ws_ready, void* stream) {
     MSQ_CHECK_ARG(B > 0 && S > 0 && H > 0 && hs > 0 && S <= S_max && workspace && n_meta <= 8,
                   "msq_relattn_bwd: bad args");
     MSQ_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || (rowmask && colmask)), "msq_relattn_bwd: dropout needs masks");
     AttnArgs a = mk(B, S, H, hs, S_max, n_meta, scale, qkv, ld_qkv, R);
     if (p > 0.f) set_drop(a, rowmask, colmask, p);
-    return relattn_bwd(dtype, dqkv, ld_dqkv, dR, dout, ld_dout, out, lse, a, workspace, stream);
+    return relattn_bwd(dtype, dqkv, ld_dqkv, dR, dout, ld_dout, out, lse, a, workspace, ws_ready, stream);
 }

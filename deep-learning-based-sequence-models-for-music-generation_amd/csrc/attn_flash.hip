@@ -306,7 +306,7 @@ int flash_fwd(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t
 }
 
 int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo, const bf16* out, bf16* dqkv,
-              int64_t ldd, float* dR, void* ws, hipStream_t s) {
+              int64_t ldd, float* dR, void* ws, bool ws_ready, hipStream_t s) {
     const int64_t B = a.B, S = a.S, H = a.H, ldr = flash_dqr_ld(S);
     char* p = (char*)ws;
     bf16* dqr = (bf16*)p;
@@ -319,8 +319,12 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     p += align256((size_t)B * H * 64 * 4);
     float* dr_ws = (float*)p;
 
-    hipLaunchKernelGGL(dqr_band_zero_kernel, dim3((unsigned)((H * B * S + 3) / 4)), dim3(256), 0, s, dqr, dsj, ldr,
-                       S, H * B * S);
+    // the band and row pads are never written non-zero by the passes below
+    // (their dS entries there are 0 by the mask), so a workspace that already
+    // served this (B, S, H) keeps them (ws_ready)
+    if (!ws_ready)
+        hipLaunchKernelGGL(dqr_band_zero_kernel, dim3((unsigned)((H * B * S + 3) / 4)), dim3(256), 0, s, dqr, dsj, ldr,
+                           S, H * B * S);
     hipMemsetAsync(meta_ds, 0, (size_t)B * H * 64 * 4, s);
     if (ldo % 8 == 0 && ((uintptr_t)dout % 16) == 0 && ((uintptr_t)out % 16) == 0)
         hipLaunchKernelGGL(flash_bwd_pre_vec_kernel, dim3((unsigned)((B * S * H + 15) / 16)), dim3(256), 0, s, a, dout,

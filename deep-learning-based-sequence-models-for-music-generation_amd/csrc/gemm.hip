@@ -447,6 +447,50 @@ extern "C" int msq_gemm(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t
 
 namespace {
 // split-K of the 128 tile for an ACCUM product (skinny-output weight gradients)
+// Tail rows of a wave-quantisation split (M % 256 rows, run by the 128 tile):
+// with a workspace, K is split over enough blocks to fill the chip, the fp32
+// sums go to a temp [Mt][N] (+ split-K partials), and tail_epi_kernel applies
+// the product's epilogue. Without it the 128 tile's ~16 blocks would walk the
+// whole K alone (60 us for a 192-row tail at K = 3072).
+struct TailPlan { int ksplit; int64_t kper; size_t tmp_bytes, part_bytes; };
+TailPlan plan_tail(int64_t Mt, int64_t N, int64_t K) {
+    TailPlan p{1, K, 0, 0};
+    const int64_t nb = ((Mt + BM - 1) / BM) * ((N + BN - 1) / BN);
+    if (nb >= 128 || N % 4) return p;  // enough blocks already / no vector partials
+    int64_t ks = std::min<int64_t>((256 + nb - 1) / nb, std::max<int64_t>(1, K / 128));
+    if (ks <= 1) return p;
+    p.kper = ((K + ks - 1) / ks + BK - 1) / BK * BK;
+    p.ksplit = (int)((K + p.kper - 1) / p.kper);
+    p.tmp_bytes = (size_t)Mt * N * 4;
+    p.part_bytes = (size_t)p.ksplit * Mt * N * 4;
+    return p;
+}
+
+template <int EPI, typename TC, typename TX>
+__global__ void tail_epi_kernel(GemmArgs t, const float* __restrict__ tmp) {
+    const int64_t nq = t.N / 4, total = t.M * nq;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t m = e / nq, n = (e - m * nq) * 4;
+        epi_apply<EPI, TC, TX>(t, (TC*)t.C, (const TX*)t.aux, m, n, load4(tmp + m * t.N + n));
+    }
+}
+
+template <typename TC>
+void tail_epi_launch(const GemmArgs& t, const float* tmp, int epi, int aux_dtype, hipStream_t s) {
+    const unsigned nb = (unsigned)std::min<int64_t>((t.M * (t.N / 4) + 255) / 256, 4096);
+    switch (epi) {
+        case MSQ_EPI_NONE: hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_NONE, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp); break;
+        case MSQ_EPI_BIAS: hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_BIAS, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp); break;
+        case MSQ_EPI_BIAS_RELU: hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_BIAS_RELU, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp); break;
+        case MSQ_EPI_BIAS_RESID: hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_BIAS_RESID, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp); break;
+        case MSQ_EPI_BIAS_DROP_RESID: hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_BIAS_DROP_RESID, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp); break;
+        case MSQ_EPI_RELU_MASK:
+            if (aux_dtype == MSQ_BF16) hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_RELU_MASK, TC, bf16>), dim3(nb), dim3(256), 0, s, t, tmp);
+            else hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_RELU_MASK, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp);
+            break;
+    }
+}
+
 void plan128_ksplit(GemmArgs& g, int dtype, int epilogue) {
     g.ksplit = 1;
     g.kper = ((g.K + BK - 1) / BK) * BK;
@@ -464,7 +508,12 @@ void plan128_ksplit(GemmArgs& g, int dtype, int epilogue) {
 
 extern "C" int64_t msq_gemm_workspace_size(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K,
                                            int64_t lda, int64_t ldb, int64_t batch, int epilogue) {
-    if (epilogue != MSQ_EPI_ACCUM || dtype != MSQ_BF16 || M <= 0 || N <= 0 || K <= 0 || batch <= 0) return 0;
+    if (dtype != MSQ_BF16 || M <= 0 || N <= 0 || K <= 0 || batch <= 0) return 0;
+    if (epilogue != MSQ_EPI_ACCUM) {  // the split-K tail of a wave-quantisation split
+        if (batch != 1 || M % 256 == 0 || M <= 256 || M <= 64) return 0;
+        const TailPlan tp = plan_tail(M % 256, N, K);
+        return tp.ksplit > 1 ? (int64_t)(tp.tmp_bytes + tp.part_bytes) : 0;
+    }
     GemmArgs g{};
     g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.batch = (int)batch;
     if (!getenv("MSQ_GEMM128") && gemm256_plan(g, ta, tb, epilogue))
@@ -558,6 +607,26 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
             t.tiles_m = (int)((t.M + BM - 1) / BM);
             g.M = Mm;
             if (gemm256_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, 0, s)) {
+                const TailPlan tp = plan_tail(t.M, N, K);
+                if (tp.ksplit > 1 && ws && (size_t)ws_bytes >= tp.tmp_bytes + tp.part_bytes) {
+                    // split-K tail: sums into tmp, then the epilogue
+                    float* tmp = (float*)ws;
+                    GemmArgs u = t;
+                    u.C = tmp; u.ldc = N; u.sC = 0;
+                    u.bias = nullptr; u.aux = nullptr;
+                    u.vec = 1;
+                    u.ksplit = tp.ksplit;
+                    u.kper = tp.kper;
+                    u.ws = (float*)((char*)ws + tp.tmp_bytes);
+                    hipMemsetAsync(tmp, 0, tp.tmp_bytes, s);
+                    const int rc = dispatch_epi<true, float>(u, ta, tb, MSQ_EPI_ACCUM, MSQ_F32, s);
+                    if (rc) return msq_set_error(MSQ_ERR_ARG, "msq_gemm: unsupported combination");
+                    splitk_reduce(u, s);
+                    if (c_dtype == MSQ_BF16) tail_epi_launch<bf16>(t, tmp, epilogue, aux_dtype, s);
+                    else tail_epi_launch<float>(t, tmp, epilogue, aux_dtype, s);
+                    MSQ_LAUNCH_CHECK();
+                    return MSQ_OK;
+                }
                 const int rc = c_dtype == MSQ_BF16 ? dispatch_epi<true, bf16>(t, ta, tb, epilogue, aux_dtype, s)
                                                    : dispatch_epi<true, float>(t, ta, tb, epilogue, aux_dtype, s);
                 if (rc) return msq_set_error(MSQ_ERR_ARG, "msq_gemm: unsupported combination");

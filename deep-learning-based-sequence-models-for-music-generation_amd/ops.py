@@ -40,21 +40,17 @@ def gemm(A, B, *, ta=False, tb=False, out=None, out_dtype=None, epilogue=L.EPI_N
     if aux is not None:
         _, _, ldx, sX, _ = _mat(aux, False)
         axd = dt(aux)
+    seed, site, p = 0, 0, 0.0
     if drop is not None and drop[2] > 0:
         assert epilogue == L.EPI_BIAS_RESID, "dropout is fused into the bias+residual epilogue only"
-        call("msq_gemm_dropout", dt(A), int(ta), int(tb), M, N, K, ptr(A), lda, sA, ptr(B), ldb, sB, ptr(out),
-             dt(out), ldc, sC, batch, L.EPI_BIAS_DROP_RESID, ptr(bias), ptr(aux), axd, ldx, sX, int(drop[0]),
-             int(drop[1]), float(drop[2]), stream())
-        return out
-    if epilogue == L.EPI_ACCUM:
-        nws = L.lib().msq_gemm_workspace_size(dt(A), int(ta), int(tb), M, N, K, lda, ldb, batch, epilogue)
-        ws = _splitk_ws(A.device, nws) if nws > 0 else None
-        call("msq_gemm_ex", dt(A), int(ta), int(tb), M, N, K, ptr(A), lda, sA, ptr(B), ldb, sB, ptr(out), dt(out),
-             ldc, sC, batch, epilogue, ptr(bias), ptr(aux), axd, ldx, sX, 0, 0, 0.0, ptr(ws), nws if ws is not None
-             else 0, stream())
-        return out
-    call("msq_gemm", dt(A), int(ta), int(tb), M, N, K, ptr(A), lda, sA, ptr(B), ldb, sB, ptr(out), dt(out), ldc,
-         sC, batch, epilogue, ptr(bias), ptr(aux), axd, ldx, sX, stream())
+        epilogue = L.EPI_BIAS_DROP_RESID
+        seed, site, p = int(drop[0]), int(drop[1]), float(drop[2])
+    # split-K partials (weight gradients) / the split-K tail of a wave-quantisation split
+    nws = L.lib().msq_gemm_workspace_size(dt(A), int(ta), int(tb), M, N, K, lda, ldb, batch, epilogue)
+    ws = _splitk_ws(A.device, nws) if nws > 0 else None
+    call("msq_gemm_ex", dt(A), int(ta), int(tb), M, N, K, ptr(A), lda, sA, ptr(B), ldb, sB, ptr(out), dt(out),
+         ldc, sC, batch, epilogue, ptr(bias), ptr(aux), axd, ldx, sX, seed, site, p, ptr(ws),
+         nws if ws is not None else 0, stream())
     return out
 
 

@@ -187,6 +187,15 @@ int msq_relattn_bwd_dropout(int dtype, void* dqkv, int64_t ld_dqkv, float* dR, c
                             const void* out, const float* lse, const void* qkv, int64_t ld_qkv, const void* R,
                             int64_t B, int64_t S, int64_t H, int64_t hs, int64_t S_max, float scale, int64_t n_meta,
                             const uint32_t* rowmask, const uint32_t* colmask, float p, void* workspace, void* stream);
+/* msq_relattn_bwd_dropout with ws_ready = 1 when this workspace already served
+ * a backward of the same (dtype, B, S, H) and was not written by anything
+ * else since: its dS layouts' zero band and row padding (which no pass writes
+ * non-zero) are then not cleared again. */
+int msq_relattn_bwd_ws(int dtype, void* dqkv, int64_t ld_dqkv, float* dR, const void* dout, int64_t ld_dout,
+                       const void* out, const float* lse, const void* qkv, int64_t ld_qkv, const void* R, int64_t B,
+                       int64_t S, int64_t H, int64_t hs, int64_t S_max, float scale, int64_t n_meta,
+                       const uint32_t* rowmask, const uint32_t* colmask, float p, void* workspace, int ws_ready,
+                       void* stream);
 
 /* ---- grammar-weighted filtered loss (train.py:79-138; CrossEntropyLoss,
  * train_parallel.py:156,179). logits [B,T,ld] (ld >= V, ld % 4 == 0) in dtype;
