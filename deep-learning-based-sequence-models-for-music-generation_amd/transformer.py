@@ -424,12 +424,13 @@ class TransformerEngine:
         hook = getattr(self, "layer_grad_ready", None)
         # Weight gradients (dW GEMMs, and the bias column sums when they read a
         # bf16 branch gradient) only feed the optimizer, not the next layer's
-        # backward: on the bf16 path they run on a second stream, overlapped
+        # backward: with overlap_dw (off by default: both streams compete for
+        # the same CUs and the step measured no faster) they run on a second stream, overlapped
         # with the dX / LayerNorm / attention chain of the main stream. Each
         # side launch waits for the main stream's producer of its inputs; the
         # main stream waits for the side stream before it overwrites a buffer
         # the side still reads (gb / gb2 / dh / dqkv, one layer of slack).
-        ov = Bw["gb2"] is not None and getattr(self, "overlap_dw", True)
+        ov = Bw["gb2"] is not None and getattr(self, "overlap_dw", False)
         main = torch.cuda.current_stream(self.device)
         if ov and getattr(self, "_dw_stream", None) is None:
             self._dw_stream = torch.cuda.Stream(device=self.device)
