@@ -102,6 +102,18 @@ CLASSIFY = {
 }
 
 
+def pmc_traffic(cls):
+    """HBM bytes per launch of a kernel class from the committed PMC passes
+    (tools/pmc_traffic.py), or None."""
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            c = json.load(f)["classes"].get(cls)
+        return round(c["hbm_bytes_per_launch"]) if c else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 class ClassTimer:
     """HIP events around every libmidiseq launch (midiseq._lib.TAP), recorded
     on the stream the launch goes to (torch's current stream at the call:
@@ -481,8 +493,10 @@ def main():
             "roofline": {"kernel": f"{dom} (dominant class of the train step: {r['ms_per_step']} ms/step, "
                                    f"{r['launches_per_step']} launches/step)",
                          "bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"],
-                         "frac": r["frac"], "traffic": None, "avg_launch_ms": r["avg_launch_ms"],
-                         "algorithmic_work_per_launch": r["work_per_launch"]},
+                         "frac": r["frac"], "traffic": pmc_traffic(dom), "avg_launch_ms": r["avg_launch_ms"],
+                         "algorithmic_work_per_launch": r["work_per_launch"],
+                         "traffic_source": "profiles/r2/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
+                                           "passes of this step, bytes per class launch)"},
             "classes": classes,
         }
         out.update(extra)

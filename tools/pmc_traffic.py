@@ -1,0 +1,78 @@
+"""HBM traffic per kernel class from two rocprofv3 PMC passes over the same
+bench command (MI355X_MICROARCH.md 'HBM': FETCH_SIZE and WRITE_SIZE in
+separate passes, both in KB; on gfx950 FETCH_SIZE reports half the bytes of
+wide coalesced reads, so it is doubled).
+
+  rocprofv3 --pmc FETCH_SIZE -d <dir_f> -o run --output-format csv -- python bench.py ...
+  rocprofv3 --pmc WRITE_SIZE -d <dir_w> -o run --output-format csv -- python bench.py ...
+  python tools/pmc_traffic.py <dir_f> <dir_w> <train steps profiled> <out.json>
+
+Kernels map to bench.py's classes by name; bytes per class launch = bytes
+per step / the class's launches per step (attention: 8 layers)."""
+import csv
+import glob
+import json
+import re
+import sys
+from collections import defaultdict
+
+# (regex on the kernel name, class, class launches per train step)
+CLASSES = [
+    (r"flash_bwd_kv3|flash_bwd_dq|flash_bwd_pre|dqr_band_zero|flash_bwd_meta|gemm_bf16_kernel<1, 1, 5", "attn_bwd", 8),
+    (r"flash_fwd3", "attn_fwd", 8),
+    (r"attn_mask_kernel", "dropout_mask", 8),
+    (r"colstats2|rowlse|cspart|cs_reduce|finish2|dbias_reduce|pad_table|wrange|mean_kernel", "loss", 1),
+    (r"adam_kernel", "adam", 1),
+    (r"ln_bwd|ln_reduce", "layernorm_bwd", 17),
+    (r"gemm256_kernel<1, 1, 5|splitk_reduce", "gemm_dW", 33),
+]
+
+
+def load(d, counter):
+    files = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)
+    rows = []
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter:
+                rows.append((r["Kernel_Name"], float(r["Counter_Value"])))
+    return rows
+
+
+def classify(name):
+    for pat, cls, n in CLASSES:
+        if re.search(pat, name):
+            return cls, n
+    return None, None
+
+
+def main(dir_f, dir_w, steps, out):
+    steps = int(steps)
+    tot = defaultdict(lambda: {"fetch_kb": 0.0, "write_kb": 0.0, "dispatches": 0})
+    for counter, key, rows in (("FETCH_SIZE", "fetch_kb", load(dir_f, "FETCH_SIZE")),
+                               ("WRITE_SIZE", "write_kb", load(dir_w, "WRITE_SIZE"))):
+        for name, v in rows:
+            cls, _ = classify(name)
+            if cls is None:
+                continue
+            tot[cls][key] += v
+            if key == "fetch_kb":
+                tot[cls]["dispatches"] += 1
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the bench step (tools/pmc_traffic.py)",
+           "correction": "FETCH_SIZE x2 (gfx950 counts half of wide coalesced reads); KB x 1024 -> bytes",
+           "train_steps_profiled": steps, "classes": {}}
+    for pat, cls, n in CLASSES:
+        if cls not in tot:
+            continue
+        t = tot[cls]
+        per_step = (2 * t["fetch_kb"] + t["write_kb"]) * 1024 / steps
+        res["classes"][cls] = {"hbm_bytes_per_step": per_step, "launches_per_step": n,
+                               "hbm_bytes_per_launch": per_step / n,
+                               "fetch_kb_per_step": t["fetch_kb"] / steps, "write_kb_per_step": t["write_kb"] / steps,
+                               "dispatches_per_step": t["dispatches"] / steps}
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:5])
