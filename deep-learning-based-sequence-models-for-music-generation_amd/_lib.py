@@ -61,6 +61,7 @@ SIGNATURES = {
     "msq_filtered_colstats": (_i, [_p, _p, _i, _i64, _i64, _i64, _i64, _p, _p]),
     "msq_gemm_colsum": (_i, [_i, _i, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _i64, _i, _p, _i, _i64, _p, _i, _p,
                              _i64, _p]),
+    "msq_transpose_bf16": (_i, [_p, _i64, _p, _i64, _i64, _i64, _p]),
     "msq_ring_lse": (_i, [_p, _p, _p, _i, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p]),
     "msq_filtered_ce_bias": (_i, [_p, _p, _i64, _p, _p, _i, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
                                   _f, _p, _p, _p]),

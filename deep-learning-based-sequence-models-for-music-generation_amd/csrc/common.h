@@ -74,11 +74,11 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
 // step seed `seed` is kept iff drop_bits(drop_row(drop_base(seed, site), row),
 // col) >= thr, thr = round(p * 2^32); kept values are scaled by 1/(1-p).
 // oracle/dropout.py restates these four functions bit-exactly.
+// one multiply (v_mul_lo_u32 is a quarter-rate op; the mask kernel and the
+// dropout epilogues are bound by this hash's VALU issue)
 __host__ __device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
     x ^= x >> 16;
-    x *= 0x21f0aaadu;
-    x ^= x >> 15;
-    x *= 0x735a2d97u;
+    x *= 0x7feb352du;
     x ^= x >> 15;
     return x;
 }

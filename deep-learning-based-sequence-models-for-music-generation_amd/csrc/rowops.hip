@@ -477,6 +477,48 @@ extern "C" int msq_cast(void* dst, int dst_dtype, const void* src, int src_dtype
     return MSQ_OK;
 }
 
+// ------------------------------------------------------------------ transpose
+// dst[c][r] = src[r][c] (bf16): the transposed weight shadows of the backward's
+// dX products (dY . W reads W^T K-contiguous: the 256 tile's tb = 0 path).
+// 64 x 64 tiles through LDS (one padding column: conflict-free columns).
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(bf16* __restrict__ dst, int64_t ldd,
+                                                             const bf16* __restrict__ src, int64_t lds,
+                                                             int64_t rows, int64_t cols) {
+    __shared__ bf16 tile[64][66];
+    const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int64_t r = r0 + ty + 8 * k;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int64_t c = c0 + tx + 32 * e;
+            tile[ty + 8 * k][tx + 32 * e] = (r < rows && c < cols) ? src[r * lds + c] : (bf16)0.f;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int64_t c = c0 + ty + 8 * k;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int64_t r = r0 + tx + 32 * e;
+            if (r < rows && c < cols) dst[c * ldd + r] = tile[tx + 32 * e][ty + 8 * k];
+        }
+    }
+}
+
+extern "C" int msq_transpose_bf16(void* dst, int64_t ld_dst, const void* src, int64_t ld_src, int64_t rows,
+                                  int64_t cols, void* stream) {
+    MSQ_CHECK_ARG(dst && src && rows > 0 && cols > 0 && ld_src >= cols && ld_dst >= rows,
+                  "msq_transpose_bf16: bad sizes");
+    const dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
+    hipLaunchKernelGGL(transpose_bf16_kernel, grid, dim3(256), 0, (hipStream_t)stream, (bf16*)dst, ld_dst,
+                       (const bf16*)src, ld_src, rows, cols);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
 // ------------------------------------------------------------------ Adam
 // torch.optim.Adam (foreach, weight_decay=0, amsgrad=False):
 //   m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2
@@ -497,6 +539,31 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
     }
 }
 
+// same update, 4 parameters per thread with 16-B loads / stores (8-B shadow
+// stores); elements [4 n4, n) are left to the scalar kernel
+__global__ void adam4_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, bf16* __restrict__ shadow, int64_t n4, float b1, float b2,
+                             float eps, float step_size, float bc2_sqrt, float gscale) {
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+        const f32x4 gv = ((const f32x4*)g)[q];
+        f32x4 mv = ((f32x4*)m)[q], vv = ((f32x4*)v)[q], pv = ((f32x4*)p)[q];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float gi = gv[t] * gscale;
+            const float mi = mv[t] + (1.f - b1) * (gi - mv[t]);
+            const float vi = vv[t] * b2 + (1.f - b2) * gi * gi;
+            mv[t] = mi;
+            vv[t] = vi;
+            const float den = sqrtf(vi) / bc2_sqrt + eps;
+            pv[t] = pv[t] - step_size * (mi / den);
+        }
+        ((f32x4*)m)[q] = mv;
+        ((f32x4*)v)[q] = vv;
+        ((f32x4*)p)[q] = pv;
+        if (shadow) store4(shadow + 4 * q, pv);
+    }
+}
+
 extern "C" int msq_adam_step(float* p, const float* g, float* m, float* v, void* p_shadow, int64_t n, float lr,
                              float beta1, float beta2, float eps, int64_t step, float grad_scale, void* stream) {
     MSQ_CHECK_ARG(n >= 0 && step >= 1, "msq_adam_step: bad args");
@@ -505,9 +572,21 @@ extern "C" int msq_adam_step(float* p, const float* g, float* m, float* v, void*
     const double bc2 = 1.0 - pow((double)beta2, (double)step);
     const float step_size = (float)(lr / bc1);
     const float bc2s = (float)sqrt(bc2);
-    const int grid = (int)std::min<int64_t>((n + 255) / 256, 16384);
-    hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (bf16*)p_shadow, n,
-                       beta1, beta2, eps, step_size, bc2s, grad_scale);
+    const bool al = (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) == 0 &&
+                    ((uintptr_t)p_shadow % 8) == 0;
+    const int64_t n4 = al ? n / 4 : 0;
+    if (n4 > 0) {
+        const int grid4 = (int)std::min<int64_t>((n4 + 255) / 256, 16384);
+        hipLaunchKernelGGL(adam4_kernel, dim3(grid4), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (bf16*)p_shadow,
+                           n4, beta1, beta2, eps, step_size, bc2s, grad_scale);
+    }
+    const int64_t rest = n - 4 * n4;
+    if (rest > 0) {
+        const int grid = (int)std::min<int64_t>((rest + 255) / 256, 16384);
+        hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, p + 4 * n4, g + 4 * n4,
+                           m + 4 * n4, v + 4 * n4, p_shadow ? (bf16*)p_shadow + 4 * n4 : nullptr, rest, beta1, beta2,
+                           eps, step_size, bc2s, grad_scale);
+    }
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }

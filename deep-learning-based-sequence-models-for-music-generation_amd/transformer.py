@@ -267,9 +267,38 @@ class TransformerEngine:
         if force or v != self._shadow_version:
             ops.cast(self.shadow, self.flat.data)
             self._shadow_version = self.flat._version
+            self._wgen = getattr(self, "_wgen", 0) + 1
 
     def mark_shadow_fresh(self):
         self._shadow_version = self.flat._version
+        self._wgen = getattr(self, "_wgen", 0) + 1
+
+    # dX products read W^T: transposed bf16 copies (K-contiguous, the 256
+    # tile's tb = 0 path), refreshed once per change of the bf16 shadow
+    _T_NAMES = ("wqkv", "wproj", "w1", "w2")
+
+    def transposed_weights(self):
+        if self.shadow is None:
+            return None
+        gen = getattr(self, "_wgen", 0)
+        if getattr(self, "_wt_gen", None) == gen:
+            return self._wt
+        cfg, W = self.cfg, self.W
+        if getattr(self, "_wt", None) is None:
+            names = [f"{l}.{n}" for l in range(cfg.n_layer) for n in self._T_NAMES] + ["lm_w"]
+            total = sum(W[n].numel() for n in names)
+            buf = torch.empty(total, device=self.device, dtype=torch.bfloat16)
+            self._wt, off = {}, 0
+            for n in names:
+                r, c = W[n].shape
+                self._wt[n] = buf[off:off + r * c].view(c, r)
+                off += r * c
+        s = stream()
+        for n, t in self._wt.items():
+            src = W[n]
+            call("msq_transpose_bf16", ptr(t), t.stride(0), ptr(src), src.stride(0), src.shape[0], src.shape[1], s)
+        self._wt_gen = gen
+        return self._wt
 
     def acts(self, B, T, save=True):
         key = (B, T, save)
@@ -473,7 +502,11 @@ class TransformerEngine:
             if not head_bias_done:
                 ops.colsum(dl, G["lm_b"][:V], accumulate=True)
         on_side("dlogits", lm_w)
-        ops.gemm(dlogits, W["lm_w"], tb=True, out=Bw["df"])
+        Wt = self.transposed_weights()
+        if Wt is not None:
+            ops.gemm(dlogits, Wt["lm_w"], out=Bw["df"])
+        else:
+            ops.gemm(dlogits, W["lm_w"], tb=True, out=Bw["df"])
         gres = Bw["gres"]
         gres.zero_()
         gb = Bw["gb"] if Bw["gb"] is not None else gres
@@ -498,13 +531,20 @@ class TransformerEngine:
             on_side("gb", ffn2_w)
             before_write("dh")
             # dh = ReLU-masked FFN2 dX; the FFN1 bias gradient (its column sums) in the same epilogue
-            ops.gemm_colsum(gb, W[f"{l}.w2"], Bw["dh"], G[f"{l}.b1"], tb=True, epilogue=L.EPI_RELU_MASK, aux=A.h[l],
-                            accumulate=True)
+            if Wt is not None:
+                ops.gemm_colsum(gb, Wt[f"{l}.w2"], Bw["dh"], G[f"{l}.b1"], epilogue=L.EPI_RELU_MASK, aux=A.h[l],
+                                accumulate=True)
+            else:
+                ops.gemm_colsum(gb, W[f"{l}.w2"], Bw["dh"], G[f"{l}.b1"], tb=True, epilogue=L.EPI_RELU_MASK,
+                                aux=A.h[l], accumulate=True)
 
             def ffn1_w(l=l):
                 ops.gemm(Bw["dh"], A.c[l], ta=True, tb=True, out=G[f"{l}.w1"], epilogue=L.EPI_ACCUM)
             on_side("dh", ffn1_w)
-            ops.gemm(Bw["dh"], W[f"{l}.w1"], tb=True, out=Bw["dtmp"])
+            if Wt is not None:
+                ops.gemm(Bw["dh"], Wt[f"{l}.w1"], out=Bw["dtmp"])
+            else:
+                ops.gemm(Bw["dh"], W[f"{l}.w1"], tb=True, out=Bw["dtmp"])
             before_write("gb2")
             ops.layernorm_bwd(gres, Bw["dtmp"], A.xm[l], A.st2[l, 0], A.st2[l, 1], P[f"{l}.ln2_w"], G[f"{l}.ln2_w"],
                               G[f"{l}.ln2_b"], dx_copy=gb2 if Bw["gb"] is not None else None,
@@ -514,7 +554,10 @@ class TransformerEngine:
             def proj_w(l=l):
                 ops.gemm(gb2, A.o[l], ta=True, tb=True, out=G[f"{l}.wproj"], epilogue=L.EPI_ACCUM)
             on_side("gb2", proj_w)
-            ops.gemm(gb2, W[f"{l}.wproj"], tb=True, out=Bw["dtmp"])
+            if Wt is not None:
+                ops.gemm(gb2, Wt[f"{l}.wproj"], out=Bw["dtmp"])
+            else:
+                ops.gemm(gb2, W[f"{l}.wproj"], tb=True, out=Bw["dtmp"])
             before_write("dqkv")
             relattn_bwd(Bw["dtmp"], A.o[l], A.lse[l], A.qkv[l], W[f"{l}.R"], B, S, H, hs, scale, dqkv=Bw["dqkv"],
                         dR=G[f"{l}.R"], drop=(A._masks[l], p) if p > 0 else None)
@@ -522,7 +565,10 @@ class TransformerEngine:
             def qkv_w(l=l):
                 ops.gemm(Bw["dqkv"], A.a[l], ta=True, tb=True, out=G[f"{l}.wqkv"], epilogue=L.EPI_ACCUM)
             on_side("dqkv", qkv_w)
-            ops.gemm(Bw["dqkv"], W[f"{l}.wqkv"], tb=True, out=Bw["dtmp"])
+            if Wt is not None:
+                ops.gemm(Bw["dqkv"], Wt[f"{l}.wqkv"], out=Bw["dtmp"])
+            else:
+                ops.gemm(Bw["dqkv"], W[f"{l}.wqkv"], tb=True, out=Bw["dtmp"])
             before_write("gb")
             ops.layernorm_bwd(gres, Bw["dtmp"], A.x[l], A.st1[l, 0], A.st1[l, 1], P[f"{l}.ln1_w"], G[f"{l}.ln1_w"],
                               G[f"{l}.ln1_b"], dx_copy=Bw["gb"], drop=dsite(DROP_FFN + l - 1) if l > 0 else None,

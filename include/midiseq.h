@@ -134,6 +134,11 @@ size_t msq_gemm_colsum_workspace(int64_t M, int64_t N);
 int msq_gemm_colsum(int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
                     int64_t ldb, void* C, int64_t ldc, int epilogue, const void* aux, int aux_dtype, int64_t ld_aux,
                     float* dbias, int accumulate, void* ws, int64_t ws_bytes, void* stream);
+/* dst[c][r] = src[r][c] for a bf16 [rows][cols] matrix (leading dims in
+ * elements): the transposed weight copies the backward's dX products read
+ * (autograd's x.grad = dy @ W of nn.Linear, model_transformer.py:47,95,97,147). */
+int msq_transpose_bf16(void* dst, int64_t ld_dst, const void* src, int64_t ld_src, int64_t rows, int64_t cols,
+                       void* stream);
 size_t msq_colsum_workspace(int64_t rows, int64_t cols);
 int msq_colsum(float* out, int accumulate, const void* x, int dtype, int64_t rows, int64_t cols, int64_t ld,
                void* workspace, void* stream);

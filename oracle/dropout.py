@@ -24,9 +24,7 @@ def mix(x):
     x = np.asarray(x, dtype=_U)
     with np.errstate(over="ignore"):
         x = x ^ (x >> _U(16))
-        x = (x * _U(0x21F0AAAD)).astype(_U)
-        x = x ^ (x >> _U(15))
-        x = (x * _U(0x735A2D97)).astype(_U)
+        x = (x * _U(0x7FEB352D)).astype(_U)
         x = x ^ (x >> _U(15))
     return x
 

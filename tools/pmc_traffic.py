@@ -25,6 +25,9 @@ CLASSES = [
     (r"adam_kernel", "adam", 1),
     (r"ln_bwd|ln_reduce", "layernorm_bwd", 17),
     (r"gemm256_kernel<1, 1, 5|splitk_reduce", "gemm_dW", 33),
+    # forward products and (with the transposed weight copies) the plain dX ones, + their split-K tails
+    (r"gemm256_kernel<0, 0|tail_epi_kernel|gemm_bf16_kernel<0, 0", "gemm_fwd", 58),
+    (r"gemm256_kernel<0, 1", "gemm_dX", 8),
 ]
 
 
