@@ -22,12 +22,13 @@ CLASSES = [
     (r"flash_fwd3", "attn_fwd", 8),
     (r"attn_mask_kernel", "dropout_mask", 8),
     (r"colstats2|rowlse|cspart|cs_reduce|finish2|dbias_reduce|pad_table|wrange|mean_kernel", "loss", 1),
-    (r"adam_kernel", "adam", 1),
+    (r"adam4?_kernel", "adam", 1),
     (r"ln_bwd|ln_reduce", "layernorm_bwd", 17),
     (r"gemm256_kernel<1, 1, 5|splitk_reduce", "gemm_dW", 33),
+    # FFN dX with the bias column sums (CS instantiation; bf16 template names come out mangled)
+    (r"gemm256_kernel<0, 1|gemm256_kernelILi0ELi[01]ELi4E\w*Lb1E|colsum_partials", "gemm_dX", 8),
     # forward products and (with the transposed weight copies) the plain dX ones, + their split-K tails
-    (r"gemm256_kernel<0, 0|tail_epi_kernel|gemm_bf16_kernel<0, 0", "gemm_fwd", 58),
-    (r"gemm256_kernel<0, 1", "gemm_dX", 8),
+    (r"gemm256_kernel<0, 0|gemm256_kernelILi0ELi0E|tail_epi_kernel|gemm_bf16_kernel<0, 0", "gemm_fwd", 58),
 ]
 
 
