@@ -44,7 +44,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // KV4_LATE_STORE=1 issues the previous tile's dS stores after the QK/QR/dP
 // MFMAs instead of right after the prefetch
 #ifndef KV4_LATE_STORE
-#define KV4_LATE_STORE 0
+#define KV4_LATE_STORE 1
 #endif
 #if KV4_SCHED
 #define KV4_SB() __builtin_amdgcn_sched_barrier(0)
@@ -53,12 +53,21 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #endif
 
 constexpr int NT = 256;
-constexpr int KB = 128, QT = 32, NCH = 6;
+// KV4_DEPTH: query tiles staged ahead (LDS-DMA issued DEPTH tiles before use)
+#ifndef KV4_DEPTH
+#define KV4_DEPTH 2
+#endif
+constexpr int DEPTH = KV4_DEPTH, NB = DEPTH + 1;
+constexpr int KB = 128, QT = 32, NCH = 5 + DEPTH;
 constexpr int TILE = QT * 256;  // 32 rows x 128 bf16
-constexpr int O_Q = 0, O_O = 2 * TILE, O_R = 4 * TILE;
-constexpr int O_L = O_R + NCH * TILE;      // lse, D: 2 tiles x 2 x 64 floats
-constexpr int O_D = O_L + 2 * 2 * 64 * 4;  // dropout keep words of the 128 keys, 2 tiles
-constexpr int O_M = O_D + 2 * KB * 4;      // metadata-block BD table
+constexpr int O_Q = 0, O_O = NB * TILE, O_R = 2 * NB * TILE;
+constexpr int O_L = O_R + NCH * TILE;       // lse, D: NB tiles x 2 x 64 floats
+constexpr int O_D = O_L + NB * 2 * 64 * 4;  // dropout keep words of the 128 keys, NB tiles
+constexpr int O_M = O_D + NB * KB * 4;      // metadata-block BD table
+// vector memory ops per thread: NDMA per staged tile (Q 2, dO 2, R 2, one
+// 4-byte piece: lse / D on waves 0-1, keep words or a dummy on waves 2-3),
+// NST dS stores per tile
+constexpr int NDMA = 7, NST = 4;
 // dS staging for the coalesced row stores: 32 query rows x 128 keys bf16
 constexpr int T_PITCH = 272, T_BYTES = QT * T_PITCH;
 constexpr int O_T = O_M + 64 * 4;
@@ -215,7 +224,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
         offR[k] = (uint32_t)((lrow[k] * HS + ch * 8) * 2);
     }
     auto stage_q = [&](int t) {  // Q, dO, lse, D of query tile t
-        const int i0 = it0 + QT * t, buf = t & 1;
+        const int i0 = it0 + QT * t, buf = t % NB;
         char* dq_ = smem + O_Q + buf * TILE + w * 2048;
         char* do_ = smem + O_O + buf * TILE + w * 2048;
         const uint32_t bq = (uint32_t)i0 * (uint32_t)(ldq * 2), bo = (uint32_t)i0 * (uint32_t)(ldo * 2);
@@ -235,10 +244,12 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
         make_rsrc(DROP ? (const void*)(a.colmask + (int64_t)(b * H + h) * (mask_bh_bytes(mld) / 4)) : (const void*)a.R,
                   DROP ? (uint32_t)mask_bh_bytes(mld) : 0u);
     auto stage_m = [&](int t) {  // keep words colmask[b,h,j][i0/32] of the block's keys (waves 2-3)
-        if (DROP && w >= 2) {
+        if (w >= 2) {
             const int i0 = it0 + QT * t, key = j0 + 64 * (w - 2) + lane;
-            dma4(rm, smem + O_D + (t & 1) * KB * 4 + (w - 2) * 256,
-                 key < S ? (uint32_t)(mask_word(mld, key, i0) * 4) : OOB);
+            // without dropout a dummy (zero-filling the unused keep-word slots)
+            // keeps every wave's per-tile op count at NDMA
+            dma4(rm, smem + O_D + (t % NB) * KB * 4 + (w - 2) * 256,
+                 DROP && key < S && i0 < S ? (uint32_t)(mask_word(mld, key, i0) * 4) : OOB);
         }
     };
     auto stage_r = [&](int c) {  // R chunk c into ring slot c % NCH
@@ -275,8 +286,11 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
     const int z = c32 + 4 * hh, bpb = (c32 - 4 * hh - 1) * 4;
 
     // prologue: tile 0 and the 5 R chunks of its window
-    stage_q(0);
-    stage_m(0);
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+        stage_q(d);
+        stage_m(d);
+    }
 #pragma unroll
     for (int c = 0; c < NCH - 1; ++c) stage_r(c);
 
@@ -311,27 +325,30 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
     uint64_t pr[6] = {0, 0, 0, 0, 0, 0};
 #endif
     for (int t = 0; t < nqt; ++t) {
-        const int i0 = it0 + QT * t, buf = t & 1;
+        const int i0 = it0 + QT * t, buf = t % NB, sb = t & 1;
         KV4_T(0);
-        if (t >= 2 && !(LAB & 1)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        // tile t's DMA was issued in iteration t - DEPTH; younger: that
+        // iteration's NST stores and DEPTH - 1 iterations of NDMA + NST (every
+        // iteration issues all of them, out-of-range ones as zero-fill)
+        if (t > DEPTH && !(LAB & 17)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST + (NDMA + NST) * (DEPTH - 1)) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         bar();  // tile t landed everywhere; tile t-1's buffers (and dS staging) are free / published
         KV4_T(1);
-        if (t + 1 < nqt && !(LAB & 16)) {
-            stage_q(t + 1);
+        if (!(LAB & 16)) {
+            stage_q(t + DEPTH);
             stage_r(t + NCH - 1);
-            stage_m(t + 1);
+            stage_m(t + DEPTH);
         }
         asm volatile("" ::: "memory");
 #if !KV4_LATE_STORE
-        if (t >= 1 && !(LAB & 1)) store_ds(i0 - QT, buf ^ 1);
+        if (t >= 1 && !(LAB & 1)) store_ds(i0 - QT, sb ^ 1);
 #endif
         KV4_T(2);
         const char* cQ = smem + O_Q + buf * TILE;
         const char* cO = smem + O_O + buf * TILE;
         const float* cL = (const float*)(smem + O_L + buf * 512);
         const float* cD = cL + 64;
-        char* st = smem + O_T + buf * T_BYTES + 4 * hh * T_PITCH + (32 * w + c32) * 2;
+        char* st = smem + O_T + sb * T_BYTES + 4 * hh * T_PITCH + (32 * w + c32) * 2;
         // (a wave whose keys all follow the tile's queries computes zeros through
         // the mask: skipping it as a branch costs the register allocator a copy
         // of every accumulator at the join)
@@ -373,7 +390,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
         }
 #if KV4_LATE_STORE
         // the previous tile's dS rows leave while the last MFMAs drain
-        if (t >= 1 && !(LAB & 1)) store_ds(i0 - QT, buf ^ 1);
+        if (t >= 1 && !(LAB & 1)) store_ds(i0 - QT, sb ^ 1);
 #endif
         if (!(LAB & 2)) kv4_drain4(sacc, dpacc, qr0, qr1);
         KV4_T(3);

@@ -23,6 +23,7 @@
 //   fix : meta-block terms (j > i inside the metadata prefix).
 #include "attn_tiles.h"
 #include "gemm.h"
+#include <cstdlib>
 #include <stdlib.h>
 
 namespace {
@@ -332,8 +333,15 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     else
         hipLaunchKernelGGL(flash_bwd_pre_kernel, dim3((unsigned)((B * S * H + 3) / 4)), dim3(256), 0, s, a, dout, ldo,
                            out, Dv);
-    // key/value pass: dK, dV, and dS in both layouts
-    if (flash_bwd_kv3(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s))
+    // key/value pass: dK, dV, and dS in both layouts (v4; MSQ_ATTN_BWD_KV=3
+    // selects the v3 pass, kept for A/B measurements)
+    static const bool use_v3 = [] {
+        const char* e = getenv("MSQ_ATTN_BWD_KV");
+        return e && e[0] == '3';
+    }();
+    const int kv_rc = use_v3 ? flash_bwd_kv3(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s)
+                             : flash_bwd_kv4(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s);
+    if (kv_rc)
         return msq_set_error(MSQ_ERR_UNSUPPORTED, "flash_bwd: shape outside the key/value pass (n_meta > 8 or > 4 GB)");
     // dq (bf16, q columns of dqkv) = dSj . K + dQR . R
     flash_bwd_dq(a, dsj, dqr, ldr, dqkv, ldd, s);
