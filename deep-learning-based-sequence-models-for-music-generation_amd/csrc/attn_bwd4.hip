@@ -53,7 +53,23 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #endif
 
 constexpr int NT = 256;
-// KV4_DEPTH: query tiles staged ahead (LDS-DMA issued DEPTH tiles before use)
+// KV4_REGSTAGE=1 (default): the next tile's Q / dO / R chunk / row constants
+// are loaded into registers at the top of a tile and written to LDS
+// (ds_write_b128) at its end; an LDS-DMA wave-instruction costs 60-185 issue
+// cycles (MI355X_MICROARCH.md, LDS-DMA piece), ~7x a register-staged KB, and
+// at one wave per SIMD nothing hides it. KV4_REGSTAGE=0: LDS-DMA KV4_DEPTH
+// tiles ahead.
+#ifndef KV4_REGSTAGE
+#define KV4_REGSTAGE 0
+#endif
+// KV4_AHEAD: k-steps of phase-1 fragments read ahead of their MFMAs (1 or 2)
+#ifndef KV4_AHEAD
+#define KV4_AHEAD 1
+#endif
+#if KV4_REGSTAGE
+#undef KV4_DEPTH
+#define KV4_DEPTH 1
+#endif
 #ifndef KV4_DEPTH
 #define KV4_DEPTH 2
 #endif
@@ -285,6 +301,49 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
     // when c32 + row(e) >= 31 (z = c32 + 4 hh against 31 - (e&3) - 8 (e>>2))
     const int z = c32 + 4 * hh, bpb = (c32 - 4 * hh - 1) * 4;
 
+#if KV4_REGSTAGE
+    // register staging of tile tn (and R chunk tn + 4) for the write at the end
+    // of the previous tile; out-of-range rows load zeros (buffer OOB)
+    u32x4 gq[2], go[2], gr[2];
+    uint32_t gl = 0u;
+    auto load_next = [&](int tn) {
+        const int i0 = it0 + QT * tn;
+        const uint32_t bq = (uint32_t)i0 * (uint32_t)(ldq * 2), bo = (uint32_t)i0 * (uint32_t)(ldo * 2);
+        const int r0 = rw0 + 128 - 32 * (tn + NCH - 2);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const bool ok = i0 + lrow[k] < S;
+            gq[k] = __builtin_amdgcn_raw_buffer_load_b128(rq, ok ? offQ[k] + bq : OOB, 0, 0);
+            go[k] = __builtin_amdgcn_raw_buffer_load_b128(ro, ok ? offO[k] + bo : OOB, 0, 0);
+            const int rg = r0 + lrow[k];
+            gr[k] = __builtin_amdgcn_raw_buffer_load_b128(rr, (rg >= 0 && rg < S) ? offR[k] + (uint32_t)(r0 * HS * 2) : OOB,
+                                                          0, 0);
+        }
+        if (w < 2) {
+            gl = __builtin_amdgcn_raw_buffer_load_b32(w == 0 ? rl : rd, i0 + lane < S ? (uint32_t)((i0 + lane) * 4) : OOB,
+                                                      0, 0);
+        } else if (DROP) {
+            const int key = j0 + 64 * (w - 2) + lane;
+            gl = __builtin_amdgcn_raw_buffer_load_b32(
+                rm, key < S && i0 < S ? (uint32_t)(mask_word(mld, key, i0) * 4) : OOB, 0, 0);
+        }
+    };
+    auto write_next = [&](int tn) {
+        const int buf = tn % NB;
+        char* dq_ = smem + O_Q + buf * TILE + w * 2048 + lane * 16;
+        char* do_ = smem + O_O + buf * TILE + w * 2048 + lane * 16;
+        char* dr_ = sR + ((tn + NCH - 2) % NCH) * TILE + w * 2048 + lane * 16;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            *(u32x4*)(dq_ + k * 1024) = gq[k];
+            *(u32x4*)(do_ + k * 1024) = go[k];
+            *(u32x4*)(dr_ + k * 1024) = gr[k];
+        }
+        if (w < 2) *(uint32_t*)(smem + O_L + (buf * 2 + w) * 256 + lane * 4) = gl;
+        else if (DROP) *(uint32_t*)(smem + O_D + buf * KB * 4 + (w - 2) * 256 + lane * 4) = gl;
+    };
+#endif
+
     // prologue: tile 0 and the 5 R chunks of its window
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {
@@ -330,6 +389,15 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
         // tile t's DMA was issued in iteration t - DEPTH; younger: that
         // iteration's NST stores and DEPTH - 1 iterations of NDMA + NST (every
         // iteration issues all of them, out-of-range ones as zero-fill)
+#if KV4_REGSTAGE
+        // tile 0 came by LDS-DMA (prologue); later tiles by this wave's own
+        // ds_writes at the end of the previous iteration
+        if (t == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        bar();  // tile t published everywhere; tile t-1's buffers (and dS staging) are free
+        KV4_T(1);
+        if (t + 1 < nqt && !(LAB & 16)) load_next(t + 1);
+#else
         if (t > DEPTH && !(LAB & 17)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST + (NDMA + NST) * (DEPTH - 1)) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         bar();  // tile t landed everywhere; tile t-1's buffers (and dS staging) are free / published
@@ -339,6 +407,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
             stage_r(t + NCH - 1);
             stage_m(t + DEPTH);
         }
+#endif
         asm volatile("" ::: "memory");
 #if !KV4_LATE_STORE
         if (t >= 1 && !(LAB & 1)) store_ds(i0 - QT, sb ^ 1);
@@ -352,6 +421,13 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
         // (a wave whose keys all follow the tile's queries computes zeros through
         // the mask: skipping it as a branch costs the register allocator a copy
         // of every accumulator at the join)
+        // row constants of this lane's 16 query rows (read ahead of the MFMAs)
+        f32x4 lrow4[4], drow4[4];
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+            lrow4[e4] = *(const f32x4*)(cL + 8 * e4 + 4 * hh);
+            drow4[e4] = *(const f32x4*)(cD + 8 * e4 + 4 * hh);
+        }
         f32x16 sacc, dpacc, qr0, qr1;
         // this wave's 64-row window starts at ring chunk t + 4 - w (block 0), t + 3 - w (block 1)
         const char* rb0 = sR + ((t + 4 - w) % NCH) * TILE;
@@ -359,7 +435,9 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
         // S = Q.K^T, QR = Q.Rwin^T (two blocks), dP = dO.V^T: 32 MFMAs, each Q
         // fragment read once; fragments one k-step ahead
         {
-            bf16x8 fq[2], fo[2], f0[2], f1[2];
+            // fragments KV4_AHEAD k-steps ahead (KV4_AHEAD + 1 register sets)
+            constexpr int NF = KV4_AHEAD + 1;
+            bf16x8 fq[NF], fo[NF], f0[NF], f1[NF];
             auto ld = [&](int ks, int n) {
                 const int o = rof[ks & 1] + 1024 * ks;
                 fq[n] = *(const bf16x8*)(cQ + o);
@@ -367,11 +445,12 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
                 f0[n] = *(const bf16x8*)(rb0 + o);
                 f1[n] = *(const bf16x8*)(rb1 + o);
             };
-            ld(0, 0);
+#pragma unroll
+            for (int k = 0; k < KV4_AHEAD; ++k) ld(k, k);
 #pragma unroll
             for (int ks = 0; ks < 8; ++ks) {
-                const int c = ks & 1;
-                if (ks + 1 < 8) ld(ks + 1, c ^ 1);
+                const int c = ks % NF;
+                if (ks + KV4_AHEAD < 8) ld(ks + KV4_AHEAD, (ks + KV4_AHEAD) % NF);
                 if (LAB & 2) {
                     asm volatile("" ::"v"(fq[c]), "v"(fo[c]), "v"(f0[c]), "v"(f1[c]));
                 } else if (ks == 0) {
@@ -427,8 +506,8 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
 #pragma unroll
                 for (int e4 = 0; e4 < 4; ++e4) {
                     const int rb = 8 * e4 + 4 * hh;  // rows rb .. rb+3 of this register quad
-                    const f32x4 l4 = *(const f32x4*)(cL + rb);
-                    const f32x4 d4 = *(const f32x4*)(cD + rb);
+                    const f32x4 l4 = lrow4[e4];
+                    const f32x4 d4 = drow4[e4];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int e = 4 * e4 + r, iq = rb + r, i = i0 + iq;
@@ -490,6 +569,9 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
         }
 #pragma unroll
         for (int e = 0; e < 16; ++e) *(bf16*)(st + (acc_row(e, hh) - 4 * hh) * T_PITCH) = da[e >> 3][e & 7];
+#if KV4_REGSTAGE
+        if (t + 1 < nqt && !(LAB & 16)) write_next(t + 1);
+#endif
 #ifdef KV4_PROF
         {
             const uint64_t tm5 = __builtin_amdgcn_s_memtime();
