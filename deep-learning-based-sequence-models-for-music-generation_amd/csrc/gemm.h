@@ -33,6 +33,10 @@ struct GemmArgs {
     float* cs_ws;
 };
 
+// hipBLASLt route of msq_gemm_ex (blaslt.cpp): 1 done, 0 not handled, -1 error
+int blaslt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
+                int64_t ldb, void* C, int c_dtype, int64_t ldc, int epilogue, const float* bias, hipStream_t s);
+
 // bytes of the split-K partial workspace an ACCUM product with this split needs
 inline size_t splitk_ws_bytes(int64_t M, int64_t N, int64_t batch, int ksplit) {
     return ksplit > 1 && N % 4 == 0 ? (size_t)ksplit * batch * M * N * 4 : 0;

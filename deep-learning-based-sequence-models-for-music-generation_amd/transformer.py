@@ -273,9 +273,11 @@ class TransformerEngine:
         self._shadow_version = self.flat._version
         self._wgen = getattr(self, "_wgen", 0) + 1
 
-    # dX products read W^T: transposed bf16 copies (K-contiguous, the 256
-    # tile's tb = 0 path), refreshed once per change of the bf16 shadow
-    _T_NAMES = ("wqkv", "wproj", "w1", "w2")
+    # the ReLU-mask dX product (the 256 tile with its fused epilogue) reads W2^T:
+    # a transposed bf16 copy (K-contiguous, the tile's tb = 0 path), refreshed
+    # once per change of the bf16 shadow; the plain dX products read W itself
+    # (hipBLASLt takes either layout at the same speed, csrc/blaslt.cpp)
+    _T_NAMES = ("w2",)
 
     def transposed_weights(self):
         if self.shadow is None:
@@ -285,7 +287,7 @@ class TransformerEngine:
             return self._wt
         cfg, W = self.cfg, self.W
         if getattr(self, "_wt", None) is None:
-            names = [f"{l}.{n}" for l in range(cfg.n_layer) for n in self._T_NAMES] + ["lm_w"]
+            names = [f"{l}.{n}" for l in range(cfg.n_layer) for n in self._T_NAMES]
             total = sum(W[n].numel() for n in names)
             buf = torch.empty(total, device=self.device, dtype=torch.bfloat16)
             self._wt, off = {}, 0
@@ -503,10 +505,7 @@ class TransformerEngine:
                 ops.colsum(dl, G["lm_b"][:V], accumulate=True)
         on_side("dlogits", lm_w)
         Wt = self.transposed_weights()
-        if Wt is not None:
-            ops.gemm(dlogits, Wt["lm_w"], out=Bw["df"])
-        else:
-            ops.gemm(dlogits, W["lm_w"], tb=True, out=Bw["df"])
+        ops.gemm(dlogits, W["lm_w"], tb=True, out=Bw["df"])
         gres = Bw["gres"]
         gres.zero_()
         gb = Bw["gb"] if Bw["gb"] is not None else gres
@@ -541,10 +540,7 @@ class TransformerEngine:
             def ffn1_w(l=l):
                 ops.gemm(Bw["dh"], A.c[l], ta=True, tb=True, out=G[f"{l}.w1"], epilogue=L.EPI_ACCUM)
             on_side("dh", ffn1_w)
-            if Wt is not None:
-                ops.gemm(Bw["dh"], Wt[f"{l}.w1"], out=Bw["dtmp"])
-            else:
-                ops.gemm(Bw["dh"], W[f"{l}.w1"], tb=True, out=Bw["dtmp"])
+            ops.gemm(Bw["dh"], W[f"{l}.w1"], tb=True, out=Bw["dtmp"])
             before_write("gb2")
             ops.layernorm_bwd(gres, Bw["dtmp"], A.xm[l], A.st2[l, 0], A.st2[l, 1], P[f"{l}.ln2_w"], G[f"{l}.ln2_w"],
                               G[f"{l}.ln2_b"], dx_copy=gb2 if Bw["gb"] is not None else None,
@@ -554,10 +550,7 @@ class TransformerEngine:
             def proj_w(l=l):
                 ops.gemm(gb2, A.o[l], ta=True, tb=True, out=G[f"{l}.wproj"], epilogue=L.EPI_ACCUM)
             on_side("gb2", proj_w)
-            if Wt is not None:
-                ops.gemm(gb2, Wt[f"{l}.wproj"], out=Bw["dtmp"])
-            else:
-                ops.gemm(gb2, W[f"{l}.wproj"], tb=True, out=Bw["dtmp"])
+            ops.gemm(gb2, W[f"{l}.wproj"], tb=True, out=Bw["dtmp"])
             before_write("dqkv")
             relattn_bwd(Bw["dtmp"], A.o[l], A.lse[l], A.qkv[l], W[f"{l}.R"], B, S, H, hs, scale, dqkv=Bw["dqkv"],
                         dR=G[f"{l}.R"], drop=(A._masks[l], p) if p > 0 else None)
@@ -565,10 +558,7 @@ class TransformerEngine:
             def qkv_w(l=l):
                 ops.gemm(Bw["dqkv"], A.a[l], ta=True, tb=True, out=G[f"{l}.wqkv"], epilogue=L.EPI_ACCUM)
             on_side("dqkv", qkv_w)
-            if Wt is not None:
-                ops.gemm(Bw["dqkv"], Wt[f"{l}.wqkv"], out=Bw["dtmp"])
-            else:
-                ops.gemm(Bw["dqkv"], W[f"{l}.wqkv"], tb=True, out=Bw["dtmp"])
+            ops.gemm(Bw["dqkv"], W[f"{l}.wqkv"], tb=True, out=Bw["dtmp"])
             before_write("gb")
             ops.layernorm_bwd(gres, Bw["dtmp"], A.x[l], A.st1[l, 0], A.st1[l, 1], P[f"{l}.ln1_w"], G[f"{l}.ln1_w"],
                               G[f"{l}.ln1_b"], dx_copy=Bw["gb"], drop=dsite(DROP_FFN + l - 1) if l > 0 else None,
