@@ -32,7 +32,9 @@ struct Plan {
     bool ok = false;
 };
 
-typedef std::tuple<int, int, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int> Key;
+typedef std::tuple<int, int, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int, int64_t, int64_t, int64_t,
+                   int64_t>
+    Key;
 
 std::mutex g_mu;
 hipblasLtHandle_t g_h = nullptr;
@@ -53,7 +55,7 @@ bool init_locked() {
 }
 
 Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int c_dtype,
-               int epilogue) {
+               int epilogue, int64_t batch, int64_t sA, int64_t sB, int64_t sC) {
     Plan p;
     if (hipblasLtMatmulDescCreate(&p.op, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return p;
     // hipBLASLt A := our B (N x K after op), B := our A (K x M after op)
@@ -75,6 +77,16 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int64_t lda, int
         hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, b_rows, b_cols, lda) != HIPBLAS_STATUS_SUCCESS ||
         hipblasLtMatrixLayoutCreate(&p.lc, ct, N, M, ldc) != HIPBLAS_STATUS_SUCCESS)
         return p;
+    if (batch > 1) {
+        const int32_t bc = (int32_t)batch;
+        const int64_t strides[3] = {sB, sA, sC};  // hipBLASLt A = our B, B = our A
+        hipblasLtMatrixLayout_t ls[3] = {p.la, p.lb, p.lc};
+        for (int i = 0; i < 3; ++i) {
+            hipblasLtMatrixLayoutSetAttribute(ls[i], HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc, sizeof(bc));
+            hipblasLtMatrixLayoutSetAttribute(ls[i], HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &strides[i],
+                                              sizeof(int64_t));
+        }
+    }
     hipblasLtMatmulPreference_t pref;
     if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return p;
     const uint64_t wsb = WS_BYTES;
@@ -92,26 +104,34 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int64_t lda, int
 
 }  // namespace
 
-// 1 = done, 0 = not handled (caller runs its own kernel), -1 = hipBLASLt error
+// 1 = done, 0 = not handled (caller runs its own kernel), -1 = hipBLASLt error.
+// epilogue NONE / BIAS / BIAS_RELU (C = result), or ACCUM (fp32 C += result);
+// batch > 1: strided batches (element strides sA, sB, sC)
 int blaslt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
-                int64_t ldb, void* C, int c_dtype, int64_t ldc, int epilogue, const float* bias, hipStream_t s) {
+                int64_t ldb, void* C, int c_dtype, int64_t ldc, int epilogue, const float* bias, hipStream_t s,
+                int64_t batch, int64_t sA, int64_t sB, int64_t sC) {
     static const bool off = getenv("MSQ_NO_BLASLT") != nullptr;
     if (off) return 0;
-    if (epilogue != MSQ_EPI_NONE && epilogue != MSQ_EPI_BIAS && epilogue != MSQ_EPI_BIAS_RELU) return 0;
-    if ((epilogue != MSQ_EPI_NONE) != (bias != nullptr)) return 0;
+    if (epilogue != MSQ_EPI_NONE && epilogue != MSQ_EPI_BIAS && epilogue != MSQ_EPI_BIAS_RELU &&
+        epilogue != MSQ_EPI_ACCUM)
+        return 0;
+    if ((epilogue == MSQ_EPI_BIAS || epilogue == MSQ_EPI_BIAS_RELU) != (bias != nullptr)) return 0;
+    if (epilogue == MSQ_EPI_ACCUM && c_dtype != MSQ_F32) return 0;
+    const int epi_l = epilogue == MSQ_EPI_ACCUM ? MSQ_EPI_NONE : epilogue;  // accumulation is beta = 1
     Plan p;
     {
         std::lock_guard<std::mutex> lk(g_mu);
         if (!init_locked()) return 0;
-        const Key k{ta, tb, M, N, K, lda, ldb, ldc, c_dtype, epilogue};
+        const Key k{ta, tb, M, N, K, lda, ldb, ldc, c_dtype, epi_l, batch, sA, sB, sC};
         auto it = g_plans.find(k);
-        if (it == g_plans.end()) it = g_plans.emplace(k, make_plan(ta, tb, M, N, K, lda, ldb, ldc, c_dtype, epilogue)).first;
+        if (it == g_plans.end())
+            it = g_plans.emplace(k, make_plan(ta, tb, M, N, K, lda, ldb, ldc, c_dtype, epi_l, batch, sA, sB, sC)).first;
         p = it->second;
     }
     if (!p.ok) return 0;
-    if (epilogue != MSQ_EPI_NONE)
+    if (epi_l != MSQ_EPI_NONE)
         hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
-    const float alpha = 1.f, beta = 0.f;
+    const float alpha = 1.f, beta = epilogue == MSQ_EPI_ACCUM ? 1.f : 0.f;
     const hipblasStatus_t st = hipblasLtMatmul(g_h, p.op, &alpha, B, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &p.algo,
                                                g_ws, p.ws, s);
     return st == HIPBLAS_STATUS_SUCCESS ? 1 : -1;

@@ -34,8 +34,10 @@ struct GemmArgs {
 };
 
 // hipBLASLt route of msq_gemm_ex (blaslt.cpp): 1 done, 0 not handled, -1 error
+// (epilogue NONE / BIAS / BIAS_RELU, or ACCUM = fp32 C += result; strided batches)
 int blaslt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
-                int64_t ldb, void* C, int c_dtype, int64_t ldc, int epilogue, const float* bias, hipStream_t s);
+                int64_t ldb, void* C, int c_dtype, int64_t ldc, int epilogue, const float* bias, hipStream_t s,
+                int64_t batch = 1, int64_t sA = 0, int64_t sB = 0, int64_t sC = 0);
 
 // bytes of the split-K partial workspace an ACCUM product with this split needs
 inline size_t splitk_ws_bytes(int64_t M, int64_t N, int64_t batch, int ksplit) {
