@@ -18,7 +18,7 @@ from collections import defaultdict
 
 # (regex on the kernel name, class, class launches per train step)
 CLASSES = [
-    (r"flash_bwd_kv3|flash_bwd_dq|flash_bwd_pre|dqr_band_zero|flash_bwd_meta|gemm_bf16_kernel<1, 1, 5", "attn_bwd", 8),
+    (r"flash_bwd_kv[34]|flash_bwd_dq|flash_bwd_pre|dqr_band_zero|flash_bwd_meta|gemm_bf16_kernel<1, 1, 5", "attn_bwd", 8),
     (r"flash_fwd3", "attn_fwd", 8),
     (r"attn_mask_kernel", "dropout_mask", 8),
     (r"colstats2|rowlse|cspart|cs_reduce|finish2|dbias_reduce|pad_table|wrange|mean_kernel", "loss", 1),
@@ -29,6 +29,8 @@ CLASSES = [
     (r"gemm256_kernel<0, 1|gemm256_kernelILi0ELi[01]ELi4E\w*Lb1E|colsum_partials", "gemm_dX", 8),
     # forward products and (with the transposed weight copies) the plain dX ones, + their split-K tails
     (r"gemm256_kernel<0, 0|gemm256_kernelILi0ELi0E|tail_epi_kernel|gemm_bf16_kernel<0, 0", "gemm_fwd", 58),
+    # hipBLASLt kernels (the plain forward and dX products, both classes): bytes per step only
+    (r"^Cijk_|^Custom_Cijk_", "gemm_blaslt", 1),
 ]
 
 
