@@ -73,7 +73,13 @@ constexpr int NT = 256;
 #ifndef KV4_DEPTH
 #define KV4_DEPTH 2
 #endif
-constexpr int DEPTH = KV4_DEPTH, NB = DEPTH + 1;
+// KV4_PIPE=1: the dV / dK MFMAs of tile t-1 are issued inside tile t's skew
+// and softmax (same basic block, no data dependence), so the MFMA pipe runs
+// under that VALU / LDS work; tile t-1's Q / dO buffer stays live one more tile
+#ifndef KV4_PIPE
+#define KV4_PIPE 1
+#endif
+constexpr int DEPTH = KV4_DEPTH, NB = DEPTH + 1 + KV4_PIPE;
 constexpr int KB = 128, QT = 32, NCH = 5 + DEPTH;
 constexpr int TILE = QT * 256;  // 32 rows x 128 bf16
 constexpr int O_Q = 0, O_O = NB * TILE, O_R = 2 * NB * TILE;
@@ -301,6 +307,41 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
     // when c32 + row(e) >= 31 (z = c32 + 4 hh against 31 - (e&3) - 8 (e>>2))
     const int z = c32 + 4 * hh, bpb = (c32 - 4 * hh - 1) * 4;
 
+    // dV^T[d][j] += dO^T[d][i] P[i][j] ;  dK^T[d][j] += Q^T[d][i] dS[i][j]  (16 MFMAs)
+    auto phase_b = [&](const char* cQb, const char* cOb, const bf16x8 (&pb)[2], const bf16x8 (&db_)[2]) {
+        bf16x8 fo[2], fq[2];
+        fo[0] = tr_frag(cOb, 0, 0);
+        fq[0] = tr_frag(cQb, 0, 0);
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+            const int c = n & 1, nx = c ^ 1, db = n >> 1, s2 = n & 1;
+            if (n + 1 < 8) {
+                fo[nx] = tr_frag(cOb, (n + 1) & 1, (n + 1) >> 1);
+                fq[nx] = tr_frag(cQb, (n + 1) & 1, (n + 1) >> 1);
+            }
+            if (LAB & 2) {
+                asm volatile("" ::"v"(fo[c]), "v"(fq[c]), "v"(pb[s2]), "v"(db_[s2]));
+            } else {
+                mfma_acc_a(dv[db], fo[c], pb[s2]);
+                mfma_acc_a(dk[db], fq[c], db_[s2]);
+            }
+            KV4_SB();
+        }
+    };
+#if KV4_PIPE
+    // P / dS of the previous tile (zero before tile 0; its buffer is zeroed below)
+    bf16x8 pa_prev[2] = {}, da_prev[2] = {};
+    {
+        const u32x4 zz = (u32x4){0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            *(u32x4*)(smem + O_Q + (NB - 1) * TILE + tid * 32 + k * 16) = zz;
+            *(u32x4*)(smem + O_O + (NB - 1) * TILE + tid * 32 + k * 16) = zz;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // published by the first tile's barrier
+    }
+#endif
+
 #if KV4_REGSTAGE
     // register staging of tile tn (and R chunk tn + 4) for the write at the end
     // of the previous tile; out-of-range rows load zeros (buffer OOB)
@@ -421,13 +462,6 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
         // (a wave whose keys all follow the tile's queries computes zeros through
         // the mask: skipping it as a branch costs the register allocator a copy
         // of every accumulator at the join)
-        // row constants of this lane's 16 query rows (read ahead of the MFMAs)
-        f32x4 lrow4[4], drow4[4];
-#pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) {
-            lrow4[e4] = *(const f32x4*)(cL + 8 * e4 + 4 * hh);
-            drow4[e4] = *(const f32x4*)(cD + 8 * e4 + 4 * hh);
-        }
         f32x16 sacc, dpacc, qr0, qr1;
         // this wave's 64-row window starts at ring chunk t + 4 - w (block 0), t + 3 - w (block 1)
         const char* rb0 = sR + ((t + 4 - w) % NCH) * TILE;
@@ -488,7 +522,14 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
             }
         }
         bf16x8 pa[2], da[2];
+#if KV4_PIPE
+        const char* cQp = smem + O_Q + ((t + NB - 1) % NB) * TILE;
+        const char* cOp = smem + O_O + ((t + NB - 1) % NB) * TILE;
+#endif
         if (LAB & 4) {
+#if KV4_PIPE
+            phase_b(cQp, cOp, pa_prev, da_prev);
+#endif
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 pa[e >> 3][e & 7] = (bf16)sacc[e];
@@ -503,65 +544,74 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
             const uint32_t kw = DROP ? ((const uint32_t*)(smem + O_D + buf * KB * 4))[32 * w + c32] : 0u;
             auto softmax = [&](auto MODE) {
                 constexpr int md = decltype(MODE)::value;
-#pragma unroll
-                for (int e4 = 0; e4 < 4; ++e4) {
-                    const int rb = 8 * e4 + 4 * hh;  // rows rb .. rb+3 of this register quad
-                    const f32x4 l4 = lrow4[e4];
-                    const f32x4 d4 = drow4[e4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int e = 4 * e4 + r, iq = rb + r, i = i0 + iq;
-                        float x = sacc[e];
-                        const float l2 = l4[r] * LOG2E, dd = d4[r];
-                        const float kbv = DROP ? ((kw >> iq) & 1u ? a.keep_scale : 0.f) : 1.f;
-                        bool ok = true;
-                        if (md == 1) ok = (i < S) && (jk <= i);
-                        if (md == 2) {
-                            ok = (i < S) && (jk < S) && (jk <= i || jk < nm);
-                            if (ok && jk >= i + 2) x += mbd[i * 8 + jk];
-                        }
-                        float p = __builtin_amdgcn_exp2f(fmaf(x, c2, -l2));
-                        float ds = p * (DROP ? fmaf(dpacc[e], kbv, -dd) : dpacc[e] - dd) * a.scale;
-                        if (md != 0) {
-                            p = ok ? p : 0.f;
-                            ds = ok ? ds : 0.f;
-                        }
-                        if (md == 2 && ok && jk > i) meta_ds[(((int64_t)b * H + h) * 8 + i) * 8 + jk] = ds;
-                        if (DROP) p *= kbv;
-                        pa[e >> 3][e & 7] = (bf16)p;
-                        da[e >> 3][e & 7] = (bf16)ds;
+                auto elem = [&](int e) {
+                    const int e4 = e >> 2, r = e & 3, iq = 8 * e4 + 4 * hh + r, i = i0 + iq;
+                    float x = sacc[e];
+                    const float l2 = cL[8 * e4 + 4 * hh + r] * LOG2E, dd = cD[8 * e4 + 4 * hh + r];
+                    const float kbv = DROP ? ((kw >> iq) & 1u ? a.keep_scale : 0.f) : 1.f;
+                    bool ok = true;
+                    if (md == 1) ok = (i < S) && (jk <= i);
+                    if (md == 2) {
+                        ok = (i < S) && (jk < S) && (jk <= i || jk < nm);
+                        if (ok && jk >= i + 2) x += mbd[i * 8 + jk];
                     }
+                    float p = __builtin_amdgcn_exp2f(fmaf(x, c2, -l2));
+                    float ds = p * (DROP ? fmaf(dpacc[e], kbv, -dd) : dpacc[e] - dd) * a.scale;
+                    if (md != 0) {
+                        p = ok ? p : 0.f;
+                        ds = ok ? ds : 0.f;
+                    }
+                    if (md == 2 && ok && jk > i) meta_ds[(((int64_t)b * H + h) * 8 + i) * 8 + jk] = ds;
+                    if (DROP) p *= kbv;
+                    pa[e >> 3][e & 7] = (bf16)p;
+                    da[e >> 3][e & 7] = (bf16)ds;
+                };
+#if KV4_PIPE
+                // the previous tile's dV / dK step n (2 MFMAs, its fragments one
+                // step ahead) beside elements 2n, 2n+1 of this tile's softmax;
+                // sched_barrier per step keeps the fragment reads from being
+                // hoisted (register budget) while the VALU runs under the MFMAs
+                bf16x8 fo[2], fq[2];
+                fo[0] = tr_frag(cOp, 0, 0);
+                fq[0] = tr_frag(cQp, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 8; ++n) {
+                    const int c = n & 1, nx = c ^ 1, db = n >> 1, s2 = n & 1;
+                    if (n + 1 < 8) {
+                        fo[nx] = tr_frag(cOp, (n + 1) & 1, (n + 1) >> 1);
+                        fq[nx] = tr_frag(cQp, (n + 1) & 1, (n + 1) >> 1);
+                    }
+                    if (!(LAB & 2)) {
+                        mfma_acc_a(dv[db], fo[c], pa_prev[s2]);
+                        mfma_acc_a(dk[db], fq[c], da_prev[s2]);
+                    }
+                    elem(2 * n);
+                    elem(2 * n + 1);
+                    __builtin_amdgcn_sched_barrier(0);
                 }
+#else
+#pragma unroll
+                for (int e = 0; e < 16; ++e) elem(e);
+#endif
             };
             if (mode == 0) softmax(std::integral_constant<int, 0>{});
             else if (mode == 1) softmax(std::integral_constant<int, 1>{});
             else softmax(std::integral_constant<int, 2>{});
         }
         KV4_T(4);
-        // dV^T[d][j] += dO^T[d][i] P[i][j] ;  dK^T[d][j] += Q^T[d][i] dS[i][j]  (16 MFMAs)
-        {
-            bf16x8 fo[2], fq[2];
-            fo[0] = tr_frag(cO, 0, 0);
-            fq[0] = tr_frag(cQ, 0, 0);
-#pragma unroll
-            for (int n = 0; n < 8; ++n) {
-                const int c = n & 1, nx = c ^ 1, db = n >> 1, s2 = n & 1;
-                if (n + 1 < 8) {
-                    fo[nx] = tr_frag(cO, (n + 1) & 1, (n + 1) >> 1);
-                    fq[nx] = tr_frag(cQ, (n + 1) & 1, (n + 1) >> 1);
-                }
-                if (LAB & 2) {
-                    asm volatile("" ::"v"(fo[c]), "v"(fq[c]), "v"(pa[s2]), "v"(da[s2]));
-                } else {
-                    mfma_acc_a(dv[db], fo[c], pa[s2]);
-                    mfma_acc_a(dk[db], fq[c], da[s2]);
-                }
-                KV4_SB();
-            }
-        }
+#if !KV4_PIPE
+        phase_b(cQ, cO, pa, da);
+#endif
         // stage this tile's dS rows for the next iteration's stores (dS is 0
         // above the diagonal except the metadata keys of the first tile, which
         // went to meta_ds and are cleared here)
+#if KV4_PIPE
+        // (unmasked: the metadata entries j > i belong to dK)
+        pa_prev[0] = pa[0];
+        pa_prev[1] = pa[1];
+        da_prev[0] = da[0];
+        da_prev[1] = da[1];
+#endif
         if (i0 < nm) {
 #pragma unroll
             for (int e = 0; e < 16; ++e)
@@ -583,6 +633,9 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
 #ifdef KV4_PROF
     if (lane == 0)
         for (int k = 0; k < 6; ++k) atomicAdd(&kv4_prof[k], (unsigned long long)pr[k]);
+#endif
+#if KV4_PIPE
+    phase_b(smem + O_Q + ((nqt - 1) % NB) * TILE, smem + O_O + ((nqt - 1) % NB) * TILE, pa_prev, da_prev);
 #endif
     if (!(LAB & 1)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
