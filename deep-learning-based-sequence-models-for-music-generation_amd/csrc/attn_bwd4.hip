@@ -77,7 +77,7 @@ constexpr int NT = 256;
 // and softmax (same basic block, no data dependence), so the MFMA pipe runs
 // under that VALU / LDS work; tile t-1's Q / dO buffer stays live one more tile
 #ifndef KV4_PIPE
-#define KV4_PIPE 1
+#define KV4_PIPE 0
 #endif
 constexpr int DEPTH = KV4_DEPTH, NB = DEPTH + 1 + KV4_PIPE;
 constexpr int KB = 128, QT = 32, NCH = 5 + DEPTH;
