@@ -5,7 +5,9 @@
 // gemm256.hip and the weight-gradient (K = B*S) products slower, so
 // msq_gemm_ex routes only the former here; the fused epilogues (dropout +
 // residual, ReLU mask, column sums) and the accumulate products stay on the
-// hand-written tiles. MSQ_NO_BLASLT=1 disables the route.
+// hand-written tiles. MSQ_NO_BLASLT=1 disables the route; the first call of a
+// shape times hipBLASLt's candidate algorithms (MSQ_BLASLT_NOTUNE=1: keep the
+// heuristic's first choice).
 //
 // Layouts: msq_gemm's C[M][N] (row major, ldc) = op(A) op(B) with A [M][K]
 // (ta = 0) or [K][M] (ta = 1) and B [N][K] (tb = 0) or [K][N] (tb = 1), all
@@ -24,12 +26,17 @@
 
 namespace {
 
+constexpr int NCAND = 8;
+
 struct Plan {
     hipblasLtMatmulDesc_t op = nullptr;
     hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
     hipblasLtMatmulAlgo_t algo{};
     size_t ws = 0;
-    bool ok = false;
+    bool ok = false, tuned = false;
+    float best_ms = 0.f;
+    int ncand = 0;
+    hipblasLtMatmulHeuristicResult_t cand[NCAND];
 };
 
 typedef std::tuple<int, int, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int, int64_t, int64_t, int64_t,
@@ -91,15 +98,67 @@ Plan make_plan(int ta, int tb, int64_t M, int64_t N, int64_t K, int64_t lda, int
     if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return p;
     const uint64_t wsb = WS_BYTES;
     hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
-    hipblasLtMatmulHeuristicResult_t res[1];
+    hipblasLtMatmulHeuristicResult_t res[NCAND];
     int n = 0;
-    const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(g_h, p.op, p.la, p.lb, p.lc, p.lc, pref, 1, res, &n);
+    const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(g_h, p.op, p.la, p.lb, p.lc, p.lc, pref, NCAND, res, &n);
     hipblasLtMatmulPreferenceDestroy(pref);
-    if (st != HIPBLAS_STATUS_SUCCESS || n < 1 || res[0].state != HIPBLAS_STATUS_SUCCESS) return p;
-    p.algo = res[0].algo;
-    p.ws = res[0].workspaceSize;
-    p.ok = p.ws <= WS_BYTES;
+    if (st != HIPBLAS_STATUS_SUCCESS || n < 1) return p;
+    p.ncand = 0;
+    for (int i = 0; i < n; ++i)
+        if (res[i].state == HIPBLAS_STATUS_SUCCESS && res[i].workspaceSize <= WS_BYTES) p.cand[p.ncand++] = res[i];
+    if (p.ncand == 0) return p;
+    p.algo = p.cand[0].algo;
+    p.ws = p.cand[0].workspaceSize;
+    p.ok = true;
     return p;
+}
+
+// First call of a shape: time every candidate algorithm twice on these
+// buffers (beta = 0 into a scratch output, so accumulating products are not
+// disturbed) and keep the fastest; the heuristic's first choice was up to 2x
+// off the best on the weight-gradient shapes. Skipped while the stream is
+// being captured into a graph (the plan then keeps the heuristic's choice).
+void autotune(Plan& p, const void* A, const void* B, int64_t M, int64_t ldc, int64_t batch, int64_t sC, int c_dtype,
+              const float* bias, hipStream_t s) {
+    p.tuned = true;
+    if (p.ncand < 2) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+    const size_t esz = c_dtype == MSQ_BF16 ? 2 : 4;
+    const size_t cbytes = (size_t)((batch > 1 ? sC * (batch - 1) : 0) + ldc * M) * esz;
+    void* scratch = nullptr;
+    if (hipMalloc(&scratch, cbytes) != hipSuccess) return;
+    if (bias) hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    const float alpha = 1.f, beta = 0.f;
+    float best = 1e30f;
+    int bi = 0;
+    for (int i = 0; i < p.ncand; ++i) {
+        float ms = 1e30f;
+        for (int rep = 0; rep < 2; ++rep) {
+            hipEventRecord(e0, s);
+            const hipblasStatus_t st = hipblasLtMatmul(g_h, p.op, &alpha, B, p.la, A, p.lb, &beta, scratch, p.lc,
+                                                       scratch, p.lc, &p.cand[i].algo, g_ws, p.cand[i].workspaceSize, s);
+            hipEventRecord(e1, s);
+            hipEventSynchronize(e1);
+            float t = 1e30f;
+            if (st == HIPBLAS_STATUS_SUCCESS) hipEventElapsedTime(&t, e0, e1);
+            ms = t;  // the second run (warm)
+        }
+        if (ms < best) {
+            best = ms;
+            bi = i;
+        }
+    }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    hipStreamSynchronize(s);
+    hipFree(scratch);
+    p.algo = p.cand[bi].algo;
+    p.ws = p.cand[bi].workspaceSize;
+    p.best_ms = best;
 }
 
 }  // namespace
@@ -126,6 +185,9 @@ int blaslt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, 
         auto it = g_plans.find(k);
         if (it == g_plans.end())
             it = g_plans.emplace(k, make_plan(ta, tb, M, N, K, lda, ldb, ldc, c_dtype, epi_l, batch, sA, sB, sC)).first;
+        static const bool no_tune = getenv("MSQ_BLASLT_NOTUNE") != nullptr;
+        if (it->second.ok && !it->second.tuned && !no_tune)
+            autotune(it->second, A, B, M, ldc, batch, sC, c_dtype, epi_l != MSQ_EPI_NONE ? bias : nullptr, s);
         p = it->second;
     }
     if (!p.ok) return 0;

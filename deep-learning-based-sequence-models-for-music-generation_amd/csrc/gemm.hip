@@ -587,7 +587,9 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
         return MSQ_OK;
     }
     // plain / bias / bias+ReLU forward and dX products: hipBLASLt (blaslt.cpp)
-    if (dtype == MSQ_BF16 && batch == 1 && M > 256 && epilogue != MSQ_EPI_ACCUM && !getenv("MSQ_GEMM128")) {
+    static const bool blaslt_dw = getenv("MSQ_BLASLT_DW") != nullptr;  // A/B switch: weight gradients too
+    if (dtype == MSQ_BF16 && batch == 1 && M > 256 && (epilogue != MSQ_EPI_ACCUM || blaslt_dw) &&
+        !getenv("MSQ_GEMM128")) {
         const int r = blaslt_gemm(ta, tb, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, epilogue, bias, s);
         if (r < 0) return msq_set_error(MSQ_ERR_HIP, "msq_gemm: hipBLASLt matmul failed");
         if (r > 0) return MSQ_OK;
