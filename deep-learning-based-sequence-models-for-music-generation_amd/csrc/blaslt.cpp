@@ -5,9 +5,10 @@
 // gemm256.hip and the weight-gradient (K = B*S) products slower, so
 // msq_gemm_ex routes only the former here; the fused epilogues (dropout +
 // residual, ReLU mask, column sums) and the accumulate products stay on the
-// hand-written tiles. MSQ_NO_BLASLT=1 disables the route; the first call of a
-// shape times hipBLASLt's candidate algorithms (MSQ_BLASLT_NOTUNE=1: keep the
-// heuristic's first choice).
+// hand-written tiles. MSQ_NO_BLASLT=1 disables the route; MSQ_BLASLT_TUNE=1
+// times hipBLASLt's candidate algorithms on the first call of a shape (a few %
+// on some shapes; off by default because timing picks are not reproducible
+// across processes).
 //
 // Layouts: msq_gemm's C[M][N] (row major, ldc) = op(A) op(B) with A [M][K]
 // (ta = 0) or [K][M] (ta = 1) and B [N][K] (tb = 0) or [K][N] (tb = 1), all
@@ -185,8 +186,10 @@ int blaslt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, 
         auto it = g_plans.find(k);
         if (it == g_plans.end())
             it = g_plans.emplace(k, make_plan(ta, tb, M, N, K, lda, ldb, ldc, c_dtype, epi_l, batch, sA, sB, sC)).first;
-        static const bool no_tune = getenv("MSQ_BLASLT_NOTUNE") != nullptr;
-        if (it->second.ok && !it->second.tuned && !no_tune)
+        // opt-in: timing picks can differ between processes (DDP ranks would
+        // then round differently), so the default is the heuristic's choice
+        static const bool tune = getenv("MSQ_BLASLT_TUNE") != nullptr;
+        if (it->second.ok && !it->second.tuned && tune)
             autotune(it->second, A, B, M, ldc, batch, sC, c_dtype, epi_l != MSQ_EPI_NONE ? bias : nullptr, s);
         p = it->second;
     }
