@@ -16,13 +16,18 @@
 // from a (row>>1)&7 chunk-swizzled image; B (K / R rows = [k][d], d contiguous)
 // with ds_read_b64_tr_b16 from a 2*g(k) chunk-swizzled image (T10).
 #include "attn.h"
+#include <cstdlib>
 
 namespace {
 
-constexpr int BM = 128, BK = 64, NT = 256, HSZ = 128;
-constexpr int A_BYTES = BM * BK * 2, B_BYTES = BK * HSZ * 2, STAGE = A_BYTES + B_BYTES;
+constexpr int BM = 128, NT = 256, HSZ = 128;
 
-__device__ __forceinline__ int swz_k(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+// A rows of BK bf16: 8 chunks (BK 64, chunk ^= (row >> 1) & 7) or 4 chunks
+// (BK 32, chunk ^= (row >> 2) & 3); either way 16 rows at one chunk are conflict-free
+template <int BK>
+__device__ __forceinline__ int swz_k(int row, int chunk) {
+    return BK == 64 ? chunk ^ ((row >> 1) & 7) : chunk ^ ((row >> 2) & 3);
+}
 __device__ __forceinline__ int swz_mn(int k, int chunk) { return chunk ^ ((((k & 3) | ((k >> 1) & 4))) << 1); }
 
 __device__ __forceinline__ u32x4 load_chunk(const bf16* p, int valid) {
@@ -33,9 +38,10 @@ __device__ __forceinline__ u32x4 load_chunk(const bf16* p, int valid) {
     return u.v;
 }
 
+template <int BK>
 __device__ __forceinline__ bf16x8 frag_k(const char* s, int rb, int ks, int lane) {
     const int row = rb + (lane & 15), ch = ks * 4 + (lane >> 4);
-    return *(const bf16x8*)(s + row * 128 + swz_k(row, ch) * 16);
+    return *(const bf16x8*)(s + row * (BK * 2) + swz_k<BK>(row, ch) * 16);
 }
 __device__ __forceinline__ bf16x8 frag_mn(const char* s, int rb, int ks, int lane) {
     const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
@@ -52,9 +58,14 @@ __device__ __forceinline__ bf16x8 frag_mn(const char* s, int rb, int ks, int lan
     return u.v;
 }
 
-__global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const bf16* __restrict__ dsj,
-                                                             const bf16* __restrict__ dqr, int64_t ldr,
-                                                             bf16* __restrict__ dqkv, int64_t ldd) {
+// BK 64: 64 KB of LDS, two workgroups per CU; BK 32: 32 KB, four
+template <int BK>
+__global__ __launch_bounds__(NT, BK == 64 ? 2 : 4) void flash_bwd_dq_kernel(AttnArgs a, const bf16* __restrict__ dsj,
+                                                                          const bf16* __restrict__ dqr, int64_t ldr,
+                                                                          bf16* __restrict__ dqkv, int64_t ldd) {
+    constexpr int A_BYTES = BM * BK * 2, B_BYTES = BK * HSZ * 2, STAGE = A_BYTES + B_BYTES;
+    constexpr int NU = BK / 16;  // 16-B chunks per thread per operand and stage
+    constexpr int CPR = BK / 8;  // chunks per A row
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int64_t S = a.S, H = a.H, ldq = a.ldq;
@@ -71,7 +82,7 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
     const int64_t kb1 = (S - 1 - ilast) / BK * BK;       // r range [kb1, S)
     const int n0 = (int)((ke0 + BK - 1) / BK), nt = n0 + (int)((S - kb1 + BK - 1) / BK);
 
-    u32x4 ra[4], rb[4];
+    u32x4 ra[NU], rb[NU];
     auto load = [&](int t) {
         const bool s1 = t >= n0;
         const int64_t k0 = s1 ? kb1 + (int64_t)(t - n0) * BK : (int64_t)t * BK;
@@ -80,15 +91,15 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
         const bf16* B = s1 ? B1 : B0;
         const int64_t ldb = s1 ? HSZ : ldq;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < NU; ++u) {
             const int c = tid + NT * u;
-            {  // A [128 rows][64 k]
-                const int row = c >> 3, ch = c & 7;
+            {  // A [128 rows][BK k]
+                const int row = c / CPR, ch = c % CPR;
                 const int64_t gi = i0 + row, gk = k0 + ch * 8;
                 const int valid = gi < S ? (int)min<int64_t>(8, kend - gk) : 0;
                 ra[u] = load_chunk(A + gi * ldr + gk, valid);
             }
-            {  // B [64 k][128 d]
+            {  // B [BK k][128 d]
                 const int kr = c >> 4, ch = c & 15;
                 const int64_t gk = k0 + kr;
                 rb[u] = load_chunk(B + gk * ldb + ch * 8, gk < kend ? 8 : 0);
@@ -99,10 +110,10 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
         char* sa = smem + buf * STAGE;
         char* sb = sa + A_BYTES;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < NU; ++u) {
             const int c = tid + NT * u;
-            const int row = c >> 3, ch = c & 7;
-            *(u32x4*)(sa + row * 128 + swz_k(row, ch) * 16) = ra[u];
+            const int row = c / CPR, ch = c % CPR;
+            *(u32x4*)(sa + row * (BK * 2) + swz_k<BK>(row, ch) * 16) = ra[u];
             const int kr = c >> 4, chb = c & 15;
             *(u32x4*)(sb + kr * 256 + swz_mn(kr, chb) * 16) = rb[u];
         }
@@ -125,10 +136,10 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
         const bool more = t + 1 < nt;
         if (more) load(t + 1);
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+        for (int ks = 0; ks < BK / 32; ++ks) {
             bf16x8 af[4], bfr[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) af[i] = frag_k(sa, wm + i * 16, ks, lane);
+            for (int i = 0; i < 4; ++i) af[i] = frag_k<BK>(sa, wm + i * 16, ks, lane);
 #pragma unroll
             for (int j = 0; j < 4; ++j) bfr[j] = frag_mn(sb, wn + j * 16, ks, lane);
 #pragma unroll
@@ -156,6 +167,11 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
 
 void flash_bwd_dq(const AttnArgs& a, const bf16* dsj, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd,
                   hipStream_t s) {
+    static const int bk = [] {
+        const char* e = getenv("MSQ_ATTN_DQ_BK");
+        return e && atoi(e) == 32 ? 32 : 64;
+    }();
     const dim3 grid((unsigned)((a.S + BM - 1) / BM), (unsigned)a.H, (unsigned)a.B);
-    hipLaunchKernelGGL(flash_bwd_dq_kernel, grid, dim3(NT), 0, s, a, dsj, dqr, ldr, dqkv, ldd);
+    if (bk == 32) hipLaunchKernelGGL(flash_bwd_dq_kernel<32>, grid, dim3(NT), 0, s, a, dsj, dqr, ldr, dqkv, ldd);
+    else hipLaunchKernelGGL(flash_bwd_dq_kernel<64>, grid, dim3(NT), 0, s, a, dsj, dqr, ldr, dqkv, ldd);
 }
