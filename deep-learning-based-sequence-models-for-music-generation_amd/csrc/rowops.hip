@@ -2,6 +2,7 @@
 // fwd/bwd, column sums (bias grads), casts and Adam. All HBM-bound; loads are
 // 16-B (fp32x4) or 8-B (bf16x4) per lane (guide §6 G13).
 #include "common.h"
+#include <cstdlib>
 
 // ------------------------------------------------------------------ embedding
 // model_transformer.py:152-155 / mamba.py:29-30: meta rows first, then tokens.
@@ -120,7 +121,7 @@ struct CopyDrop {
 // residual branch that produced this LayerNorm's input (model_transformer.py
 // :51,101 proj / FFN output biases), which would otherwise be a separate
 // column-sum pass over the same rows
-template <typename TD, typename TO, int MAXC, bool BIAS>
+template <typename TD, typename TO, int MAXC, bool BIAS, bool PF = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO* __restrict__ dcopy,
                                                      float* __restrict__ part, const TD* __restrict__ dy,
                                                      const float* __restrict__ x, const float* __restrict__ mean,
@@ -133,8 +134,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
     for (int64_t row = blockIdx.x * 4LL + wid; row < rows; row += (int64_t)gridDim.x * 4) {
         const float mu = mean[row], rs = rstd[row];
         const int64_t xrow = map_row(row, seg, skip);
-        f32x4 xh[MAXC], g[MAXC];
+        f32x4 xh[MAXC], g[MAXC], acc[MAXC];
         float s1 = 0.f, s2 = 0.f;
+        // PF: the accumulated gradient row is read with x and dy (one memory
+        // latency per row instead of two)
+        if (PF) {
+#pragma unroll
+            for (int c = 0; c < MAXC; ++c) {
+                const int col = (c * 64 + lane) * 4;
+                if (col < d) acc[c] = *(const f32x4*)(dxa + xrow * d + col);
+            }
+        }
 #pragma unroll
         for (int c = 0; c < MAXC; ++c) {
             const int col = (c * 64 + lane) * 4;
@@ -161,7 +171,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
             const int col = (c * 64 + lane) * 4;
             if (col < d) {
                 float* dp = dxa + xrow * d + col;
-                f32x4 o = *(f32x4*)dp;
+                f32x4 o = PF ? acc[c] : *(f32x4*)dp;
 #pragma unroll
                 for (int t = 0; t < 4; ++t) o[t] += rs * (g[c][t] - m1 - xh[c][t] * m2);
                 *(f32x4*)dp = o;
@@ -274,7 +284,11 @@ static void ln_bwd_launch_b(float* dxa, TO* dcopy, float* part, const TD* dy, co
                             CopyDrop cd, hipStream_t s) {
     const dim3 grid(LN_BWD_BLOCKS);
     if (d <= 256) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 1, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
-    else if (d <= 1024) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
+    else if (d <= 1024) {
+        static const bool pf = getenv("MSQ_LNB_PF") != nullptr;  // A/B switch: dx_acc read with x and dy
+        if (pf) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4, BIAS, true>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
+        else hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
+    }
     else hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 8, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
 }
 template <typename TD, typename TO>
