@@ -23,6 +23,8 @@ SIGNATURES = {
     "msq_version": (_i, []),
     "msq_embed_fwd": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "msq_embed_bwd": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "msq_embed_bwd_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64, _i64]),
+    "msq_embed_bwd_sorted": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _p]),
     "msq_layernorm_fwd": (_i, [_p, _i, _p, _p, _p, _p, _p, _i64, _i64, _f, _i64, _i64, _p]),
     "msq_layernorm_bwd_workspace": (_sz, [_i64, _i64]),
     "msq_layernorm_bwd": (_i, [_p, _p, _i, _p, _p, _p, _i, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _p]),

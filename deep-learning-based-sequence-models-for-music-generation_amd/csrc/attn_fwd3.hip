@@ -28,8 +28,11 @@ constexpr int O_M = O_S + 8 * 16 * SCR * 4;
 constexpr int O_D = O_M + 64 * 4;  // dropout keep words of the block's 256 queries, 2 tiles
 constexpr int LDS_BYTES = O_D + 2 * QB * 4;
 constexpr uint32_t OOB = 0xFFFF0000u;
+// 1: the next K / V / R tile is staged through registers (loads after the
+// barrier, ds_write at the end of the tile) instead of in-loop LDS-DMA.
+// Measured 1-2 % slower at cfg 2 (0.908 vs 0.892 ms per launch, same box), so off.
 #ifndef FWD3_REGSTAGE
-#define FWD3_REGSTAGE 1
+#define FWD3_REGSTAGE 0
 #endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {

@@ -55,6 +55,256 @@ extern "C" int msq_embed_bwd(float* g_tok, float* g_meta, const float* dx, const
     return MSQ_OK;
 }
 
+// ------------------------------------------------ deterministic embedding backward
+// The same scatter-add as embed_bwd_kernel with a fixed summation order, so the
+// gradient is bitwise reproducible (a sorted segment sum). Every
+// dx row r gets one key: its token id, or V_tok + its metadata id (ids out of
+// range get the dropped key K = V_tok + V_meta). An LSD radix sort with 8-bit
+// digits (2 passes at the 17 914 + 568 keys of cfg 2) orders the rows by key,
+// stably, so each table row then sums its rows in sequence order:
+//   key:     keys[r], pos[r] = r
+//   per pass rank: per 256-row chunk, a row's rank among the equal digits before
+//                  it (LDS compare); the chunk's last one writes cnt[digit][chunk]
+//            scan: exclusive scan of cnt (digit-major) = where each
+//                  (digit, chunk) group lands
+//            scatter: (key, pos) to its place
+//   sum:     blocks of EMB_P sorted rows, one wave per 256 columns: a key run
+//            wholly inside the block is added to its table row directly (its only
+//            writer); runs crossing a block edge leave per-block partials
+//   fix:     the block where a crossing run ends adds that run's partials in
+//            block order
+// HBM traffic: one read of dx (the row sums) plus ~50 B of index arrays per row.
+#define EMB_CH 256
+#define EMB_P 64
+
+__global__ void emb_key_kernel(int* __restrict__ key, int* __restrict__ pos, const int64_t* __restrict__ idx,
+                               const int64_t* __restrict__ meta, int64_t N, int64_t T, int64_t nm, int64_t Vt,
+                               int64_t Vm) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= N) return;
+    const int64_t S = T + nm, K = Vt + Vm;
+    const int64_t b = r / S, s = r % S;
+    int64_t k;
+    if (s < nm) {
+        const int64_t m = meta[b * nm + s];
+        k = (m >= 0 && m < Vm) ? Vt + m : K;
+    } else {
+        const int64_t t = idx[b * T + (s - nm)];
+        k = (t >= 0 && t < Vt) ? t : K;
+    }
+    key[r] = (int)k;
+    pos[r] = (int)r;
+}
+
+__global__ __launch_bounds__(EMB_CH) void emb_rank_kernel(int* __restrict__ cnt, int* __restrict__ rank,
+                                                          const int* __restrict__ key, int64_t N, int shift,
+                                                          int64_t nch) {
+    __shared__ int dig[EMB_CH];
+    const int tid = threadIdx.x;
+    const int64_t r = (int64_t)blockIdx.x * EMB_CH + tid;
+    const int dg = r < N ? (key[r] >> shift) & 255 : -1;
+    dig[tid] = dg;
+    __syncthreads();
+    int rk = 0;
+    bool last = true;
+#pragma unroll 8
+    for (int j = 0; j < EMB_CH; ++j) {  // broadcast LDS reads
+        const int dj = dig[j];
+        rk += (j < tid && dj == dg);
+        last = last && !(j > tid && dj == dg);
+    }
+    if (r < N) {
+        rank[r] = rk;
+        if (last) cnt[(int64_t)dg * nch + blockIdx.x] = rk + 1;
+    }
+}
+
+// exclusive scan of n ints in place, one workgroup; a[n] = total
+__global__ __launch_bounds__(1024) void emb_scan_kernel(int* __restrict__ a, int64_t n) {
+    __shared__ int part[1024];
+    const int tid = threadIdx.x;
+    const int64_t per = (n + 1023) / 1024;
+    const int64_t lo = std::min<int64_t>(n, tid * per), hi = std::min<int64_t>(n, lo + per);
+    int s = 0;
+    for (int64_t i = lo; i < hi; ++i) s += a[i];
+    part[tid] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan of the partials
+        const int v = tid >= off ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int run = tid ? part[tid - 1] : 0;
+    for (int64_t i = lo; i < hi; ++i) {
+        const int c = a[i];
+        a[i] = run;
+        run += c;
+    }
+    if (tid == 1023) a[n] = part[1023];
+}
+
+__global__ void emb_scatter_kernel(int* __restrict__ key_out, int* __restrict__ pos_out, const int* __restrict__ off,
+                                   const int* __restrict__ rank, const int* __restrict__ key_in,
+                                   const int* __restrict__ pos_in, int64_t N, int shift, int64_t nch) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= N) return;
+    const int k = key_in[r];
+    const int64_t dst = off[(int64_t)((k >> shift) & 255) * nch + r / EMB_CH] + rank[r];
+    key_out[dst] = k;
+    pos_out[dst] = pos_in[r];
+}
+
+__device__ __forceinline__ float* emb_row(float* gt, float* gm, int key, int64_t Vt, int64_t d) {
+    return key < Vt ? gt + (int64_t)key * d : gm + ((int64_t)key - Vt) * d;
+}
+
+// grid (blocks of EMB_P sorted rows, column slices of 256), one wave
+__global__ __launch_bounds__(64) void emb_sum_kernel(float* __restrict__ gt, float* __restrict__ gm,
+                                                     float* __restrict__ part, const float* __restrict__ dx,
+                                                     const int* __restrict__ spos, const int* __restrict__ skey,
+                                                     int64_t N, int64_t d, int64_t Vt, int K) {
+    const int64_t blk = blockIdx.x;
+    const int64_t b0 = blk * EMB_P, b1 = std::min<int64_t>(N, b0 + EMB_P);
+    const int64_t c = ((int64_t)blockIdx.y * 64 + threadIdx.x) * 4;
+    const bool on = c < d;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    int cur = skey[b0];
+    int64_t rs = b0;
+    auto flush = [&](int key, int64_t s0, int64_t s1) {
+        if (key == K || !on) return;
+        const bool start_in = s0 > b0 || s0 == 0 || skey[s0 - 1] != key;
+        const bool end_in = s1 < b1 || s1 == N || skey[s1] != key;
+        if (start_in && end_in) {
+            f32x4* dst = (f32x4*)(emb_row(gt, gm, key, Vt, d) + c);
+            *dst = *dst + acc;
+        } else {
+            *(f32x4*)(part + (blk * 2 + (s0 == b0 ? 0 : 1)) * d + c) = acc;
+        }
+    };
+    for (int64_t j0 = b0; j0 < b1; j0 += 8) {
+        f32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {  // 8 row loads in flight before the ordered adds
+            v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (j0 + u < b1 && on) v[u] = *(const f32x4*)(dx + (int64_t)spos[j0 + u] * d + c);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t j = j0 + u;
+            if (j < b1) {
+                const int k = skey[j];
+                if (k != cur) {
+                    flush(cur, rs, j);
+                    acc = f32x4{0.f, 0.f, 0.f, 0.f};
+                    cur = k;
+                    rs = j;
+                }
+                acc = acc + v[u];
+            }
+        }
+    }
+    flush(cur, rs, b1);
+}
+
+// grid (blocks, column slices), one wave: the block in which a run that began in
+// an earlier block ends sums the run's partials (first block's, then one per
+// block) and adds them to the table row
+__global__ __launch_bounds__(64) void emb_fix_kernel(float* __restrict__ gt, float* __restrict__ gm,
+                                                     const float* __restrict__ part, const int* __restrict__ skey,
+                                                     int64_t N, int64_t d, int64_t Vt, int K) {
+    const int64_t blk = blockIdx.x;
+    const int64_t b0 = blk * EMB_P, b1 = std::min<int64_t>(N, b0 + EMB_P);
+    if (blk == 0) return;
+    const int key = skey[b0];
+    if (key == K || skey[b0 - 1] != key || (b1 < N && skey[b1] == key)) return;
+    const int64_t c = ((int64_t)blockIdx.y * 64 + threadIdx.x) * 4;
+    if (c >= d) return;
+    int64_t lo = 0, hi = b0 - 1;  // first sorted row of the key (skey[hi] == key)
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) / 2;
+        if (skey[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    const int64_t s = lo;
+    f32x4 acc = *(const f32x4*)(part + ((s / EMB_P) * 2 + (s % EMB_P == 0 ? 0 : 1)) * d + c);
+    for (int64_t k = s / EMB_P + 1; k <= blk; ++k) acc = acc + *(const f32x4*)(part + k * 2 * d + c);
+    f32x4* dst = (f32x4*)(emb_row(gt, gm, key, Vt, d) + c);
+    *dst = *dst + acc;
+}
+
+namespace {
+struct EmbWs {
+    int64_t N, nch, nblk, ncnt;
+    int passes;
+    size_t o_cnt, o_rank, o_k0, o_p0, o_k1, o_p1, o_part, total;
+};
+size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+EmbWs emb_ws(int64_t B, int64_t T, int64_t nm, int64_t d, int64_t Vt, int64_t Vm) {
+    EmbWs w;
+    w.N = B * (T + nm);
+    w.nch = (w.N + EMB_CH - 1) / EMB_CH;
+    w.nblk = (w.N + EMB_P - 1) / EMB_P;
+    w.ncnt = 256 * w.nch;
+    w.passes = 1;
+    while ((Vt + Vm) >> (8 * w.passes)) ++w.passes;  // digits of the largest key K
+    const size_t nb = al16(w.N * 4);
+    w.o_cnt = 0;
+    w.o_rank = al16((w.ncnt + 1) * 4);
+    w.o_k0 = w.o_rank + nb;
+    w.o_p0 = w.o_k0 + nb;
+    w.o_k1 = w.o_p0 + nb;
+    w.o_p1 = w.o_k1 + nb;
+    w.o_part = w.o_p1 + nb;
+    w.total = w.o_part + al16(w.nblk * 2 * d * 4);
+    return w;
+}
+}  // namespace
+
+extern "C" size_t msq_embed_bwd_workspace(int64_t B, int64_t T, int64_t n_meta, int64_t d, int64_t V_tok,
+                                          int64_t V_meta) {
+    return emb_ws(B, T, n_meta, d, V_tok, V_meta).total;
+}
+
+extern "C" int msq_embed_bwd_sorted(float* g_tok, float* g_meta, const float* dx, const int64_t* idx,
+                                    const int64_t* meta, int64_t B, int64_t T, int64_t n_meta, int64_t d,
+                                    int64_t V_tok, int64_t V_meta, void* workspace, void* stream) {
+    MSQ_CHECK_ARG(B > 0 && T >= 0 && n_meta >= 0 && d > 0 && d % 4 == 0 && V_tok > 0 && V_meta >= 0 && workspace,
+                  "msq_embed_bwd_sorted: bad sizes or no workspace");
+    const EmbWs w = emb_ws(B, T, n_meta, d, V_tok, V_meta);
+    MSQ_CHECK_ARG(w.N < INT32_MAX && V_tok + V_meta < INT32_MAX, "msq_embed_bwd_sorted: more than 2^31 rows or keys");
+    MSQ_CHECK_ARG(((uintptr_t)workspace % 16) == 0, "msq_embed_bwd_sorted: workspace must be 16-B aligned");
+    if (w.N == 0) return MSQ_OK;
+    hipStream_t s = (hipStream_t)stream;
+    char* ws = (char*)workspace;
+    int* cnt = (int*)(ws + w.o_cnt);
+    int* rank = (int*)(ws + w.o_rank);
+    int* key[2] = {(int*)(ws + w.o_k0), (int*)(ws + w.o_k1)};
+    int* pos[2] = {(int*)(ws + w.o_p0), (int*)(ws + w.o_p1)};
+    float* part = (float*)(ws + w.o_part);
+    const int K = (int)(V_tok + V_meta);
+    const int slices = (int)((d / 4 + 63) / 64);
+    const unsigned rows256 = (unsigned)((w.N + 255) / 256);
+    hipLaunchKernelGGL(emb_key_kernel, dim3(rows256), dim3(256), 0, s, key[0], pos[0], idx, meta, w.N, T, n_meta,
+                       V_tok, V_meta);
+    for (int p = 0; p < w.passes; ++p) {
+        const int in = p & 1, shift = 8 * p;
+        if (hipMemsetAsync(cnt, 0, w.ncnt * 4, s) != hipSuccess)
+            return msq_set_error(MSQ_ERR_HIP, "msq_embed_bwd_sorted: memset");
+        hipLaunchKernelGGL(emb_rank_kernel, dim3((unsigned)w.nch), dim3(EMB_CH), 0, s, cnt, rank, key[in], w.N, shift,
+                           w.nch);
+        hipLaunchKernelGGL(emb_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, w.ncnt);
+        hipLaunchKernelGGL(emb_scatter_kernel, dim3(rows256), dim3(256), 0, s, key[in ^ 1], pos[in ^ 1], cnt, rank,
+                           key[in], pos[in], w.N, shift, w.nch);
+    }
+    const int out = w.passes & 1;
+    hipLaunchKernelGGL(emb_sum_kernel, dim3((unsigned)w.nblk, slices), dim3(64), 0, s, g_tok, g_meta, part, dx,
+                       pos[out], key[out], w.N, d, V_tok, K);
+    hipLaunchKernelGGL(emb_fix_kernel, dim3((unsigned)w.nblk, slices), dim3(64), 0, s, g_tok, g_meta, part, key[out],
+                       w.N, d, V_tok, K);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
 // ------------------------------------------------------------------ LayerNorm
 // one wave per row; the row (d <= 64*4*MAXC) is held in registers.
 // Row r of the compact output maps to input row

@@ -144,10 +144,18 @@ def embed_fwd(x, tok_table, meta_table, idx, meta):
     return x
 
 
-def embed_bwd(g_tok, g_meta, dx, idx, meta):
+def embed_bwd(g_tok, g_meta, dx, idx, meta, deterministic=True):
+    """g_tok[idx] += dx token rows, g_meta[meta] += dx metadata rows. deterministic:
+    sorted segment sums (bitwise reproducible); else fp32 atomics."""
     B, T = idx.shape
-    call("msq_embed_bwd", ptr(g_tok), ptr(g_meta), ptr(dx), ptr(idx), ptr(meta), B, T, meta.shape[1],
-         g_tok.shape[1], stream())
+    nm, d = meta.shape[1], g_tok.shape[1]
+    if not deterministic:
+        call("msq_embed_bwd", ptr(g_tok), ptr(g_meta), ptr(dx), ptr(idx), ptr(meta), B, T, nm, d, stream())
+        return
+    Vt, Vm = g_tok.shape[0], g_meta.shape[0]
+    ws = workspace(L.lib().msq_embed_bwd_workspace(B, T, nm, d, Vt, Vm), dx.device, "embed")
+    call("msq_embed_bwd_sorted", ptr(g_tok), ptr(g_meta), ptr(dx), ptr(idx), ptr(meta), B, T, nm, d, Vt, Vm,
+         ptr(ws), stream())
 
 
 def cast(dst, src):

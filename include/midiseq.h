@@ -57,6 +57,14 @@ int msq_embed_fwd(float* x, const float* tok_table, const float* meta_table, con
  * (fp32 atomics; caller zeroes or accumulates).                               */
 int msq_embed_bwd(float* g_tok, float* g_meta, const float* dx, const int64_t* idx, const int64_t* meta,
                   int64_t B, int64_t T, int64_t n_meta, int64_t d, void* stream);
+/* deterministic form of msq_embed_bwd (bitwise reproducible): a stable
+ * counting sort of the dx rows by table row, then in-order segment sums.
+ * Table sizes V_tok / V_meta are needed for the sort; ids outside them are
+ * dropped. workspace: msq_embed_bwd_workspace() bytes, 16-B aligned.          */
+size_t msq_embed_bwd_workspace(int64_t B, int64_t T, int64_t n_meta, int64_t d, int64_t V_tok, int64_t V_meta);
+int msq_embed_bwd_sorted(float* g_tok, float* g_meta, const float* dx, const int64_t* idx, const int64_t* meta,
+                         int64_t B, int64_t T, int64_t n_meta, int64_t d, int64_t V_tok, int64_t V_meta,
+                         void* workspace, void* stream);
 
 /* ---- LayerNorm (nn.LayerNorm, model_transformer.py:115-116,146; mamba.py:25)
  * y = (x - mean) * rstd * gamma + beta; x fp32; y in y_dtype, compact [rows, d].

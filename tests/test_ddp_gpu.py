@@ -58,6 +58,7 @@ def test_world2_same_data_equals_single_process(kind, tmp_path):
     g, flat, loss = _single(kind, slice(0, 2))
     assert abs(float(got["loss"]) - loss) <= 1e-5 * abs(loss)
     err = np.abs(got["grads"] - g).max()
+    print(f"\n{kind} same-data max |grad diff| = {err:.3e} (max |g| {np.abs(g).max():.3e})")
     assert err <= 1e-5 * np.abs(g).max(), err
     # parameters after one Adam step (scale 1/world folded into the kernel).
     # Step 1 of Adam moves each parameter by lr * g / (|g| + eps): where |g| is

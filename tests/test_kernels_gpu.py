@@ -223,9 +223,70 @@ def test_embedding():
     dx = torch.randn(B, T + 6, d, generator=g)
     gt = torch.zeros(V, d, device=dev)
     gm = torch.zeros(MV, d, device=dev)
-    ops.embed_bwd(gt, gm, dx.to(dev), idx.to(dev), meta.to(dev))
+    ops.embed_bwd(gt, gm, dx.to(dev), idx.to(dev), meta.to(dev), deterministic=False)
     rt = torch.zeros(V, d).index_add_(0, idx.reshape(-1), dx[:, 6:].reshape(-1, d))
     rm = torch.zeros(MV, d).index_add_(0, meta.reshape(-1), dx[:, :6].reshape(-1, d))
+    assert _rel(gt, rt) < 1e-5 and _rel(gm, rm) < 1e-5
+
+
+def _embed_bwd_seq(V, MV, idx, meta, dx):
+    """fp64 scatter-add in sequence order (the order the sorted path sums in)."""
+    d = dx.shape[-1]
+    nm = meta.shape[1]
+    rt = torch.zeros(V, d, dtype=torch.float64)
+    rm = torch.zeros(MV, d, dtype=torch.float64)
+    rt.index_add_(0, idx.reshape(-1), dx[:, nm:].reshape(-1, d).double())
+    rm.index_add_(0, meta.reshape(-1), dx[:, :nm].reshape(-1, d).double())
+    return rt, rm
+
+
+@pytest.mark.parametrize("case", ["small", "skewed", "ragged_d", "one_hot_key", "large"])
+def test_embedding_sorted_deterministic(case):
+    """msq_embed_bwd_sorted: same sums as the fp64 scatter-add and bitwise equal
+    across repeats (the atomic path is not). 'skewed': one token id holds half
+    the rows, so its sorted run spans many 64-row blocks (partials + fix pass);
+    'one_hot_key': every row the same id; 'large': cfg-2 vocabularies and width (two radix passes)."""
+    g = torch.Generator().manual_seed(11)
+    V, MV, d, B, T, nm = {"small": (50, 9, 64, 3, 17, 6), "skewed": (300, 20, 256, 4, 700, 6),
+                          "ragged_d": (37, 5, 516, 2, 333, 3), "one_hot_key": (10, 4, 128, 3, 500, 2),
+                          "large": (17914, 568, 1024, 4, 2048, 6)}[case]
+    idx = torch.randint(0, V, (B, T), generator=g)
+    meta = torch.randint(0, MV, (B, nm), generator=g)
+    if case == "skewed":
+        hot = torch.rand(B, T, generator=g) < 0.5
+        idx[hot] = 7
+    if case == "one_hot_key":
+        idx.fill_(3)
+        meta.fill_(1)
+    dx = torch.randn(B, T + nm, d, generator=g)
+    outs = []
+    for _ in range(2):
+        gt = torch.full((V, d), 0.5, device=dev)  # accumulates into what is there
+        gm = torch.full((MV, d), -0.25, device=dev)
+        ops.embed_bwd(gt, gm, dx.to(dev), idx.to(dev), meta.to(dev))
+        outs.append((gt.cpu(), gm.cpu()))
+    rt, rm = _embed_bwd_seq(V, MV, idx, meta, dx)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert (outs[0][0].double() - 0.5 - rt).abs().max() <= 1e-5 * (1 + rt.abs().max())
+    assert (outs[0][1].double() + 0.25 - rm).abs().max() <= 1e-5 * (1 + rm.abs().max())
+
+
+def test_embedding_sorted_drops_out_of_range_ids():
+    g = torch.Generator().manual_seed(12)
+    V, MV, d, B, T, nm = 20, 6, 64, 2, 90, 3
+    idx = torch.randint(0, V, (B, T), generator=g)
+    meta = torch.randint(0, MV, (B, nm), generator=g)
+    idx[0, :5] = V + 3
+    idx[1, 7] = -1
+    meta[1, 0] = MV
+    dx = torch.randn(B, T + nm, d, generator=g)
+    gt = torch.zeros(V, d, device=dev)
+    gm = torch.zeros(MV, d, device=dev)
+    ops.embed_bwd(gt, gm, dx.to(dev), idx.to(dev), meta.to(dev))
+    ok_t = (idx >= 0) & (idx < V)
+    ok_m = meta < MV
+    rt = torch.zeros(V, d).index_add_(0, idx[ok_t], dx[:, nm:][ok_t])
+    rm = torch.zeros(MV, d).index_add_(0, meta[ok_m], dx[:, :nm][ok_m])
     assert _rel(gt, rt) < 1e-5 and _rel(gm, rm) < 1e-5
 
 
