@@ -65,7 +65,7 @@ extern "C" int msq_embed_bwd(float* g_tok, float* g_meta, const float* dx, const
 //   key:     keys[r], pos[r] = r
 //   per pass rank: per 256-row chunk, a row's rank among the equal digits before
 //                  it (LDS compare); the chunk's last one writes cnt[digit][chunk]
-//            scan: exclusive scan of cnt (digit-major) = where each
+//            scan: exclusive scan of cnt (digit-major, two launches) = where each
 //                  (digit, chunk) group lands
 //            scatter: (key, pos) to its place
 //   sum:     blocks of EMB_P sorted rows, one wave per 256 columns: a key run
@@ -119,29 +119,53 @@ __global__ __launch_bounds__(EMB_CH) void emb_rank_kernel(int* __restrict__ cnt,
     }
 }
 
-// exclusive scan of n ints in place, one workgroup; a[n] = total
-__global__ __launch_bounds__(1024) void emb_scan_kernel(int* __restrict__ a, int64_t n) {
-    __shared__ int part[1024];
+// exclusive scan of n ints in place (n % 4 == 0), two launches: each 1024-thread
+// block scans 4096 ints (int4 per thread, LDS scan of the thread sums) and
+// leaves its total; then every block adds the totals of the blocks before it.
+// a[n] = the grand total.
+#define EMB_SCAN 4096
+__device__ __forceinline__ int block_excl_scan(int v, int* lds) {  // 1024 threads
     const int tid = threadIdx.x;
-    const int64_t per = (n + 1023) / 1024;
-    const int64_t lo = std::min<int64_t>(n, tid * per), hi = std::min<int64_t>(n, lo + per);
-    int s = 0;
-    for (int64_t i = lo; i < hi; ++i) s += a[i];
-    part[tid] = s;
+    lds[tid] = v;
     __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan of the partials
-        const int v = tid >= off ? part[tid - off] : 0;
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int u = tid >= off ? lds[tid - off] : 0;
         __syncthreads();
-        part[tid] += v;
+        lds[tid] += u;
         __syncthreads();
     }
-    int run = tid ? part[tid - 1] : 0;
-    for (int64_t i = lo; i < hi; ++i) {
-        const int c = a[i];
-        a[i] = run;
-        run += c;
+    return lds[tid] - v;
+}
+
+__global__ __launch_bounds__(1024) void emb_scan_local_kernel(int* __restrict__ a, int* __restrict__ tot, int64_t n) {
+    __shared__ int lds[1024];
+    const int64_t i = (int64_t)blockIdx.x * EMB_SCAN + threadIdx.x * 4;
+    int4 v = {0, 0, 0, 0};
+    if (i < n) v = *(const int4*)(a + i);
+    const int ex = block_excl_scan(v.x + v.y + v.z + v.w, lds);
+    if (i < n) *(int4*)(a + i) = int4{ex, ex + v.x, ex + v.x + v.y, ex + v.x + v.y + v.z};
+    if (threadIdx.x == 1023) tot[blockIdx.x] = lds[1023];
+}
+
+__global__ __launch_bounds__(1024) void emb_scan_add_kernel(int* __restrict__ a, const int* __restrict__ tot,
+                                                            int64_t n) {
+    __shared__ int lds[1024];
+    const int g = blockIdx.x;
+    int s = 0;
+    for (int h = threadIdx.x; h < g; h += 1024) s += tot[h];
+    lds[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 512; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) lds[threadIdx.x] += lds[threadIdx.x + off];
+        __syncthreads();
     }
-    if (tid == 1023) a[n] = part[1023];
+    const int pre = lds[0];
+    const int64_t i = (int64_t)g * EMB_SCAN + threadIdx.x * 4;
+    if (i < n) {
+        int4 v = *(const int4*)(a + i);
+        *(int4*)(a + i) = int4{v.x + pre, v.y + pre, v.z + pre, v.w + pre};
+    }
+    if (g == (int)gridDim.x - 1 && threadIdx.x == 0) a[n] = pre + tot[g];
 }
 
 __global__ void emb_scatter_kernel(int* __restrict__ key_out, int* __restrict__ pos_out, const int* __restrict__ off,
@@ -159,44 +183,55 @@ __device__ __forceinline__ float* emb_row(float* gt, float* gm, int key, int64_t
     return key < Vt ? gt + (int64_t)key * d : gm + ((int64_t)key - Vt) * d;
 }
 
-// grid (blocks of EMB_P sorted rows, column slices of 256), one wave
+// grid (blocks of EMB_P sorted rows, column slices of 256), one wave. Lane j
+// holds the block's j-th (row, key); rows are broadcast with readlane so 16
+// row loads are in flight before the ordered adds.
 __global__ __launch_bounds__(64) void emb_sum_kernel(float* __restrict__ gt, float* __restrict__ gm,
                                                      float* __restrict__ part, const float* __restrict__ dx,
                                                      const int* __restrict__ spos, const int* __restrict__ skey,
                                                      int64_t N, int64_t d, int64_t Vt, int K) {
+    static_assert(EMB_P == 64, "one sorted row per lane");
     const int64_t blk = blockIdx.x;
-    const int64_t b0 = blk * EMB_P, b1 = std::min<int64_t>(N, b0 + EMB_P);
-    const int64_t c = ((int64_t)blockIdx.y * 64 + threadIdx.x) * 4;
+    const int64_t b0 = blk * EMB_P;
+    const int n = (int)std::min<int64_t>(EMB_P, N - b0);
+    const int lane = threadIdx.x;
+    const int64_t c = ((int64_t)blockIdx.y * 64 + lane) * 4;
     const bool on = c < d;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    int cur = skey[b0];
-    int64_t rs = b0;
-    auto flush = [&](int key, int64_t s0, int64_t s1) {
+    const int myp = lane < n ? spos[b0 + lane] : 0;
+    const int myk = lane < n ? skey[b0 + lane] : -1;
+    const int prevk = b0 > 0 ? skey[b0 - 1] : -1;  // the keys either side of the block
+    const int nextk = b0 + n < N ? skey[b0 + n] : -1;
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc = zero;
+    int cur = __builtin_amdgcn_readlane(myk, 0);
+    int rs = 0;
+    auto flush = [&](int key, int s0, int s1) {
         if (key == K || !on) return;
-        const bool start_in = s0 > b0 || s0 == 0 || skey[s0 - 1] != key;
-        const bool end_in = s1 < b1 || s1 == N || skey[s1] != key;
+        const bool start_in = s0 > 0 || prevk != key;
+        const bool end_in = s1 < n || nextk != key;
         if (start_in && end_in) {
             f32x4* dst = (f32x4*)(emb_row(gt, gm, key, Vt, d) + c);
             *dst = *dst + acc;
         } else {
-            *(f32x4*)(part + (blk * 2 + (s0 == b0 ? 0 : 1)) * d + c) = acc;
+            *(f32x4*)(part + (blk * 2 + (s0 == 0 ? 0 : 1)) * d + c) = acc;
         }
     };
-    for (int64_t j0 = b0; j0 < b1; j0 += 8) {
-        f32x4 v[8];
+    for (int j0 = 0; j0 < n; j0 += 16) {
+        f32x4 v[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {  // 8 row loads in flight before the ordered adds
-            v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (j0 + u < b1 && on) v[u] = *(const f32x4*)(dx + (int64_t)spos[j0 + u] * d + c);
+        for (int u = 0; u < 16; ++u) {
+            const int j = j0 + u;
+            const int row = __builtin_amdgcn_readlane(myp, j & 63);
+            v[u] = (j < n && on) ? *(const f32x4*)(dx + (int64_t)row * d + c) : zero;
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int64_t j = j0 + u;
-            if (j < b1) {
-                const int k = skey[j];
+        for (int u = 0; u < 16; ++u) {
+            const int j = j0 + u;
+            if (j < n) {
+                const int k = __builtin_amdgcn_readlane(myk, j & 63);
                 if (k != cur) {
                     flush(cur, rs, j);
-                    acc = f32x4{0.f, 0.f, 0.f, 0.f};
+                    acc = zero;
                     cur = k;
                     rs = j;
                 }
@@ -204,7 +239,7 @@ __global__ __launch_bounds__(64) void emb_sum_kernel(float* __restrict__ gt, flo
             }
         }
     }
-    flush(cur, rs, b1);
+    flush(cur, rs, n);
 }
 
 // grid (blocks, column slices), one wave: the block in which a run that began in
@@ -236,7 +271,8 @@ namespace {
 struct EmbWs {
     int64_t N, nch, nblk, ncnt;
     int passes;
-    size_t o_cnt, o_rank, o_k0, o_p0, o_k1, o_p1, o_part, total;
+    int64_t nscan;
+    size_t o_cnt, o_tot, o_rank, o_k0, o_p0, o_k1, o_p1, o_part, total;
 };
 size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 EmbWs emb_ws(int64_t B, int64_t T, int64_t nm, int64_t d, int64_t Vt, int64_t Vm) {
@@ -248,8 +284,10 @@ EmbWs emb_ws(int64_t B, int64_t T, int64_t nm, int64_t d, int64_t Vt, int64_t Vm
     w.passes = 1;
     while ((Vt + Vm) >> (8 * w.passes)) ++w.passes;  // digits of the largest key K
     const size_t nb = al16(w.N * 4);
+    w.nscan = (w.ncnt + EMB_SCAN - 1) / EMB_SCAN;
     w.o_cnt = 0;
-    w.o_rank = al16((w.ncnt + 1) * 4);
+    w.o_tot = al16((w.ncnt + 1) * 4);
+    w.o_rank = w.o_tot + al16(w.nscan * 4);
     w.o_k0 = w.o_rank + nb;
     w.o_p0 = w.o_k0 + nb;
     w.o_k1 = w.o_p0 + nb;
@@ -277,6 +315,7 @@ extern "C" int msq_embed_bwd_sorted(float* g_tok, float* g_meta, const float* dx
     hipStream_t s = (hipStream_t)stream;
     char* ws = (char*)workspace;
     int* cnt = (int*)(ws + w.o_cnt);
+    int* tot = (int*)(ws + w.o_tot);
     int* rank = (int*)(ws + w.o_rank);
     int* key[2] = {(int*)(ws + w.o_k0), (int*)(ws + w.o_k1)};
     int* pos[2] = {(int*)(ws + w.o_p0), (int*)(ws + w.o_p1)};
@@ -292,7 +331,8 @@ extern "C" int msq_embed_bwd_sorted(float* g_tok, float* g_meta, const float* dx
             return msq_set_error(MSQ_ERR_HIP, "msq_embed_bwd_sorted: memset");
         hipLaunchKernelGGL(emb_rank_kernel, dim3((unsigned)w.nch), dim3(EMB_CH), 0, s, cnt, rank, key[in], w.N, shift,
                            w.nch);
-        hipLaunchKernelGGL(emb_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, w.ncnt);
+        hipLaunchKernelGGL(emb_scan_local_kernel, dim3((unsigned)w.nscan), dim3(1024), 0, s, cnt, tot, w.ncnt);
+        hipLaunchKernelGGL(emb_scan_add_kernel, dim3((unsigned)w.nscan), dim3(1024), 0, s, cnt, tot, w.ncnt);
         hipLaunchKernelGGL(emb_scatter_kernel, dim3(rows256), dim3(256), 0, s, key[in ^ 1], pos[in ^ 1], cnt, rank,
                            key[in], pos[in], w.N, shift, w.nch);
     }
