@@ -32,6 +32,11 @@ def main():
     shapes = [("mamba in_proj", 64, 4384, 1024, L.EPI_NONE), ("mamba out_proj", 64, 1024, 2048, L.EPI_NONE),
               ("lm_head", 64, 17914, 1024, L.EPI_BIAS), ("tf qkv", 64, 3072, 1024, L.EPI_NONE),
               ("tf ffn1", 64, 4096, 1024, L.EPI_BIAS_RELU), ("tf ffn2", 64, 1024, 4096, L.EPI_BIAS)]
+    if len(sys.argv) > 1 and sys.argv[1] == "probe":  # overhead structure of the persistent kernel
+        shapes = [("probe m16", 16, 4384, 1024, L.EPI_NONE), ("probe m32", 32, 4384, 1024, L.EPI_NONE),
+                  ("probe n256", 64, 256, 1024, L.EPI_NONE), ("probe n4096", 64, 4096, 1024, L.EPI_NONE),
+                  ("probe n8192", 64, 8192, 1024, L.EPI_NONE), ("probe n16384", 64, 16384, 1024, L.EPI_NONE),
+                  ("probe k512", 64, 4384, 512, L.EPI_NONE)]
     print(f"{'shape':16s} {'M':>3s} {'N':>6s} {'K':>5s} {'msq us':>8s} {'GB/s':>7s} {'blas us':>8s} {'GB/s':>7s}")
     for name, M, N, K, epi in shapes:
         x = torch.randn(M, K, device=dev, generator=g).bfloat16()
