@@ -396,7 +396,19 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(TY* __restrict__ y, float* 
     }
 }
 
-constexpr int LN_BWD_BLOCKS = 512;
+// persistent grid of the LayerNorm backward (4 rows in flight per block); the
+// partial-sum workspace is sized for the largest grid. 768 = 3 waves per SIMD,
+// the kernel's VGPR-bound occupancy: 3.57 ms per cfg-2 step against 4.43 at
+// 512 and 4.72 at 1024 (same box). MSQ_LNB_BLOCKS: A/B switch.
+constexpr int LN_BWD_MAX_BLOCKS = 1024;
+static int ln_bwd_blocks() {
+    static const int nb = [] {
+        const char* e = getenv("MSQ_LNB_BLOCKS");
+        const int v = e ? atoi(e) : 768;
+        return v < 64 ? 64 : (v > LN_BWD_MAX_BLOCKS ? LN_BWD_MAX_BLOCKS : v);
+    }();
+    return nb;
+}
 
 // dropout keep mask applied to the copy (the gradient into the dropped branch)
 struct CopyDrop {
@@ -544,7 +556,7 @@ __global__ __launch_bounds__(256) void ln_reduce_kernel(float* __restrict__ dg, 
 
 extern "C" size_t msq_layernorm_bwd_workspace(int64_t rows, int64_t d) {
     (void)rows;
-    return (size_t)LN_BWD_BLOCKS * 3 * d * sizeof(float);
+    return (size_t)LN_BWD_MAX_BLOCKS * 3 * d * sizeof(float);
 }
 
 template <typename TY>
@@ -572,7 +584,7 @@ template <typename TD, typename TO, bool BIAS>
 static void ln_bwd_launch_b(float* dxa, TO* dcopy, float* part, const TD* dy, const float* x, const float* mean,
                             const float* rstd, const float* gamma, int64_t rows, int d, int64_t seg, int64_t skip,
                             CopyDrop cd, hipStream_t s) {
-    const dim3 grid(LN_BWD_BLOCKS);
+    const dim3 grid(ln_bwd_blocks());
     if (d <= 256) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 1, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
     else if (d <= 1024) {
         static const bool pf = getenv("MSQ_LNB_PF") != nullptr;  // A/B switch: dx_acc read with x and dy
@@ -628,7 +640,7 @@ extern "C" int msq_layernorm_bwd_bias(float* dx_acc, void* dx_copy, int copy_dty
     }
     const int nout = (bias ? 3 : 2) * di;
     hipLaunchKernelGGL(ln_reduce_kernel, dim3((unsigned)((nout + 63) / 64)), dim3(256), 0, s, dgamma, dbeta, dbias,
-                       part, LN_BWD_BLOCKS, di, nout);
+                       part, ln_bwd_blocks(), di, nout);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }

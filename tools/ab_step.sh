@@ -1,8 +1,8 @@
 #!/bin/bash
-# Mamba decode: fused in_proj + conv step (default) vs the two-launch path (MSQ_NO_CONV_FUSE=1).
+# Same-box A/B of the LayerNorm backward grid (MSQ_LNB_BLOCKS) and its dx_acc prefetch (MSQ_LNB_PF).
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python -u -m pytest tests/test_mamba_decode_gpu.py tests/test_generate_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/dect.log 2>&1; rc=$?; tail -3 gpurun_out/dect.log; [ $rc = 0 ] || exit 1
-for v in fused two fused two; do
-  if [ $v = two ]; then export MSQ_NO_CONV_FUSE=1; else unset MSQ_NO_CONV_FUSE; fi
-  echo "== $v"; timeout -k 10 120 python -u tools/decode_prof.py mamba 60 2>&1 | grep -v amdgpu.ids | tail -4 || exit 1
-done
+run() { tag=$1; shift
+  env "$@" timeout -k 10 200 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-extra > gpurun_out/ab_$tag.json 2>gpurun_out/ab.err || return 1
+  python -c "import json;d=json.load(open('gpurun_out/ab_$tag.json'));c=d['classes'];print('$tag', d['ms_per_step'], 'lnb', c['other:layernorm_bwd_bias']['ms_per_step'])"
+}
+run b512 A=1 && run b768 MSQ_LNB_BLOCKS=768 && run b1024 MSQ_LNB_BLOCKS=1024 && run b768pf MSQ_LNB_BLOCKS=768 MSQ_LNB_PF=1 && run b1024pf MSQ_LNB_BLOCKS=1024 MSQ_LNB_PF=1 && run b512_2 A=1 && run b768_2 MSQ_LNB_BLOCKS=768 && run b1024_2 MSQ_LNB_BLOCKS=1024
