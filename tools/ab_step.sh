@@ -1,8 +1,6 @@
 #!/bin/bash
-# Same-box A/B of the LayerNorm backward grid (MSQ_LNB_BLOCKS) and its dx_acc prefetch (MSQ_LNB_PF).
+# Loss-path check after a kernel change: loss / transformer / DDP GPU tests, then the bench line.
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-run() { tag=$1; shift
-  env "$@" timeout -k 10 200 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-extra > gpurun_out/ab_$tag.json 2>gpurun_out/ab.err || return 1
-  python -c "import json;d=json.load(open('gpurun_out/ab_$tag.json'));c=d['classes'];print('$tag', d['ms_per_step'], 'lnb', c['other:layernorm_bwd_bias']['ms_per_step'])"
-}
-run b512 A=1 && run b768 MSQ_LNB_BLOCKS=768 && run b1024 MSQ_LNB_BLOCKS=1024 && run b768pf MSQ_LNB_BLOCKS=768 MSQ_LNB_PF=1 && run b1024pf MSQ_LNB_BLOCKS=1024 MSQ_LNB_PF=1 && run b512_2 A=1 && run b768_2 MSQ_LNB_BLOCKS=768 && run b1024_2 MSQ_LNB_BLOCKS=1024
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_transformer_gpu.py tests/test_train_gpu.py tests/test_ddp_gpu.py tests/test_fullsize_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/lt.log 2>&1; rc=$?; tail -3 gpurun_out/lt.log; [ $rc = 0 ] || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pm -o run --output-format csv -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra > gpurun_out/pm.log 2>&1 || exit 1
+grep -h "mean_kernel" gpurun_out/pm/run_kernel_stats.csv | cut -c1-120
