@@ -664,28 +664,31 @@ __global__ __launch_bounds__(256) void gnorm_fwd_row_kernel(const float* __restr
 // lane owns columns 4 lane + 256 k, k < NK (NK = ceil(d_inner / 256), compile time).
 constexpr int GN_K = 16;
 template <typename TZ, typename TD, int NK>
-__global__ __launch_bounds__(256) void gnorm_bwd_kernel(const float* __restrict__ y, int64_t ldy,
-                                                        const TZ* __restrict__ z, int64_t ldz,
-                                                        const float* __restrict__ w, const float* __restrict__ rstd,
-                                                        const float* __restrict__ dout, int64_t ldd,
-                                                        float* __restrict__ dy, TD* __restrict__ dz,
-                                                        float* __restrict__ dw, int64_t rows, int dn) {
-    const int lane = threadIdx.x & 63;
-    float pw[NK][4];
+__global__ __launch_bounds__(256, (NK >= 8 ? 3 : 1)) void gnorm_bwd_kernel(
+    const float* __restrict__ y, int64_t ldy, const TZ* __restrict__ z, int64_t ldz, const float* __restrict__ w,
+    const float* __restrict__ rstd, const float* __restrict__ dout, int64_t ldd, float* __restrict__ dy,
+    TD* __restrict__ dz, float* __restrict__ dw, int64_t rows, int dn) {
+    // ZRE (d_inner > 1024): z is read again in the second pass instead of held,
+    // and the dw partials live in each wave's LDS slice (lane-owned columns), so
+    // the kernel fits 168 VGPRs (3 waves per SIMD; holding all of it took 256)
+    constexpr bool ZRE = NK >= 8;
+    const int lane = threadIdx.x & 63, ws = threadIdx.x >> 6;
+    __shared__ f32x4 red[4][64 * NK];
 #pragma unroll
-    for (int k = 0; k < NK; ++k) pw[k][0] = pw[k][1] = pw[k][2] = pw[k][3] = 0.f;
-    for (int64_t row = blockIdx.x * 4LL + (threadIdx.x >> 6); row < rows; row += (int64_t)gridDim.x * 4) {
+    for (int k = 0; k < NK; ++k) red[ws][lane + 64 * k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int64_t row = blockIdx.x * 4LL + ws; row < rows; row += (int64_t)gridDim.x * 4) {
         const float r = rstd[row];
-        f32x4 yv[NK], zv[NK], dv[NK];
+        f32x4 yv[NK], dv[NK], zv[ZRE ? 1 : NK];
         float s = 0.f;
 #pragma unroll
         for (int k = 0; k < NK; ++k) {
             const int c = lane * 4 + 256 * k;
-            yv[k] = zv[k] = dv[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            yv[k] = dv[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (!ZRE) zv[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
             if (c < dn) {
                 yv[k] = *(const f32x4*)(y + row * ldy + c);
-                zv[k] = load4(z + row * ldz + c);
                 dv[k] = *(const f32x4*)(dout + row * ldd + c);
+                if (!ZRE) zv[k] = load4(z + row * ldz + c);
             }
         }
 #pragma unroll
@@ -693,8 +696,9 @@ __global__ __launch_bounds__(256) void gnorm_bwd_kernel(const float* __restrict_
             const int c = lane * 4 + 256 * k;
             if (c >= dn) continue;
             const f32x4 wv = *(const f32x4*)(w + c);
+            const f32x4 zk = ZRE ? load4(z + row * ldz + c) : zv[ZRE ? 0 : k];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) s += dv[k][t] * wv[t] * yv[k][t] * silu(zv[k][t]) * r;
+            for (int t = 0; t < 4; ++t) s += dv[k][t] * wv[t] * yv[k][t] * silu(zk[t]) * r;
         }
         const float mdn = wave_sum(s) / dn;
 #pragma unroll
@@ -702,30 +706,30 @@ __global__ __launch_bounds__(256) void gnorm_bwd_kernel(const float* __restrict_
             const int c = lane * 4 + 256 * k;
             if (c >= dn) continue;
             const f32x4 wv = *(const f32x4*)(w + c);
-            f32x4 o, zo;
+            const f32x4 zk = ZRE ? load4(z + row * ldz + c) : zv[ZRE ? 0 : k];
+            f32x4 o, zo, pw = red[ws][lane + 64 * k];
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                const float sg = sigm(zv[k][t]);
-                const float sl = zv[k][t] * sg;
+                const float sg = sigm(zk[t]);
+                const float sl = zk[t] * sg;
                 const float n = yv[k][t] * sl * r;
                 const float dg = r * (dv[k][t] * wv[t] - n * mdn);
                 o[t] = dg * sl;
-                zo[t] = dg * yv[k][t] * sg * (1.f + zv[k][t] * (1.f - sg));
-                pw[k][t] += dv[k][t] * n;
+                zo[t] = dg * yv[k][t] * sg * (1.f + zk[t] * (1.f - sg));
+                pw[t] += dv[k][t] * n;
             }
+            red[ws][lane + 64 * k] = pw;
             *(f32x4*)(dy + row * ldy + c) = o;
             store4(dz + row * ldz + c, zo);
         }
     }
-    // dw: the 4 waves' column partials summed in LDS, then one atomic per column per block
-    __shared__ float red[4][256 * NK];
-    const int ws = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < NK; ++k)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) red[ws][lane * 4 + 256 * k + t] = pw[k][t];
+    // dw: the 4 waves' column partials summed, then one atomic per column per block
     __syncthreads();
-    for (int c = threadIdx.x; c < dn; c += 256) atomicAdd(dw + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+    const float* rf = (const float*)red;
+    for (int c = threadIdx.x; c < dn; c += 256) {
+        const int i = ((c % 256) / 4 + 64 * (c / 256)) * 4 + c % 4;  // column c: red[w][l + 64 k][t]
+        atomicAdd(dw + c, rf[i] + rf[64 * NK * 4 + i] + rf[2 * 64 * NK * 4 + i] + rf[3 * 64 * NK * 4 + i]);
+    }
 }
 
 template <typename TZ, typename TD>
@@ -1429,7 +1433,9 @@ extern "C" int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const float* y, int
                                    int64_t ldd, float* dw, int64_t rows, int64_t d_inner, void* stream) {
     MSQ_CHECK_ARG(rows > 0 && d_inner % 4 == 0 && d_inner <= 256 * GN_K, "mamba gnorm bwd: bad sizes");
     hipStream_t s = (hipStream_t)stream;
-    const dim3 grid(512);  // two workgroups per CU; each reduces its dw partials in LDS first
+    // persistent: 3 workgroups per CU (the wide-row kernel's occupancy); each
+    // reduces its dw partials in LDS first
+    const dim3 grid(768);
     if (dtype == MSQ_BF16)
         gnorm_bwd_launch<bf16, bf16>(grid, s, y, ldy, (const bf16*)zxbcdt, ldz, w, rstd, dout, ldd, dy, (bf16*)dzxbcdt,
                                      dw, rows, (int)d_inner);
