@@ -379,11 +379,22 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ 
     for (int64_t e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
         const int64_t z = e / per, r = e - z * per, m = r / nq, n = (r - m * nq) * 4;
         const float* w = ws + (z * M + m) * N + n;
-        f32x4 v = load4(w);
-        for (int k = 1; k < ksplit; ++k) v += load4(w + k * slice);
         float* cp = C + z * sC + m * ldc + n;
-        if (((uintptr_t)cp & 15) == 0) {
-            store4(cp, v + load4(cp));
+        const bool al = ((uintptr_t)cp & 15) == 0;
+        const f32x4 c0 = al ? load4(cp) : f32x4{0.f, 0.f, 0.f, 0.f};  // issued with the partials
+        f32x4 v = load4(w);
+        int k = 1;
+        for (; k + 3 < ksplit; k += 4) {  // 4 partial loads in flight; the sum order is unchanged
+            const f32x4 p0 = load4(w + k * slice), p1 = load4(w + (k + 1) * slice);
+            const f32x4 p2 = load4(w + (k + 2) * slice), p3 = load4(w + (k + 3) * slice);
+            v += p0;
+            v += p1;
+            v += p2;
+            v += p3;
+        }
+        for (; k < ksplit; ++k) v += load4(w + k * slice);
+        if (al) {
+            store4(cp, v + c0);
         } else {
             for (int t = 0; t < 4; ++t) cp[t] += v[t];
         }
