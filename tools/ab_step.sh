@@ -1,6 +1,8 @@
 #!/bin/bash
-# GEMM split-K reduction check: DDP / transformer GPU tests (bitwise paths), then the reduce kernel's rocprof time.
+# Adam kernel check: optimizer / DDP GPU tests, then the bench's adam class (two runs).
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_transformer_gpu.py tests/test_ddp_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/lt.log 2>&1; rc=$?; tail -3 gpurun_out/lt.log; [ $rc = 0 ] || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pk -o run --output-format csv -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra > gpurun_out/pk.log 2>&1 || exit 1
-grep -h "splitk_reduce\|gemm256_kernel<1, 1, 5" gpurun_out/pk/run_kernel_stats.csv | cut -c1-160
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_train_gpu.py tests/test_ddp_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/at.log 2>&1; rc=$?; tail -2 gpurun_out/at.log; [ $rc = 0 ] || exit 1
+for i in 1 2; do
+  timeout -k 10 200 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-extra > gpurun_out/ad$i.json 2>gpurun_out/ad.err || exit 1
+  python -c "import json;d=json.load(open('gpurun_out/ad$i.json'));c=d['classes'];print(d['ms_per_step'], 'adam', c['adam'])"
+done
