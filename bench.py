@@ -249,16 +249,23 @@ def timed(fn, steps, warmup, world, dev):
     return el
 
 
+def _group(world):
+    """decode legs: rows sharded over the default group (generate(group=True))"""
+    return True if world > 1 else None
+
+
 def decode_leg(dev, rank, world, steps=3, B=64, T=2048):
     """Config 5: B=64 composer-conditioned prompts of 2048 tokens per GPU
-    (replicas, no communication), exact sliding-window decode (full forward
-    + filtered logit + penalties + top-k + sampling per new token)."""
+    (the global batch of world x 64 rows sharded by row: generate(group=...),
+    one all-gather of the last tokens per step for the host-side k choice),
+    exact sliding-window decode (full forward + filtered logit + penalties +
+    top-k + sampling per new token)."""
     import random
     from midiseq.generate import generate
     m = Transformer(TransformerConfig(precision="bf16", dropout=0.0)).to(dev)
     src, _, meta = SyntheticMIDI(B, T, dev, rank, n_batches=1).batches[0]
-    el = timed(lambda: generate(m, T, src, meta, num_tokens=1, rng=random.Random(rank), device=dev), steps, 1,
-               world, dev)
+    el = timed(lambda: generate(m, T, src, meta, num_tokens=1, rng=random.Random(0), device=dev,
+                                group=_group(world)), steps, 1, world, dev)
     del m
     return {"value": round(world * B * steps / el, 2), "unit": "new tokens/s", "ms_per_token_step": round(el / steps * 1e3, 3),
             "config": {"workload": "cfg 5 exact sliding-window decode (full fwd per step)", "batch_per_gpu": B,
@@ -275,12 +282,12 @@ def mamba_decode_leg(dev, rank, world, B=64, T0=1024, K=64, steps=2):
     from midiseq.mamba import Mamba
     m = Mamba(precision="bf16").to(dev)
     src, _, meta = SyntheticMIDI(B, T0, dev, rank, n_batches=1).batches[0]
-    run = lambda n: generate(m, 2048, src, meta, num_tokens=n, rng=random.Random(rank), device=dev,  # noqa: E731
-                             mode="cached")
+    run = lambda n: generate(m, 2048, src, meta, num_tokens=n, rng=random.Random(0), device=dev,  # noqa: E731
+                             mode="cached", group=_group(world))
     el_pre = timed(lambda: run(1), steps, 1, world, dev)
     el_all = timed(lambda: run(1 + K), steps, 1, world, dev)
-    el_exact = timed(lambda: generate(m, 2048, src, meta, num_tokens=1, rng=random.Random(rank), device=dev),
-                     steps, 1, world, dev)
+    el_exact = timed(lambda: generate(m, 2048, src, meta, num_tokens=1, rng=random.Random(0), device=dev,
+                                      group=_group(world)), steps, 1, world, dev)
     del m
     ms_step = (el_all - el_pre) / (steps * K) * 1e3
     return {"value": round(world * B / (ms_step * 1e-3), 1), "unit": "new tokens/s", "ms_per_token_step": round(ms_step, 3),
@@ -342,8 +349,8 @@ def decode_cached_leg(dev, rank, world, B=64, T=2048, K=32, steps=2):
     from midiseq.generate import generate
     m = Transformer(TransformerConfig(precision="bf16", dropout=0.0)).to(dev).eval()
     src, _, meta = SyntheticMIDI(B, T, dev, rank, n_batches=1).batches[0]
-    run = lambda n: generate(m, T, src, meta, num_tokens=n, rng=random.Random(rank), device=dev,  # noqa: E731
-                             mode="cached", return_tensor=True)
+    run = lambda n: generate(m, T, src, meta, num_tokens=n, rng=random.Random(0), device=dev,  # noqa: E731
+                             mode="cached", return_tensor=True, group=_group(world))
     el_pre = timed(lambda: run(1), steps, 1, world, dev)
     el_all = timed(lambda: run(1 + K), steps, 1, world, dev)
     del m

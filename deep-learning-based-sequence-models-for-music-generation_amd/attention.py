@@ -24,8 +24,10 @@ def relattn_fwd(qkv, R, B, S, H, hs, scale, out=None, lse=None, n_meta=N_META, d
     return out, lse
 
 
-# workspace pointer -> (dtype, B, S, H) of the backward it last served (its zero
-# bands stay valid for the next backward of the same shape: msq_relattn_bwd_ws)
+# workspace slot ("attn", device, stream) -> (buffer address, (dtype, B, S, H,
+# n_meta)) of the backward it last served: its zero bands stay valid for the
+# next backward of the same shape in the SAME buffer (msq_relattn_bwd_ws). A
+# slot whose buffer was replaced (grown) has a new address and starts cold.
 _ws_served = {}
 
 
@@ -38,11 +40,12 @@ def relattn_bwd(dout, out, lse, qkv, R, B, S, H, hs, scale, dqkv=None, dR=None, 
     nbytes = L.lib().msq_relattn_bwd_workspace(dt(qkv), B, S, H)
     ws = workspace(nbytes, qkv.device, "attn")
     masks, p = drop if drop is not None else (None, 0.0)
-    key = (dt(qkv), B, S, H)
-    ready = int(_ws_served.get(ws.data_ptr()) == key)  # the "attn" workspace serves only this op
+    key = (dt(qkv), B, S, H, n_meta)
+    slot = ("attn", qkv.device, torch.cuda.current_stream(qkv.device).cuda_stream)
+    ready = int(_ws_served.get(slot) == (ws.data_ptr(), key))  # the "attn" workspace serves only this op
     call("msq_relattn_bwd_ws", dt(qkv), ptr(dqkv), dqkv.stride(0), ptr(dR), ptr(dout), dout.stride(0), ptr(out),
          ptr(lse), ptr(qkv), qkv.stride(0), ptr(R), B, S, H, hs, R.shape[1], float(scale), n_meta,
          ptr(masks[0]) if masks is not None else None, ptr(masks[1]) if masks is not None else None, float(p),
          ptr(ws), ready, stream())
-    _ws_served[ws.data_ptr()] = key
+    _ws_served[slot] = (ws.data_ptr(), key)
     return dqkv, dR

@@ -29,10 +29,22 @@ Cached mode (``mode="cached"``):
   ``context_len`` tokens; filtered_logit's time-axis LSE runs over the
   window's cached logits rows. oracle/transformer.py CachedTransformer
   restates these semantics; tests/test_decode_cached_gpu.py pins the build to it.
+
+Sharded decode (``group=``): the global batch of world x B
+prompts is split by rows over the ranks of a process group, one model
+replica per GPU. The only exchange is the host-side k choice: the reference
+draws ``random.choice`` for every row in row order each step, so every rank
+all-gathers the world x B last tokens (one small collective per step) and
+replays that whole sequence, then keeps its own rows' k's; the per-row
+uniforms are drawn for all world x B rows from the same seed and sliced the
+same way. Rank r's rows are then bit for bit rows r*B .. r*B+B-1 of a single
+process run over the concatenated batch with the same seeds
+(tests/test_decode_shard_gpu.py).
 """
 import random as _random
 
 import torch
+import torch.distributed as dist
 
 from . import _lib as L
 from ._lib import ptr, call, stream, dt
@@ -56,14 +68,44 @@ def choose_k(last_tokens, start, rng):
     return ks
 
 
+class _Shard:
+    """Row shard of a decode over a process group (module docstring)."""
+
+    def __init__(self, group, B, dev):
+        if not dist.is_initialized():
+            raise RuntimeError("generate(group=...) needs an initialised torch.distributed process group")
+        if group is True:
+            group = None  # the default group
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.gloo = dist.get_backend(group) == "gloo"
+        self.dev = dev
+        sizes = self.gather(torch.tensor([B], dtype=torch.int64, device=dev))
+        if any(n != B for n in sizes):
+            raise ValueError(f"sharded generate needs the same batch on every rank, got {sizes}")
+        self.B = B
+        self.lo, self.hi = self.rank * B, (self.rank + 1) * B
+
+    def gather(self, t):
+        """all-gather of a small int64 device vector -> host list, rank order"""
+        t = t.cpu() if self.gloo else t.contiguous()
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t, group=self.group)
+        return torch.cat(parts).tolist()
+
+
 @torch.no_grad()
 def generate(model, context_len, token_ids, meta_ids, num_tokens=1000, device="cuda", rng=None, uniforms=None,
-             grammar: Grammar = None, return_tensor=False, mode="exact"):
+             grammar: Grammar = None, return_tensor=False, mode="exact", group=None):
     """Returns a list of B token lists of length T0 + num_tokens (like the
     reference). ``rng`` defaults to the global ``random`` module (as in the
     reference); ``uniforms`` is an optional iterator of floats (one per row
     per step, rows in order) for reproducible sampling, else a device
-    torch.Generator is used."""
+    torch.Generator is used. ``group`` (a torch.distributed process group, or
+    True for the default one): this call decodes this rank's B rows of a
+    sharded batch of world x B rows (module docstring); ``rng``, ``uniforms``
+    (world x B per step) and torch's seed must then be the same on every rank."""
     grammar = grammar or Grammar()
     rng = rng or _random
     eng = model.engine
@@ -80,7 +122,9 @@ def generate(model, context_len, token_ids, meta_ids, num_tokens=1000, device="c
     out_tok = torch.empty(B, dtype=torch.int64, device=dev)
     wtab = grammar_table(dev, grammar)
     b = grammar.bounds
-    last_host = token_ids[:, -1].tolist()
+    shard = _Shard(group, B, dev) if group is not None else None
+    nrow = shard.world * B if shard else B  # rows the host-side RNG replays per step
+    last_host = shard.gather(token_ids[:, -1]) if shard else token_ids[:, -1].tolist()
     gen = None
     if mode not in ("exact", "cached"):
         raise ValueError(f"mode must be 'exact' or 'cached', not {mode!r}")
@@ -112,7 +156,7 @@ def generate(model, context_len, token_ids, meta_ids, num_tokens=1000, device="c
                  b[0], b[1], b[2], b[3], B, W, V, W - 1, ptr(col_lse), ptr(ws), stream())
         ks = choose_k(last_host, start, rng)
         if uniforms is not None:
-            u = torch.tensor([next(uniforms) for _ in range(B)], dtype=torch.float32).to(dev)
+            u = torch.tensor([next(uniforms) for _ in range(nrow)], dtype=torch.float32).to(dev)
         else:
             if gen is None:
                 # the reference samples with torch.multinomial, i.e. from torch's
@@ -121,11 +165,14 @@ def generate(model, context_len, token_ids, meta_ids, num_tokens=1000, device="c
                 # exactly the reference's random.choice sequence
                 gen = torch.Generator(device=dev)
                 gen.manual_seed(int(torch.randint(0, 2 ** 62, (1,)).item()))
-            u = torch.rand(B, device=dev, generator=gen)
+            u = torch.rand(nrow, device=dev, generator=gen)
+        if shard:
+            ks, u = ks[shard.lo:shard.hi], u[shard.lo:shard.hi].contiguous()
         kt = torch.tensor(ks, dtype=torch.int32).to(dev)
         call("msq_decode_sample", ptr(hist), ldh, cur, ptr(z), ldz, B, V, ptr(kt), ptr(u), ptr(out_tok),
              start["dyn"], start["length"], start["time"], start["tempo"], stream())
-        last_host = out_tok.tolist()  # the one device->host sync per step (host-side k choice)
+        # the one device->host sync per step (host-side k choice); sharded: all ranks' rows
+        last_host = shard.gather(out_tok) if shard else out_tok.tolist()
         del logits
     seq = hist[:, :T0 + num_tokens]
     return seq if return_tensor else seq.tolist()

@@ -81,7 +81,10 @@ def generate_band(models, band, data_root, metadata, output_path, length, B=BATC
     print(f"Processing band: {band}")
     written, done = [], 0
     while done < B:
-        src, meta = band_prompts(data_root, band, metadata, B, block_len, device, seed)
+        # a fixed seed gives each pass its own loader draw (the reference builds a
+        # fresh randomly shuffled loader per pass)
+        src, meta = band_prompts(data_root, band, metadata, B, block_len, device,
+                                 None if seed is None else seed + done)
         src, meta = src[:B - done], meta[:B - done]
         A = src.shape[0]
         if no_metadata:

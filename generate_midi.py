@@ -18,6 +18,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import _pkgload  # noqa: E402
+import torch  # noqa: E402
 
 _pkgload.load()
 from midiseq.config import BATCH_SIZE, BLOCK_LEN  # noqa: E402
@@ -50,6 +51,10 @@ def main():
     if args.length is None:
         ap.error("--length is required")
     rng = random.Random(args.seed) if args.seed is not None else None
+    if args.seed is not None:
+        # the device sampler draws from torch's generator (as torch.multinomial
+        # does in the reference), so --seed seeds it too
+        torch.manual_seed(args.seed)
     models = {}
     for kind in ("mamba", "transformer"):
         if getattr(args, kind):

@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
 
+    torch.manual_seed(args.seed)  # dropout seeds of the train step come from torch's generator
     rank, local, world = setup_distributed()
     dev = f"cuda:{local}"
     kw = {} if args.model == "mamba" else {"block_len": args.block_len}
