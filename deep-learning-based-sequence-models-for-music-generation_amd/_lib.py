@@ -13,6 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmidiseq.so")
 
 F32, BF16 = 0, 1
+ROUTE_DEFAULT, ROUTE_TILE256, ROUTE_TILE128 = range(3)  # msq_gemm_set_route
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_RESID, EPI_RELU_MASK, EPI_ACCUM, EPI_BIAS_DROP_RESID = range(7)
 
 _p, _i, _i64, _f, _sz, _u32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint32
@@ -64,6 +65,10 @@ SIGNATURES = {
     "msq_gemm_colsum": (_i, [_i, _i, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _i64, _i, _p, _i, _i64, _p, _i, _p,
                              _i64, _p]),
     "msq_transpose_bf16": (_i, [_p, _i64, _p, _i64, _i64, _i64, _p]),
+    "msq_gemm_set_route": (_i, [_i]),
+    "msq_ring_step": (_i, [_p, _p, _p, _i, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p]),
+    "msq_relattn_decode_pos": (_i, [_i, _p, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _f,
+                                    _p]),
     "msq_ring_lse": (_i, [_p, _p, _p, _i, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p]),
     "msq_filtered_ce_bias": (_i, [_p, _p, _i64, _p, _p, _i, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
                                   _f, _p, _p, _p]),

@@ -72,7 +72,8 @@ __global__ __launch_bounds__(NT) void relattn_decode_kernel(T* __restrict__ out,
                                                             T* __restrict__ kc, T* __restrict__ vc,
                                                             const T* __restrict__ R, int64_t S_max, int H,
                                                             int S_ring, int n_meta, int n_tok, int new_slot,
-                                                            int first_mod, float scale, int hs) {
+                                                            int first_mod, float scale, int hs,
+                                                            const int64_t* __restrict__ posp) {
     __shared__ float q_s[HS];
     __shared__ float p_s[MAXS];
     __shared__ float red[NT / 64];
@@ -81,6 +82,12 @@ __global__ __launch_bounds__(NT) void relattn_decode_kernel(T* __restrict__ out,
     const int l16 = lane & 15, grp = w * 4 + (lane >> 4);  // 16 key groups per block
     const int h = blockIdx.x, b = blockIdx.y;
     const int ctx = S_ring - n_meta;
+    if (posp) {  // the step's position from device memory (graph-replayed steps)
+        const int64_t pos = *posp;
+        n_tok = (int)min<int64_t>(pos + 1, ctx);
+        new_slot = n_meta + (int)(pos % ctx);
+        first_mod = (int)((pos + 1 - n_tok) % ctx);
+    }
     const int S = n_meta + n_tok;
     const T* qrow = qkv + (int64_t)b * ldq + (int64_t)h * hs;
     const T* knew = qrow + (int64_t)H * hs;
@@ -192,11 +199,38 @@ extern "C" int msq_relattn_decode(int dtype, void* out, int64_t ldo, const void*
     if (dtype == MSQ_BF16)
         hipLaunchKernelGGL(relattn_decode_kernel<bf16>, grid, dim3(NT), 0, (hipStream_t)stream, (bf16*)out, ldo,
                            (const bf16*)qkv, ldq, (bf16*)kcache, (bf16*)vcache, (const bf16*)R, S_max, (int)H,
-                           (int)S_ring, (int)n_meta, (int)n_tok, (int)new_slot, (int)first_mod, scale, (int)hs);
+                           (int)S_ring, (int)n_meta, (int)n_tok, (int)new_slot, (int)first_mod, scale, (int)hs, nullptr);
     else
         hipLaunchKernelGGL(relattn_decode_kernel<float>, grid, dim3(NT), 0, (hipStream_t)stream, (float*)out, ldo,
                            (const float*)qkv, ldq, (float*)kcache, (float*)vcache, (const float*)R, S_max, (int)H,
-                           (int)S_ring, (int)n_meta, (int)n_tok, (int)new_slot, (int)first_mod, scale, (int)hs);
+                           (int)S_ring, (int)n_meta, (int)n_tok, (int)new_slot, (int)first_mod, scale, (int)hs, nullptr);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
+// msq_relattn_decode with the step's position read from device memory: n_tok =
+// min(pos + 1, ctx), new slot n_meta + pos % ctx, first_mod = (pos + 1 - n_tok)
+// % ctx (pos >= 0 is the caller's contract), so that a captured graph of the
+// decode step replays unchanged from step to step.
+extern "C" int msq_relattn_decode_pos(int dtype, void* out, int64_t ldo, const void* qkv, int64_t ldq, void* kcache,
+                                      void* vcache, const void* R, int64_t S_max, int64_t B, int64_t H, int64_t hs,
+                                      int64_t S_ring, int64_t n_meta, const int64_t* pos, float scale, void* stream) {
+    MSQ_CHECK_ARG(out && qkv && kcache && vcache && R && pos, "msq_relattn_decode_pos: null pointer");
+    MSQ_CHECK_ARG(hs > 0 && hs <= HS && hs % 8 == 0, "msq_relattn_decode_pos: head size %lld (8 | hs <= 128)",
+                  (long long)hs);
+    MSQ_CHECK_ARG(B > 0 && H > 0 && n_meta >= 0 && S_ring > n_meta && S_ring <= MAXS && S_ring <= S_max,
+                  "msq_relattn_decode_pos: bad sizes");
+    MSQ_CHECK_ARG(ldq >= 3 * H * hs && ldo >= H * hs, "msq_relattn_decode_pos: bad leading dims");
+    MSQ_CHECK_ARG(dtype == MSQ_BF16 || dtype == MSQ_F32, "msq_relattn_decode_pos: dtype %d", dtype);
+    const dim3 grid((unsigned)H, (unsigned)B);
+    if (dtype == MSQ_BF16)
+        hipLaunchKernelGGL(relattn_decode_kernel<bf16>, grid, dim3(NT), 0, (hipStream_t)stream, (bf16*)out, ldo,
+                           (const bf16*)qkv, ldq, (bf16*)kcache, (bf16*)vcache, (const bf16*)R, S_max, (int)H,
+                           (int)S_ring, (int)n_meta, 1, (int)n_meta, 0, scale, (int)hs, pos);
+    else
+        hipLaunchKernelGGL(relattn_decode_kernel<float>, grid, dim3(NT), 0, (hipStream_t)stream, (float*)out, ldo,
+                           (const float*)qkv, ldq, (float*)kcache, (float*)vcache, (const float*)R, S_max, (int)H,
+                           (int)S_ring, (int)n_meta, 1, (int)n_meta, 0, scale, (int)hs, pos);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }

@@ -15,6 +15,7 @@ struct GemmArgs {
     int ksplit;  // >1: K range split over blocks, ACCUM epilogue via fp32 atomics
     int64_t kper;
     uint32_t a_ext, b_ext;  // bytes of one batch's A / B extent (256-tile buffer descriptors)
+    uint32_t c_ext, x_ext;  // bytes of the C / aux extents (persistent 256 tile's buffer stores / loads)
     // triangular K ranges of the relative-attention products (128 tile only):
     // 1 = rows m are (segment, i = m % seg) and need k >= seg-1-i (dq = dQR.R);
     // 2 = K is nseg segments of seg rows, tile rows m = r need k%seg >= seg-1-r (dR)
@@ -32,12 +33,6 @@ struct GemmArgs {
     // partials [tiles_m * 2][N], reduced in a fixed order afterwards
     float* cs_ws;
 };
-
-// hipBLASLt route of msq_gemm_ex (blaslt.cpp): 1 done, 0 not handled, -1 error
-// (epilogue NONE / BIAS / BIAS_RELU, or ACCUM = fp32 C += result; strided batches)
-int blaslt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
-                int64_t ldb, void* C, int c_dtype, int64_t ldc, int epilogue, const float* bias, hipStream_t s,
-                int64_t batch = 1, int64_t sA = 0, int64_t sB = 0, int64_t sC = 0);
 
 // bytes of the split-K partial workspace an ACCUM product with this split needs
 inline size_t splitk_ws_bytes(int64_t M, int64_t N, int64_t batch, int ksplit) {
@@ -123,6 +118,9 @@ __device__ __forceinline__ f32x4 epi_apply(const GemmArgs& g, TC* C, const TX* X
 // preconditions (the caller then uses the 128x128 kernel).
 bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, size_t ws_bytes,
                     hipStream_t s);
+// persistent 256 tile (forward / dX products: no ACCUM, one batch, N % 8 == 0,
+// 16-B aligned C / aux / bias); false when it does not apply
+bool gemm256p_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s);
 // skinny-M weight-streaming kernel of the decode steps (gemm_skinny.hip):
 // false when the problem is not M <= 64 / ta = tb = 0 / a forward epilogue
 bool gemm_skinny_launch(const GemmArgs& g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s);

@@ -19,8 +19,21 @@ extern "C" size_t msq_colsum_workspace(int64_t rows, int64_t cols);
 extern "C" int msq_colsum(float* out, int accumulate, const void* x, int dtype, int64_t rows, int64_t cols,
                           int64_t ld, void* workspace, void* stream);
 #include <stdlib.h>
+#include <atomic>
 
 namespace {
+// msq_gemm_set_route; -1 = not read from the environment yet
+std::atomic<int> g_route{-1};
+int gemm_route() {
+    int r = g_route.load(std::memory_order_relaxed);
+    if (r < 0) {
+        r = getenv("MSQ_GEMM128") ? MSQ_ROUTE_TILE128 : getenv("MSQ_GEMM_NOP") ? MSQ_ROUTE_TILE256 : MSQ_ROUTE_DEFAULT;
+        int expect = -1;
+        g_route.compare_exchange_strong(expect, r);
+        r = g_route.load(std::memory_order_relaxed);
+    }
+    return r;
+}
 
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 
@@ -517,6 +530,13 @@ void plan128_ksplit(GemmArgs& g, int dtype, int epilogue) {
 }
 }  // namespace
 
+extern "C" int msq_gemm_set_route(int route) {
+    if (route < MSQ_ROUTE_DEFAULT || route > MSQ_ROUTE_TILE128) return msq_set_error(MSQ_ERR_ARG, "msq_gemm_set_route: bad route %d", route);
+    const int prev = gemm_route();
+    g_route.store(route, std::memory_order_relaxed);
+    return prev;
+}
+
 extern "C" int64_t msq_gemm_workspace_size(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K,
                                            int64_t lda, int64_t ldb, int64_t batch, int epilogue) {
     if (dtype != MSQ_BF16 || M <= 0 || N <= 0 || K <= 0 || batch <= 0) return 0;
@@ -527,7 +547,7 @@ extern "C" int64_t msq_gemm_workspace_size(int dtype, int ta, int tb, int64_t M,
     }
     GemmArgs g{};
     g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.batch = (int)batch;
-    if (!getenv("MSQ_GEMM128") && gemm256_plan(g, ta, tb, epilogue))
+    if (gemm_route() != MSQ_ROUTE_TILE128 && gemm256_plan(g, ta, tb, epilogue))
         return (int64_t)splitk_ws_bytes(M, N, batch, g.ksplit);
     g.tiles_m = (int)((M + BM - 1) / BM);
     g.tiles_n = (int)((N + BN - 1) / BN);
@@ -597,15 +617,14 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
         MSQ_LAUNCH_CHECK();
         return MSQ_OK;
     }
-    // plain / bias / bias+ReLU forward and dX products: hipBLASLt (blaslt.cpp)
-    static const bool blaslt_dw = getenv("MSQ_BLASLT_DW") != nullptr;  // A/B switch: weight gradients too
-    if (dtype == MSQ_BF16 && batch == 1 && M > 256 && (epilogue != MSQ_EPI_ACCUM || blaslt_dw) &&
-        !getenv("MSQ_GEMM128")) {
-        const int r = blaslt_gemm(ta, tb, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, epilogue, bias, s);
-        if (r < 0) return msq_set_error(MSQ_ERR_HIP, "msq_gemm: hipBLASLt matmul failed");
-        if (r > 0) return MSQ_OK;
-    }
-    if (dtype == MSQ_BF16 && !getenv("MSQ_GEMM128")) {
+    if (dtype == MSQ_BF16 && gemm_route() != MSQ_ROUTE_TILE128) {
+        // the 256 tile: persistent form for the forward / dX products
+        // (gemm256p_kernel), the per-tile launch for the rest (MSQ_ROUTE_TILE256: all)
+        const bool nop = gemm_route() == MSQ_ROUTE_TILE256;
+        auto big = [&](const GemmArgs& a, size_t wsb) {
+            return (!nop && gemm256p_launch(a, ta, tb, epilogue, c_dtype, aux_dtype, s)) ||
+                   gemm256_launch(a, ta, tb, epilogue, c_dtype, aux_dtype, wsb, s);
+        };
         // wave quantisation: M = B*S rows rarely divide by 256 (32 x 2054 =
         // 256.75 tiles), and the partial last row of 256 tiles alone would
         // take one more full round of the 256 tile on a few CUs. Run the
@@ -625,7 +644,7 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
             if (aux) t.aux = (const char*)aux + Mm * ld_aux * xsz;
             t.tiles_m = (int)((t.M + BM - 1) / BM);
             g.M = Mm;
-            if (gemm256_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, 0, s)) {
+            if (big(g, 0)) {
                 const TailPlan tp = plan_tail(t.M, N, K);
                 if (tp.ksplit > 1 && ws && (size_t)ws_bytes >= tp.tmp_bytes + tp.part_bytes) {
                     // split-K tail: sums into tmp, then the epilogue
@@ -653,7 +672,7 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
                 return MSQ_OK;
             }
             g.M = M;
-        } else if (gemm256_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, (size_t)ws_bytes, s)) {
+        } else if (big(g, (size_t)ws_bytes)) {
             MSQ_LAUNCH_CHECK();
             return MSQ_OK;
         }
@@ -697,7 +716,7 @@ extern "C" int msq_gemm_colsum(int ta, int tb, int64_t M, int64_t N, int64_t K, 
                   "msq_gemm_colsum: leading dims / alignment (bf16 needs ld %% 8 == 0, 16-B aligned)");
     MSQ_CHECK_ARG(aux || epilogue == MSQ_EPI_NONE, "msq_gemm_colsum: RELU_MASK needs aux");
     hipStream_t s = (hipStream_t)stream;
-    if (!getenv("MSQ_GEMM128")) {
+    if (gemm_route() != MSQ_ROUTE_TILE128) {
         GemmArgs g{};
         g.M = M; g.N = N; g.K = K;
         g.A = A; g.lda = lda;

@@ -1,0 +1,393 @@
+// Persistent 256x256 GEMM tile for the forward / dX products (see the comment
+// block below and gemm256.hip for the tile itself).
+#include "gemm256_tile.h"
+
+namespace {
+
+using namespace g256;
+
+// ---------------------------------------------------------------------------
+// Persistent form of the same tile for the forward / dX products (K ~ 1024 to
+// 18 k, one workgroup per CU walking the tiles round-robin).
+//
+// At K = 1024 a tile is 16 K-steps, and the non-persistent kernel pays a fixed
+// prologue (every CU loading its first 96 KB at once) and epilogue (every CU
+// storing its 128 KB C tile at once) around each one. Here the next tile's
+// prologue LDS-DMA is issued as soon as the last MFMA phase of the current tile
+// has read its fragments, BEFORE the current tile's epilogue, and the epilogue
+// stores are not waited for: the next tile's first K-step counts them in its
+// vmcnt waits (vm_wait<8 + S>: the S stores were issued after the prologue
+// halves it waits for), so the C write burst drains under the next tile's
+// MFMAs. For the count to be exact every lane issues exactly S stores per tile
+// (buffer stores; rows / columns past M / N get an offset beyond the
+// descriptor's num_records and are dropped), and before the first tile S
+// dropped stores stand in for the previous epilogue.
+//
+// bf16 C: a 16x16 accumulator leaves each lane 4 columns of a row; lanes l and
+// l + 16 hold the two halves of 8 consecutive columns of the neighbouring
+// 16-column block, so one v_permlane16_swap per dword turns 2 x 8-B pieces into
+// one 16-B store (cdna_hip_programming.md T21, in its 16-lane form).
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <typename TC>
+constexpr int p_stores() {
+    return sizeof(TC) == 2 ? 16 : 32;
+}
+
+__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
+    const bf16x2 v = (bf16x2){(bf16)a, (bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+template <typename TX>
+__device__ __forceinline__ f32x4 p_aux_load(__amdgpu_buffer_rsrc_t rx, uint32_t off) {
+    if (sizeof(TX) == 4) {
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+    } else {
+        const bf16x4 h = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(rx, off, 0, 0));
+        return (f32x4){(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+    }
+}
+
+// epilogue of one tile: exactly p_stores<TC>() buffer stores per lane
+template <int EPI, typename TC, typename TX>
+__device__ __forceinline__ void p_epilogue(const GemmArgs& g, __amdgpu_buffer_rsrc_t rc, __amdgpu_buffer_rsrc_t rx,
+                                           __amdgpu_buffer_rsrc_t rbias, int64_t m0, int64_t n0, int wr, int wc,
+                                           int lane, f32x4 (&acc)[2][2][4][2]) {
+    constexpr bool HAS_BIAS = EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID ||
+                              EPI == MSQ_EPI_BIAS_DROP_RESID;
+    const int r = lane & 15, gq = lane >> 4;
+    f32x4 bv[2][2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            bv[b][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (HAS_BIAS && g.bias) {
+                const int64_t n = n0 + b * 128 + wc * 32 + j * 16 + 4 * gq;
+                bv[b][j] = __builtin_bit_cast(
+                    f32x4, __builtin_amdgcn_raw_buffer_load_b128(rbias, n < g.N ? (uint32_t)(n * 4) : OOB, 0, 0));
+            }
+        }
+    // aux rows in groups of 2 of the lane's 8 rows (4 x 16-B loads in flight
+    // per row; a whole half-tile's 64 VGPRs of aux would spill beside acc)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int ih = 0; ih < 2; ++ih) {
+        f32x4 xp[4][2][2];
+        if (epi_reads_aux<EPI>()) {
+#pragma unroll
+            for (int i = 2 * ih; i < 2 * ih + 2; ++i)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int64_t m = m0 + a * 128 + wr * 64 + i * 16 + r;
+                        const int64_t n = n0 + b * 128 + wc * 32 + j * 16 + 4 * gq;
+                        const uint32_t off =
+                            (m < g.M && n < g.N) ? (uint32_t)((m * g.ldx + n) * (int64_t)sizeof(TX)) : OOB;
+                        xp[i][b][j] = p_aux_load<TX>(rx, off);
+                    }
+        }
+#pragma unroll
+        for (int i = 2 * ih; i < 2 * ih + 2; ++i) {
+            const int64_t m = m0 + a * 128 + wr * 64 + i * 16 + r;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                f32x4 v[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int64_t n = n0 + b * 128 + wc * 32 + j * 16 + 4 * gq;
+                    f32x4 t = acc[a][b][i][j];
+                    if (HAS_BIAS) t += bv[b][j];
+                    if (EPI == MSQ_EPI_BIAS_DROP_RESID) t = epi_drop(g, m, n, t) + xp[i][b][j];
+                    if (EPI == MSQ_EPI_BIAS_RELU) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) t[e] = fmaxf(t[e], 0.f);
+                    }
+                    if (EPI == MSQ_EPI_BIAS_RESID) t += xp[i][b][j];
+                    if (EPI == MSQ_EPI_RELU_MASK) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) t[e] = xp[i][b][j][e] > 0.f ? t[e] : 0.f;
+                    }
+                    v[j] = t;
+                }
+                if (sizeof(TC) == 2) {
+                    uint32_t p0x = pack_bf16(v[0][0], v[0][1]), p0y = pack_bf16(v[0][2], v[0][3]);
+                    uint32_t p1x = pack_bf16(v[1][0], v[1][1]), p1y = pack_bf16(v[1][2], v[1][3]);
+                    // rows (lane >> 4) 1, 3 of the block-0 pieces <-> rows 0, 2 of the block-1 pieces
+                    const auto sx = __builtin_amdgcn_permlane16_swap(p0x, p1x, false, false);
+                    const auto sy = __builtin_amdgcn_permlane16_swap(p0y, p1y, false, false);
+                    const int64_t n = n0 + b * 128 + wc * 32 + (gq & 1) * 16 + (gq >> 1) * 8;
+                    const uint32_t off = (m < g.M && n < g.N) ? (uint32_t)((m * g.ldc + n) * 2) : OOB;
+                    const u32x4 d = (u32x4){(uint32_t)sx[0], (uint32_t)sy[0], (uint32_t)sx[1], (uint32_t)sy[1]};
+                    __builtin_amdgcn_raw_buffer_store_b128(d, rc, off, 0, 0);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int64_t n = n0 + b * 128 + wc * 32 + j * 16 + 4 * gq;
+                        const uint32_t off = (m < g.M && n < g.N) ? (uint32_t)((m * g.ldc + n) * 4) : OOB;
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[j]), rc, off, 0, 0);
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <int TA, int TB, int EPI, typename TC, typename TX>
+__global__ __launch_bounds__(NT, 1) void gemm256p_kernel(GemmArgs g) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    lds_t* smem = (lds_t*)smem_raw;
+    constexpr int S = p_stores<TC>();
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 2, wc = w & 3;
+    const int ntiles = g.tiles_m * g.tiles_n;
+    const int G = gridDim.x;
+    // tile id of round q for this workgroup: q * G + widx; blocks sharing an
+    // XCD take consecutive ids (T1), which the grouped order below turns into
+    // shared A / B panels in that XCD's L2
+    const int widx = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, G));
+    auto tile_mn = [&](int id, int64_t& m0, int64_t& n0) {
+        const int GROUP = 8;
+        const int per_group = GROUP * g.tiles_n;
+        const int grp = id / per_group, first_m = grp * GROUP;
+        const int gsz = min(g.tiles_m - first_m, GROUP);
+        m0 = (int64_t)(first_m + (id % per_group) % gsz) * 256;
+        n0 = (int64_t)((id % per_group) / gsz) * 256;
+    };
+
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc((const char*)g.A, g.a_ext);
+    const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)g.B, g.b_ext);
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc((const char*)g.C, g.c_ext);
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc((const char*)(g.aux ? g.aux : g.C), g.aux ? g.x_ext : 0u);
+    const __amdgpu_buffer_rsrc_t rbias =
+        make_rsrc((const char*)(g.bias ? (const void*)g.bias : g.C), g.bias ? (uint32_t)(g.N * 4) : 0u);
+
+    int loA[4], loB[4];
+    {
+        const int r = lane & 15, gq = lane >> 4;
+        if (TA == 0) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) loA[ks] = r * 128 + ((ks * 4 + gq) ^ ((r >> 1) & 7)) * 16;
+            loA[2] = loA[3] = 0;
+        } else {
+            const int q = r >> 2, p = r & 3, k = 8 * gq + q;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                loA[i] = k * 256 + ((((wr * 64 + i * 16) >> 3) ^ gmn(k)) | (p >> 1)) * 16 + (p & 1) * 8;
+        }
+        if (TB == 0) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) loB[ks] = r * 128 + ((ks * 4 + gq) ^ ((r >> 1) & 7)) * 16;
+            loB[2] = loB[3] = 0;
+        } else {
+            const int q = r >> 2, p = r & 3, k = 8 * gq + q;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                loB[i] = k * 256 + ((((wc * 32 + i * 16) >> 3) ^ gmn(k)) | (p >> 1)) * 16 + (p & 1) * 8;
+            loB[2] = loB[3] = 0;
+        }
+    }
+
+    const int nk = (int)((g.K + 63) / 64);
+    Stage<TA == 0> sa;
+    Stage<TB == 0> sb;
+    auto slot = [&](int b, int s) { return smem + (b * 4 + s) * HALF; };
+    auto issue = [&](int u, int h) {
+        const int64_t k0 = (int64_t)u * 64;
+        lds_t* dst = slot(u & 1, h);
+        if (h == 0) sa.issue(ra, dst, 0, k0, g.K - k0, w);
+        else if (h == 1) sb.issue(rb, dst, 0, k0, g.K - k0, w);
+        else if (h == 2) sa.issue(ra, dst, 1, k0, g.K - k0, w);
+        else sb.issue(rb, dst, 1, k0, g.K - k0, w);
+    };
+    auto prologue = [&](int64_t m0, int64_t n0) {
+        sa.init(m0, g.M, g.lda, w, lane);
+        sb.init(n0, g.N, g.ldb, w, lane);
+        issue(0, 0);
+        issue(0, 1);
+        issue(0, 2);
+        issue(0, 3);
+        if (nk > 1) {
+            issue(1, 0);
+            issue(1, 1);
+        }
+    };
+
+    int id = widx;
+    if (id >= ntiles) return;
+    int64_t m0, n0;
+    tile_mn(id, m0, n0);
+    prologue(m0, n0);
+    order_fence();
+    // the S stores a previous tile's epilogue would have left outstanding (to
+    // distinct, non-adjacent dropped offsets: identical ones would be merged
+    // into one store by dead-store elimination, adjacent ones widened)
+#pragma unroll
+    for (int e = 0; e < S; ++e)
+        __builtin_amdgcn_raw_buffer_store_b32(0u, rc, OOB + 64u * e, 0, 0);
+    order_fence();
+
+    f32x4 acc[2][2][4][2];
+    bf16x8 af[2][2][4];
+    bf16x8 bfr[2][2][2];
+
+    // one phase (gemm256_kernel's MSQ_PHASE) with the wait count of its K-step
+#define MSQ_PPHASE(Q, BUF, WAITN)                                                                       \
+    {                                                                                                   \
+        constexpr int mi = (Q == 1 || Q == 2) ? 1 : 0;                                                  \
+        constexpr int ni = (Q >= 2) ? 1 : 0;                                                            \
+        if (Q == 0) {                                                                                   \
+            read_set<TA == 0, 4>(af[0], slot(BUF, 0), wr * 64, loA);                                    \
+            read_set<TB == 0, 2>(bfr[0], slot(BUF, 1), wc * 32, loB);                                   \
+        } else if (Q == 1) {                                                                            \
+            read_set<TA == 0, 4>(af[1], slot(BUF, 2), wr * 64, loA);                                    \
+        } else if (Q == 2) {                                                                            \
+            read_set<TB == 0, 2>(bfr[1], slot(BUF, 3), wc * 32, loB);                                   \
+        }                                                                                               \
+        const int su = (Q < 2) ? t + 1 : t + 2;                                                         \
+        if (su < nk) {                                                                                  \
+            issue(su, (Q + 2) & 3);                                                                     \
+            vm_wait<WAITN>();                                                                           \
+        } else {                                                                                        \
+            vm_wait0();                                                                                 \
+        }                                                                                               \
+        barrier();                                                                                      \
+        __builtin_amdgcn_s_setprio(1);                                                                  \
+        _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                                \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i)                                               \
+                _Pragma("unroll") for (int j = 0; j < 2; ++j)                                           \
+                    acc[mi][ni][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ni][ks][j], af[mi][ks][i], \
+                                                                                acc[mi][ni][i][j], 0, 0, 0); \
+        __builtin_amdgcn_s_setprio(0);                                                                  \
+        barrier();                                                                                      \
+    }
+
+    for (;;) {
+        // A0 / B0 of K-step 0 landed: younger are 4 half-tiles (8 DMA) and the S stores
+        if (nk > 1) vm_wait<8 + S>();
+        else vm_wait0();
+        barrier();
+        if (wr == 1) barrier();
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        {
+            int t = 0;  // K-step 0: the stores sit between its prologue halves and its own DMA
+            MSQ_PPHASE(0, 0, 8 + S)
+            MSQ_PPHASE(1, 0, 8 + S)
+            MSQ_PPHASE(2, 0, 8 + S)
+            MSQ_PPHASE(3, 0, 8 + S)
+        }
+        for (int t = 1; t < nk; t += 2) {
+            MSQ_PPHASE(0, 1, 8)
+            MSQ_PPHASE(1, 1, 8)
+            MSQ_PPHASE(2, 1, 8)
+            MSQ_PPHASE(3, 1, 8)
+            if (t + 1 < nk) {
+                ++t;
+                MSQ_PPHASE(0, 0, 8)
+                MSQ_PPHASE(1, 0, 8)
+                MSQ_PPHASE(2, 0, 8)
+                MSQ_PPHASE(3, 0, 8)
+                --t;
+            }
+        }
+        if (wr == 0) barrier();
+        // every wave has read its last fragments: the next tile's prologue may
+        // overwrite the LDS slots while this tile's epilogue runs
+        const int nid = id + G;
+        const bool more = nid < ntiles;
+        int64_t m1 = 0, n1 = 0;
+        if (more) {
+            tile_mn(nid, m1, n1);
+            prologue(m1, n1);
+        }
+        order_fence();
+        p_epilogue<EPI, TC, TX>(g, rc, rx, rbias, m0, n0, wr, wc, lane, acc);
+        order_fence();
+        if (!more) break;
+        id = nid;
+        m0 = m1;
+        n0 = n1;
+    }
+#undef MSQ_PPHASE
+}
+
+}  // namespace
+
+namespace {
+int num_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    }
+    return n;
+}
+
+template <int TA, int TB, int EPI, typename TC, typename TX>
+void launch_p(const GemmArgs& g, hipStream_t s) {
+    static bool attr = false;
+    auto k = gemm256p_kernel<TA, TB, EPI, TC, TX>;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * HALF);
+        attr = true;
+    }
+    const int ntiles = g.tiles_m * g.tiles_n;
+    hipLaunchKernelGGL(k, dim3(std::min(ntiles, num_cus())), dim3(NT), 8 * HALF, s, g);
+}
+
+template <int EPI, typename TC, typename TX>
+void dispatch_p_t(const GemmArgs& g, int ta, int tb, hipStream_t s) {
+    if (ta == 0 && tb == 0) launch_p<0, 0, EPI, TC, TX>(g, s);
+    else if (ta == 0 && tb == 1) launch_p<0, 1, EPI, TC, TX>(g, s);
+    else if (ta == 1 && tb == 1) launch_p<1, 1, EPI, TC, TX>(g, s);
+    else launch_p<1, 0, EPI, TC, TX>(g, s);
+}
+
+template <typename TC>
+void dispatch_p(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hipStream_t s) {
+    switch (epi) {
+        case MSQ_EPI_NONE: dispatch_p_t<MSQ_EPI_NONE, TC, float>(g, ta, tb, s); break;
+        case MSQ_EPI_BIAS: dispatch_p_t<MSQ_EPI_BIAS, TC, float>(g, ta, tb, s); break;
+        case MSQ_EPI_BIAS_RELU: dispatch_p_t<MSQ_EPI_BIAS_RELU, TC, float>(g, ta, tb, s); break;
+        case MSQ_EPI_BIAS_RESID: dispatch_p_t<MSQ_EPI_BIAS_RESID, TC, float>(g, ta, tb, s); break;
+        case MSQ_EPI_BIAS_DROP_RESID: dispatch_p_t<MSQ_EPI_BIAS_DROP_RESID, TC, float>(g, ta, tb, s); break;
+        case MSQ_EPI_RELU_MASK:
+            if (aux_dtype == MSQ_BF16) dispatch_p_t<MSQ_EPI_RELU_MASK, TC, bf16>(g, ta, tb, s);
+            else dispatch_p_t<MSQ_EPI_RELU_MASK, TC, float>(g, ta, tb, s);
+            break;
+    }
+}
+}  // namespace
+
+bool gemm256p_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s) {
+    if (epi == MSQ_EPI_ACCUM || g.batch != 1) return false;
+    const int esz = c_dtype == MSQ_BF16 ? 2 : 4, xsz = aux_dtype == MSQ_BF16 ? 2 : 4;
+    // 16-B C pieces (bf16: 8 columns, fp32: 4), 16-B aligned rows
+    if (g.N % 8 || g.ldc % 8 || ((uintptr_t)g.C % 16)) return false;
+    if (g.bias && ((uintptr_t)g.bias % 16)) return false;
+    if (g.aux && (g.ldx % 4 || ((uintptr_t)g.aux % 16))) return false;
+    const int64_t cext = ((g.M - 1) * g.ldc + g.N) * esz;
+    const int64_t xext = g.aux ? ((g.M - 1) * g.ldx + g.N) * xsz : 0;
+    if (cext >= (int64_t)OOB || xext >= (int64_t)OOB || g.N * 4 >= (int64_t)OOB) return false;
+    if (!gemm256_plan(g, ta, tb, epi) || g.ksplit != 1) return false;
+    g.c_ext = (uint32_t)cext;
+    g.x_ext = (uint32_t)xext;
+    if (c_dtype == MSQ_BF16) dispatch_p<bf16>(g, ta, tb, epi, aux_dtype, s);
+    else dispatch_p<float>(g, ta, tb, epi, aux_dtype, s);
+    return true;
+}
+

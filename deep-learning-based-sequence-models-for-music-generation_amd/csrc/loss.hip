@@ -765,15 +765,14 @@ void colstats_launch(const LossArgs& a, float* col_lse, float* part, hipStream_t
 // ---- cached decode (TransformerEngine.step): time-axis LSE over a ring of
 // logits rows [B][ctx][ld], kept as per-block partials lse_blk[b][blk][v] over
 // RB-row blocks, so a step re-reads one or two blocks instead of the window.
+// partial LSE of ring rows [blk*rb, blk*rb + rb) except row `skip` for this
+// thread's N columns v..v+N-1 of row set b
 template <typename T>
-__global__ __launch_bounds__(NT) void ring_block_lse_kernel(const T* __restrict__ ring, int64_t ld, int64_t ctx,
-                                                            int64_t V, int64_t rb, int64_t blk0, int64_t skip,
-                                                            float* __restrict__ part, int64_t nblk) {
+__device__ __forceinline__ void ring_block_lse(const T* __restrict__ ring, int64_t ld, int64_t ctx, int64_t V,
+                                               int64_t rb, int64_t b, int64_t blk, int64_t skip, int64_t v,
+                                               float* __restrict__ part, int64_t nblk) {
     constexpr int N = VecOf<T>::N;
     constexpr float L2E = 1.4426950408889634f;
-    const int64_t v = ((int64_t)blockIdx.x * NT + threadIdx.x) * N;
-    const int64_t b = blockIdx.y, blk = blk0 + blockIdx.z;
-    if (v >= V) return;
     const int64_t t0 = blk * rb, t1 = min(ctx, t0 + rb);
     float m[N], sm[N];
 #pragma unroll
@@ -797,9 +796,48 @@ __global__ __launch_bounds__(NT) void ring_block_lse_kernel(const T* __restrict_
         if (v + i < V) pp[v + i] = m[i] == -INFINITY ? -INFINITY : m[i] + logf(sm[i]);
 }
 
+template <typename T>
+__global__ __launch_bounds__(NT) void ring_block_lse_kernel(const T* __restrict__ ring, int64_t ld, int64_t ctx,
+                                                            int64_t V, int64_t rb, int64_t blk0, int64_t skip,
+                                                            float* __restrict__ part, int64_t nblk) {
+    const int64_t v = ((int64_t)blockIdx.x * NT + threadIdx.x) * VecOf<T>::N;
+    if (v >= V) return;
+    ring_block_lse<T>(ring, ld, ctx, V, rb, blockIdx.y, blk0 + blockIdx.z, skip, v, part, nblk);
+}
+
+// graph-replayed decode step (msq_ring_step): the position comes from *pos.
+// z = 0: the new row's block without the new row; z = 1: the previous row's
+// block when it is another one (that row joined the ring last step)
+template <typename T>
+__global__ __launch_bounds__(NT) void ring_step_lse_kernel(const T* __restrict__ ring, int64_t ld, int64_t ctx,
+                                                           int64_t V, int64_t rb, const int64_t* __restrict__ posp,
+                                                           float* __restrict__ part, int64_t nblk) {
+    const int64_t v = ((int64_t)blockIdx.x * NT + threadIdx.x) * VecOf<T>::N;
+    const int64_t pos = *posp, slot = pos % ctx, blk = slot / rb;
+    const int64_t prev = ((pos - 1 + ctx) % ctx) / rb;
+    if (v >= V || (blockIdx.z == 1 && (prev == blk || pos == 0))) return;
+    if (blockIdx.z == 0) ring_block_lse<T>(ring, ld, ctx, V, rb, blockIdx.y, blk, slot, v, part, nblk);
+    else ring_block_lse<T>(ring, ld, ctx, V, rb, blockIdx.y, prev, -1, v, part, nblk);
+}
+
+// the new logits row into its ring slot and its token into the token ring
+template <typename T>
+__global__ __launch_bounds__(NT) void ring_put_kernel(T* __restrict__ ring, int64_t ld, int64_t ctx,
+                                                      const T* __restrict__ row, int64_t ldrow,
+                                                      int64_t* __restrict__ tokens, const int64_t* __restrict__ tok,
+                                                      const int64_t* __restrict__ posp) {
+    constexpr int N = VecOf<T>::N;
+    const int64_t b = blockIdx.y, v = ((int64_t)blockIdx.x * NT + threadIdx.x) * N;
+    const int64_t slot = *posp % ctx;
+    if (v + N <= ld) *(u32x4*)(ring + (b * ctx + slot) * ld + v) = *(const u32x4*)(row + b * ldrow + v);
+    if (blockIdx.x == 0 && threadIdx.x == 0) tokens[b * ctx + slot] = tok[b];
+}
+
 __global__ void ring_lse_merge_kernel(const float* __restrict__ part, int64_t B, int64_t nblk, int64_t V,
-                                      float* __restrict__ col_lse) {
+                                      float* __restrict__ col_lse, int64_t* __restrict__ pos_inc) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // the step's last reader of *pos ran before this launch: advance it
+    if (pos_inc && e == 0) *pos_inc += 1;
     if (e >= B * V) return;
     const int64_t b = e / V, v = e % V;
     const float* p = part + b * nblk * V + v;
@@ -990,7 +1028,38 @@ extern "C" int msq_ring_lse(float* col_lse, float* part, const void* ring, int d
     blocks(blk_lo, blk_hi - blk_lo, skip_row);
     if (blk_extra >= 0 && (blk_extra < blk_lo || blk_extra >= blk_hi)) blocks(blk_extra, 1, -1);
     hipLaunchKernelGGL(ring_lse_merge_kernel, dim3((unsigned)((B * V + 255) / 256)), dim3(256), 0, s, part, B, nblk, V,
-                       col_lse);
+                       col_lse, nullptr);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
+extern "C" int msq_ring_step(float* col_lse, float* part, void* ring, int dtype, int64_t ld, int64_t B, int64_t ctx,
+                             int64_t V, int64_t rows_per_block, const void* row, int64_t ld_row, int64_t* tokens,
+                             const int64_t* tok, int64_t* pos, void* stream) {
+    const int64_t nblk = rows_per_block > 0 ? (ctx + rows_per_block - 1) / rows_per_block : 0;
+    MSQ_CHECK_ARG(col_lse && part && ring && row && tokens && tok && pos, "msq_ring_step: null pointer");
+    MSQ_CHECK_ARG(B > 0 && ctx > 0 && V > 0 && ld >= V && ld % 8 == 0 && ld_row >= ld && ld_row % 8 == 0 &&
+                      rows_per_block > 0 && ((uintptr_t)ring % 16) == 0 && ((uintptr_t)row % 16) == 0,
+                  "msq_ring_step: bad sizes (ld %% 8 == 0, 16-B aligned ring / row)");
+    MSQ_CHECK_ARG(dtype == MSQ_BF16 || dtype == MSQ_F32, "msq_ring_step: dtype %d", dtype);
+    hipStream_t s = (hipStream_t)stream;
+    const bool bfl = dtype == MSQ_BF16;
+    const int N = bfl ? 8 : 4;
+    const dim3 gp((unsigned)((ld + NT * N - 1) / (NT * N)), (unsigned)B);
+    const dim3 gl((unsigned)((V + NT * N - 1) / (NT * N)), (unsigned)B, 2u);
+    if (bfl) {
+        hipLaunchKernelGGL(ring_put_kernel<bf16>, gp, dim3(NT), 0, s, (bf16*)ring, ld, ctx, (const bf16*)row, ld_row,
+                           tokens, tok, pos);
+        hipLaunchKernelGGL(ring_step_lse_kernel<bf16>, gl, dim3(NT), 0, s, (const bf16*)ring, ld, ctx, V,
+                           rows_per_block, pos, part, nblk);
+    } else {
+        hipLaunchKernelGGL(ring_put_kernel<float>, gp, dim3(NT), 0, s, (float*)ring, ld, ctx, (const float*)row,
+                           ld_row, tokens, tok, pos);
+        hipLaunchKernelGGL(ring_step_lse_kernel<float>, gl, dim3(NT), 0, s, (const float*)ring, ld, ctx, V,
+                           rows_per_block, pos, part, nblk);
+    }
+    hipLaunchKernelGGL(ring_lse_merge_kernel, dim3((unsigned)((B * V + 255) / 256)), dim3(256), 0, s, part, B, nblk, V,
+                       col_lse, pos);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }

@@ -18,7 +18,7 @@ from . import _lib as L
 from . import ops
 from ._lib import ptr, call, stream
 from .config import N_META, VOCAB_SIZE, METADATA_VOCAB_SIZE
-from .transformer import TransformerEngine, _align, _select
+from .transformer import TransformerEngine, _align, _select, dx_gemm
 
 D_STATE, D_CONV, HEADDIM = 64, 4, 64
 
@@ -190,6 +190,10 @@ class MambaEngine:
 
     refresh_shadow = TransformerEngine.refresh_shadow
     mark_shadow_fresh = TransformerEngine.mark_shadow_fresh
+    transposed_weights = TransformerEngine.transposed_weights
+
+    def _t_names(self):
+        return [f"{l}.{n}" for l in range(self.cfg.n_layers) for n in ("in_w", "out_w")] + ["lm_w"]
 
     def acts(self, B, T, save=True):
         key = (B, T, save)
@@ -329,7 +333,8 @@ class MambaEngine:
         ops.gemm(dlogits, A.f, ta=True, tb=True, out=G["lm_w"], epilogue=L.EPI_ACCUM)  # pad columns are 0
         if not head_bias_done:
             ops.colsum(dl, G["lm_b"][:V], accumulate=True)
-        ops.gemm(dlogits, W["lm_w"], tb=True, out=Bw["df"])
+        Wt = self.transposed_weights()
+        dx_gemm(dlogits, W, Wt, "lm_w", Bw["df"])
         gx, gxb = Bw["gx"], Bw["gxb"]
         gx.zero_()
         ops.layernorm_bwd(gx, Bw["df"], A.xlast, A.stf[0], A.stf[1], P["lnf_w"], G["lnf_w"], G["lnf_b"],
@@ -345,7 +350,7 @@ class MambaEngine:
             else:
                 gin = gx
             ops.gemm(gin, A.yn[l], ta=True, tb=True, out=G[f"{l}.out_w"], epilogue=L.EPI_ACCUM)
-            ops.gemm(gin, W[f"{l}.out_w"], tb=True, out=Bw["dyn"])
+            dx_gemm(gin, W, Wt, f"{l}.out_w", Bw["dyn"])
             call("msq_mamba_gnorm_bwd", ptr(Bw["dy"]), ptr(Bw["dzx"]), ptr(A.y[l]), di, ptr(A.zx[l]), cfg.d_in_proj,
                  dtc, ptr(P[f"{l}.norm_w"]), ptr(A.rstd[l]), ptr(Bw["dyn"]), di, ptr(G[f"{l}.norm_w"]), M, di, s)
             call("msq_mamba_ssd_bwd", ptr(Bw["dxc"]), cfg.conv_dim, ptr(Bw["dzx"]), ptr(Bw["dy"]), di,
@@ -356,7 +361,7 @@ class MambaEngine:
                  ptr(P[f"{l}.conv_w"]), ptr(P[f"{l}.conv_b"]), ptr(G[f"{l}.conv_w"]), ptr(G[f"{l}.conv_b"]), Bb, Ll,
                  di, H, s)
             ops.gemm(Bw["dzx"], A.xa[l], ta=True, tb=True, out=G[f"{l}.in_w"], epilogue=L.EPI_ACCUM)
-            ops.gemm(Bw["dzx"], W[f"{l}.in_w"], tb=True, out=gx)
+            dx_gemm(Bw["dzx"], W, Wt, f"{l}.in_w", gx)
             if hook is not None:
                 hook(l)
         ops.embed_bwd(G["tok_emb"], G["meta_emb"], gx, idx, meta)

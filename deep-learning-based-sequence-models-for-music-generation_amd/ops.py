@@ -54,6 +54,23 @@ def gemm(A, B, *, ta=False, tb=False, out=None, out_dtype=None, epilogue=L.EPI_N
     return out
 
 
+class gemm_route:
+    """with ops.gemm_route(L.ROUTE_TILE256): ... runs the large bf16 products
+    on that kernel family (msq_gemm_set_route; tests and A/B tools)."""
+
+    def __init__(self, route):
+        self.route = route
+
+    def __enter__(self):
+        self.prev = L.lib().msq_gemm_set_route(self.route)
+        if self.prev < 0:
+            raise RuntimeError(L.lib().msq_last_error().decode())
+        return self
+
+    def __exit__(self, *exc):
+        L.lib().msq_gemm_set_route(self.prev)
+
+
 def gemm_colsum(A, B, out, dbias, *, ta=False, tb=False, epilogue=L.EPI_NONE, aux=None, accumulate=False):
     """out = epi(op(A) . op(B)) (bf16, epilogue NONE / RELU_MASK) and
     dbias (+)= its column sums (fp32, fused into the GEMM epilogue)."""

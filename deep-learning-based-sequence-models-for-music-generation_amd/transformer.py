@@ -14,6 +14,7 @@ Layout in HBM (one allocation per kind, everything resident):
 Names in state_dict() are exactly the reference's (406 keys incl. the 64
 ``tril`` buffers, which are emitted as views of ONE shared mask)."""
 import math
+import os
 from collections import OrderedDict
 from dataclasses import dataclass
 
@@ -232,6 +233,21 @@ class TransformerDecodeCache:
         self.part = e(B, self.nblk, cfg.vocab_size, dt=f32)
         self.part_valid = False
         self.length = 0  # tokens absorbed (sequence positions 0 .. length-1)
+        # graph-replayed steps (TransformerEngine.step): the position of the
+        # next step on the device (advanced by msq_ring_step), the logits row of
+        # the step before it goes into the ring, and the captured graph
+        self.pos_dev = torch.zeros(1, device=device, dtype=torch.int64)
+        self.row_buf = e(B, cfg.v_pad)
+        self.graph, self.graph_tok, self.graph_gen = None, None, None
+
+
+def dx_gemm(dy, W, Wt, name, out):
+    """out = dy . W[name] (the input gradient of an nn.Linear): through the
+    transposed copy Wt[name] (tb = 0) when the engine keeps one (bf16), else
+    W itself (tb = 1)."""
+    if Wt is not None:
+        return ops.gemm(dy, Wt[name], out=out)
+    return ops.gemm(dy, W[name], tb=True, out=out)
 
 
 class TransformerEngine:
@@ -273,11 +289,13 @@ class TransformerEngine:
         self._shadow_version = self.flat._version
         self._wgen = getattr(self, "_wgen", 0) + 1
 
-    # the ReLU-mask dX product (the 256 tile with its fused epilogue) reads W2^T:
-    # a transposed bf16 copy (K-contiguous, the tile's tb = 0 path), refreshed
-    # once per change of the bf16 shadow; the plain dX products read W itself
-    # (hipBLASLt takes either layout at the same speed, csrc/blaslt.cpp)
-    _T_NAMES = ("w2",)
+    # the dX products (dX = dY . W of every nn.Linear) read W^T: transposed
+    # bf16 copies (K-contiguous, the 256 tile's tb = 0 operand: its row reads
+    # run ~15-20 % faster than the transposed-quad reads of W itself,
+    # tools/gemm_vs_blas.py), refreshed once per change of the bf16 shadow
+    # (0.1 ms per step for all of them)
+    def _t_names(self):
+        return [f"{l}.{n}" for l in range(self.cfg.n_layer) for n in ("wqkv", "wproj", "w1", "w2")] + ["lm_w"]
 
     def transposed_weights(self):
         if self.shadow is None:
@@ -285,9 +303,9 @@ class TransformerEngine:
         gen = getattr(self, "_wgen", 0)
         if getattr(self, "_wt_gen", None) == gen:
             return self._wt
-        cfg, W = self.cfg, self.W
+        W = self.W
         if getattr(self, "_wt", None) is None:
-            names = [f"{l}.{n}" for l in range(cfg.n_layer) for n in self._T_NAMES]
+            names = self._t_names()
             total = sum(W[n].numel() for n in names)
             buf = torch.empty(total, device=self.device, dtype=torch.bfloat16)
             self._wt, off = {}, 0
@@ -378,10 +396,15 @@ class TransformerEngine:
             cache.ring[:, :T].copy_(A.logits.view(B, T, cfg.v_pad))
             cache.tokens[:, :T].copy_(idx)
             cache.length = T
+            cache.pos_dev.fill_(T)
         return A.logits.view(B, T, cfg.v_pad)[:, :, :V]
 
     def decode_cache(self, B, context=None):
         return TransformerDecodeCache(self.cfg, B, context or self.cfg.block_len, self.device, self.act)
+
+    # decode steps after the first replay one captured HIP graph
+    # (MSQ_NO_STEP_GRAPH=1: eager launches with host-side positions)
+    step_graphs = not os.environ.get("MSQ_NO_STEP_GRAPH")
 
     @torch.no_grad()
     def step(self, tok, cache):
@@ -390,11 +413,67 @@ class TransformerEngine:
         last row of its window, keys / values of the window from the cache).
         Leaves cache.lse = the time-axis LSE of the window's OTHER rows (what
         msq_filtered_logit_step then extends by this row) and writes the row
-        into the window's logits ring."""
-        cfg, P, W = self.cfg, self.P, self.W
+        into the window's logits ring.
+
+        The first step after the prefill (every ring block's partial LSE) runs
+        eagerly; every later one has the same ~60 launches with the same
+        arguments once the position comes from device memory
+        (msq_relattn_decode_pos, msq_ring_step), so it is captured once and
+        replayed as one HIP graph."""
         if not tok.is_cuda:
             raise RuntimeError("the MI355X engine runs on the GPU only (no CPU fallback)")
         self.refresh_shadow()
+        if self.step_graphs and cache.part_valid and tok.is_contiguous() and cache.length >= 1:
+            if cache.graph is None or cache.graph_tok != tok.data_ptr() or cache.graph_gen != self._wgen_now():
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._step_dev(tok, cache)
+                cache.graph, cache.graph_tok, cache.graph_gen = g, tok.data_ptr(), self._wgen_now()
+            cache.graph.replay()
+            cache.length += 1
+            cache.logits = cache.row_buf
+            return cache.row_buf
+        row = self._step_host(tok, cache)
+        cache.pos_dev.fill_(cache.length)
+        return row
+
+    def _wgen_now(self):
+        return getattr(self, "_wgen", 0)
+
+    def _layers_step(self, x, cache, attn):
+        """the per-layer body of a decode step; attn(l) runs the decode attention"""
+        cfg, P, W = self.cfg, self.P, self.W
+        for l in range(cfg.n_layer):
+            ops.layernorm_fwd(x, P[f"{l}.ln1_w"], P[f"{l}.ln1_b"], out=cache.a, mean=cache.st[0], rstd=cache.st[1])
+            ops.gemm(cache.a, W[f"{l}.wqkv"], out=cache.qkv)
+            attn(l)
+            ops.gemm(cache.o, W[f"{l}.wproj"], out=cache.xm, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.bproj"], aux=x)
+            ops.layernorm_fwd(cache.xm, P[f"{l}.ln2_w"], P[f"{l}.ln2_b"], out=cache.c, mean=cache.st[0],
+                              rstd=cache.st[1])
+            ops.gemm(cache.c, W[f"{l}.w1"], out=cache.h, epilogue=L.EPI_BIAS_RELU, bias=P[f"{l}.b1"])
+            ops.gemm(cache.h, W[f"{l}.w2"], out=x, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.b2"], aux=cache.xm)
+        ops.layernorm_fwd(x, P["lnf_w"], P["lnf_b"], out=cache.f, mean=cache.stf[0], rstd=cache.stf[1])
+
+    def _step_dev(self, tok, cache):
+        """step() with every position-dependent quantity read from cache.pos_dev"""
+        cfg, P, W = self.cfg, self.P, self.W
+        B, d, H, hs = cache.B, cfg.n_embd, cfg.n_heads, cfg.head_size
+        s = stream()
+        scale = d ** -0.5
+        call("msq_embed_fwd", ptr(cache.x), ptr(P["tok_emb"]), ptr(P["meta_emb"]), ptr(tok), None, B, 1, 0, d, s)
+
+        def attn(l):
+            call("msq_relattn_decode_pos", dt(cache.qkv), ptr(cache.o), cache.o.stride(0), ptr(cache.qkv),
+                 cache.qkv.stride(0), ptr(cache.k[l]), ptr(cache.v[l]), ptr(W[f"{l}.R"]), cfg.s_max, B, H, hs,
+                 cache.S_ring, N_META, ptr(cache.pos_dev), float(scale), s)
+        self._layers_step(cache.x, cache, attn)
+        ops.gemm(cache.f, W["lm_w"], out=cache.row_buf, epilogue=L.EPI_BIAS, bias=P["lm_b"])
+        call("msq_ring_step", ptr(cache.lse), ptr(cache.part), ptr(cache.ring), dt(cache.ring), cfg.v_pad, B, cache.ctx,
+             cfg.vocab_size, cache.RB, ptr(cache.row_buf), cache.row_buf.stride(0), ptr(cache.tokens), ptr(tok),
+             ptr(cache.pos_dev), s)
+
+    def _step_host(self, tok, cache):
+        cfg, P, W = self.cfg, self.P, self.W
         B, d, H, hs = cache.B, cfg.n_embd, cfg.n_heads, cfg.head_size
         ctx, pos = cache.ctx, cache.length
         n_tok = min(pos + 1, ctx)
@@ -404,19 +483,12 @@ class TransformerEngine:
         scale = d ** -0.5
         tok = tok.contiguous()
         call("msq_embed_fwd", ptr(cache.x), ptr(P["tok_emb"]), ptr(P["meta_emb"]), ptr(tok), None, B, 1, 0, d, s)
-        x = cache.x
-        for l in range(cfg.n_layer):
-            ops.layernorm_fwd(x, P[f"{l}.ln1_w"], P[f"{l}.ln1_b"], out=cache.a, mean=cache.st[0], rstd=cache.st[1])
-            ops.gemm(cache.a, W[f"{l}.wqkv"], out=cache.qkv)
+
+        def attn(l):
             call("msq_relattn_decode", dt(cache.qkv), ptr(cache.o), cache.o.stride(0), ptr(cache.qkv),
                  cache.qkv.stride(0), ptr(cache.k[l]), ptr(cache.v[l]), ptr(W[f"{l}.R"]), cfg.s_max, B, H, hs,
                  cache.S_ring, N_META, n_tok, N_META + slot, first % ctx, float(scale), s)
-            ops.gemm(cache.o, W[f"{l}.wproj"], out=cache.xm, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.bproj"], aux=x)
-            ops.layernorm_fwd(cache.xm, P[f"{l}.ln2_w"], P[f"{l}.ln2_b"], out=cache.c, mean=cache.st[0],
-                              rstd=cache.st[1])
-            ops.gemm(cache.c, W[f"{l}.w1"], out=cache.h, epilogue=L.EPI_BIAS_RELU, bias=P[f"{l}.b1"])
-            ops.gemm(cache.h, W[f"{l}.w2"], out=x, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.b2"], aux=cache.xm)
-        ops.layernorm_fwd(x, P["lnf_w"], P["lnf_b"], out=cache.f, mean=cache.stf[0], rstd=cache.stf[1])
+        self._layers_step(cache.x, cache, attn)
         # the new row goes straight into its ring slot, over the row that leaves
         # the window (or the empty slot); the LSE below leaves that slot out
         row = cache.ring[:, slot]
@@ -505,7 +577,7 @@ class TransformerEngine:
                 ops.colsum(dl, G["lm_b"][:V], accumulate=True)
         on_side("dlogits", lm_w)
         Wt = self.transposed_weights()
-        ops.gemm(dlogits, W["lm_w"], tb=True, out=Bw["df"])
+        dx_gemm(dlogits, W, Wt, "lm_w", Bw["df"])
         gres = Bw["gres"]
         gres.zero_()
         gb = Bw["gb"] if Bw["gb"] is not None else gres
@@ -540,7 +612,7 @@ class TransformerEngine:
             def ffn1_w(l=l):
                 ops.gemm(Bw["dh"], A.c[l], ta=True, tb=True, out=G[f"{l}.w1"], epilogue=L.EPI_ACCUM)
             on_side("dh", ffn1_w)
-            ops.gemm(Bw["dh"], W[f"{l}.w1"], tb=True, out=Bw["dtmp"])
+            dx_gemm(Bw["dh"], W, Wt, f"{l}.w1", Bw["dtmp"])
             before_write("gb2")
             ops.layernorm_bwd(gres, Bw["dtmp"], A.xm[l], A.st2[l, 0], A.st2[l, 1], P[f"{l}.ln2_w"], G[f"{l}.ln2_w"],
                               G[f"{l}.ln2_b"], dx_copy=gb2 if Bw["gb"] is not None else None,
@@ -550,7 +622,7 @@ class TransformerEngine:
             def proj_w(l=l):
                 ops.gemm(gb2, A.o[l], ta=True, tb=True, out=G[f"{l}.wproj"], epilogue=L.EPI_ACCUM)
             on_side("gb2", proj_w)
-            ops.gemm(gb2, W[f"{l}.wproj"], tb=True, out=Bw["dtmp"])
+            dx_gemm(gb2, W, Wt, f"{l}.wproj", Bw["dtmp"])
             before_write("dqkv")
             relattn_bwd(Bw["dtmp"], A.o[l], A.lse[l], A.qkv[l], W[f"{l}.R"], B, S, H, hs, scale, dqkv=Bw["dqkv"],
                         dR=G[f"{l}.R"], drop=(A._masks[l], p) if p > 0 else None)
@@ -558,7 +630,7 @@ class TransformerEngine:
             def qkv_w(l=l):
                 ops.gemm(Bw["dqkv"], A.a[l], ta=True, tb=True, out=G[f"{l}.wqkv"], epilogue=L.EPI_ACCUM)
             on_side("dqkv", qkv_w)
-            ops.gemm(Bw["dqkv"], W[f"{l}.wqkv"], tb=True, out=Bw["dtmp"])
+            dx_gemm(Bw["dqkv"], W, Wt, f"{l}.wqkv", Bw["dtmp"])
             before_write("gb")
             ops.layernorm_bwd(gres, Bw["dtmp"], A.x[l], A.st1[l, 0], A.st1[l, 1], P[f"{l}.ln1_w"], G[f"{l}.ln1_w"],
                               G[f"{l}.ln1_b"], dx_copy=Bw["gb"], drop=dsite(DROP_FFN + l - 1) if l > 0 else None,

@@ -131,6 +131,17 @@ int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, cons
                 int64_t strideC, int64_t batch, int epilogue, const float* bias, const void* aux, int aux_dtype,
                 int64_t ld_aux, int64_t stride_aux, uint32_t seed, uint32_t site, float p, void* ws,
                 int64_t ws_bytes, void* stream);
+/* Which kernel family runs the large (M > 64) bf16 products (tests / A-B
+ * tools; process-wide, default from the environment at the first call):
+ *   MSQ_ROUTE_DEFAULT  persistent 256 tile for the forward / dX products, the
+ *                      per-tile 256 tile (split-K) for the weight gradients;
+ *   MSQ_ROUTE_TILE256  the per-tile 256 tile for every product (MSQ_GEMM_NOP);
+ *   MSQ_ROUTE_TILE128  the 128 tile only (MSQ_GEMM128).
+ * Returns the previous route.                                                 */
+#define MSQ_ROUTE_DEFAULT 0
+#define MSQ_ROUTE_TILE256 1
+#define MSQ_ROUTE_TILE128 2
+int msq_gemm_set_route(int route);
 /* column sums (bias gradients): out[c] (+)= sum_r x[r, c]                      */
 /* C = epi(op(A) op(B)) in bf16 (epilogue NONE or RELU_MASK with aux, no
  * batch) and dbias[n] = (accumulate ? dbias[n] : 0) + sum_m C[m][n] in fp32:
@@ -230,6 +241,16 @@ int msq_filtered_colstats(float* col_lse, const void* logits, int dtype, int64_t
 int msq_ring_lse(float* col_lse, float* part, const void* ring, int dtype, int64_t ld, int64_t B, int64_t ctx,
                  int64_t V, int64_t rows_per_block, int64_t blk_lo, int64_t blk_hi, int64_t skip_row,
                  int64_t blk_extra, void* stream);
+/* One graph-replayable cached-decode step of the ring (the same computation as
+ * writing the new logits row into slot pos % ctx and calling msq_ring_lse for
+ * that slot's block and the previous row's block): copies row [B][ld_row] into
+ * ring slot pos % ctx and tok[b] into tokens [B][ctx], recomputes those two
+ * blocks' partials, merges col_lse and advances *pos by one. pos: int64 on the
+ * device (>= 1, the sequence position of the new row), so the launch arguments
+ * do not change from step to step. scripts/generate.py:29-33 per new token. */
+int msq_ring_step(float* col_lse, float* part, void* ring, int dtype, int64_t ld, int64_t B, int64_t ctx, int64_t V,
+                  int64_t rows_per_block, const void* row, int64_t ld_row, int64_t* tokens, const int64_t* tok,
+                  int64_t* pos, void* stream);
 /* loss (fp32 scalar, device) = mean over B*T of the row CE of Z. If dlogits
  * != NULL also writes grad_scale * d(sum of row CE)/dlogits (so grad_scale =
  * 1/(B*T) gives the gradient of the mean).                                  */
@@ -369,6 +390,13 @@ int msq_midi_decode(const int64_t* rows, int64_t B, int64_t L, int64_t ld, const
 int msq_relattn_decode(int dtype, void* out, int64_t ldo, const void* qkv, int64_t ldq, void* kcache, void* vcache, const void* R,
                        int64_t S_max, int64_t B, int64_t H, int64_t hs, int64_t S_ring, int64_t n_meta, int64_t n_tok,
                        int64_t new_slot, int64_t first_mod, float scale, void* stream);
+/* msq_relattn_decode with the step's sequence position read from device
+ * memory (*pos, int64): n_tok = min(pos + 1, S_ring - n_meta), new_slot =
+ * n_meta + pos % ctx, first_mod = (pos + 1 - n_tok) % ctx; for a captured
+ * (graph-replayed) decode step whose launch arguments stay fixed.          */
+int msq_relattn_decode_pos(int dtype, void* out, int64_t ldo, const void* qkv, int64_t ldq, void* kcache, void* vcache,
+                           const void* R, int64_t S_max, int64_t B, int64_t H, int64_t hs, int64_t S_ring,
+                           int64_t n_meta, const int64_t* pos, float scale, void* stream);
 
 /* Note -> token encode of a batch of songs (replaces processing/processing.py
  * :129-152 encode + :111-126 adjust_note_time, the preprocessing step of

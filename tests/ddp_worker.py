@@ -47,7 +47,36 @@ def rank_slice(mode, rank, world, B=4):
     return slice(rank * n, (rank + 1) * n)
 
 
+class _CallLog:
+    """libmidiseq launch observer (midiseq._lib.TAP): keeps the last calls so
+    that a failing rank names the launches before its error (a device fault
+    surfaces at a later API call; AMD_SERIALIZE_KERNEL=3 makes it the next one)."""
+
+    def __init__(self, n=12):
+        self.names, self.n = [], n
+
+    trace = bool(os.environ.get("MSQ_TRACE_CALLS"))  # diagnostics: synchronise after every launch
+
+    def __call__(self, name, args, launch):
+        self.names = (self.names + [name])[-self.n:]
+        r = launch()
+        if self.trace:
+            torch.cuda.synchronize()
+        return r
+
+
 def main():
+    from midiseq import _lib
+    log = _CallLog()
+    _lib.TAP = log
+    try:
+        _main()
+    except BaseException:
+        print(f"rank {os.environ.get('RANK')}: last libmidiseq calls {log.names}", file=sys.stderr, flush=True)
+        raise
+
+
+def _main():
     kind, mode, out = sys.argv[1], sys.argv[2], sys.argv[3]
     rank, _, world = setup_distributed(backend="gloo")
     assert world == 2

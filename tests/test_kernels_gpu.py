@@ -122,24 +122,33 @@ def test_gemm_skinny_decode_shapes(M, N, K):
     assert _rel(ob.float(), base + bias) < 1e-2
 
 
+ROUTES = {"persistent": L.ROUTE_DEFAULT, "tile256": L.ROUTE_TILE256, "tile128": L.ROUTE_TILE128}
+
+
+@pytest.mark.parametrize("route", list(ROUTES))
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 1), (1, 0)])
-@pytest.mark.parametrize("M,N,K", [(4104, 2056, 1000), (2304, 4096, 512)])
-def test_gemm256_layouts_and_edges(ta, tb, M, N, K):
-    """Large products take the 256x256 LDS-DMA tile; M/N/K edges are
-    zero-filled by the buffer descriptor (K % 64 != 0, M % 256 != 0)."""
+@pytest.mark.parametrize("M,N,K", [(4104, 2056, 1000), (2304, 4096, 512), (1800, 776, 64)])
+def test_gemm256_layouts_and_edges(route, ta, tb, M, N, K):
+    """Large products on each kernel family (msq_gemm_set_route): the
+    persistent 256 tile (forward / dX products), the per-tile 256 LDS-DMA tile
+    and the 128 tile; M/N/K edges are zero-filled by the buffer descriptor
+    (K % 64 != 0, M % 256 != 0, a single K-step), fp32 and bf16 outputs."""
     g = torch.Generator().manual_seed(M + N + K + ta + 2 * tb)
     a = torch.randn(M, K, generator=g).bfloat16()
     b = torch.randn(N, K, generator=g).bfloat16()
     ref = a.float() @ b.float().t()
     A = (a.t().contiguous() if ta else a).to(dev)
     Bm = (b.t().contiguous() if tb else b).to(dev)
-    out = ops.gemm(A, Bm, ta=bool(ta), tb=bool(tb), out_dtype=torch.float32)
-    torch.cuda.synchronize()
-    assert _rel(out, ref) < 2e-3
-    acc = torch.randn(M, N, generator=g).to(dev)
-    ref2 = acc.cpu() + ref
-    ops.gemm(A, Bm, ta=bool(ta), tb=bool(tb), out=acc, epilogue=L.EPI_ACCUM)
-    assert _rel(acc, ref2) < 2e-3
+    with ops.gemm_route(ROUTES[route]):
+        out = ops.gemm(A, Bm, ta=bool(ta), tb=bool(tb), out_dtype=torch.float32)
+        outb = ops.gemm(A, Bm, ta=bool(ta), tb=bool(tb), out_dtype=torch.bfloat16)
+        torch.cuda.synchronize()
+        assert _rel(out, ref) < 2e-3
+        assert _rel(outb.float(), ref) < 1e-2
+        acc = torch.randn(M, N, generator=g).to(dev)
+        ref2 = acc.cpu() + ref
+        ops.gemm(A, Bm, ta=bool(ta), tb=bool(tb), out=acc, epilogue=L.EPI_ACCUM)
+        assert _rel(acc, ref2) < 2e-3
 
 
 def test_gemm256_splitk_weight_grad():
@@ -154,21 +163,55 @@ def test_gemm256_splitk_weight_grad():
     assert _rel(G.cpu() - 0.5, ref) < 2e-3
 
 
-def test_gemm256_epilogues_bf16_out():
-    g = torch.Generator().manual_seed(12)
-    M, N, K = 3000, 3072, 1024
+@pytest.mark.parametrize("route", list(ROUTES))
+@pytest.mark.parametrize("M", [3000, 4096])
+def test_gemm256_epilogues_bf16_out(route, M):
+    """Every forward / dX epilogue on each kernel family, with and without an
+    M tail (3000 = 11 x 256 + 184)."""
+    g = torch.Generator().manual_seed(12 + M)
+    N, K = 3072, 1024
     a = torch.randn(M, K, generator=g).bfloat16()
     w = (torch.randn(N, K, generator=g) * 0.05).bfloat16()
     bias = torch.randn(N, generator=g)
     res = torch.randn(M, N, generator=g)
     base = a.float() @ w.float().t()
     A, W, bi, R = a.to(dev), w.to(dev), bias.to(dev), res.to(dev)
-    o = ops.gemm(A, W, out_dtype=torch.bfloat16, epilogue=L.EPI_BIAS_RELU, bias=bi)
-    assert _rel(o.float(), torch.relu(base + bias)) < 1e-2
-    o = ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_BIAS_RESID, bias=bi, aux=R)
-    assert _rel(o, base + bias + res) < 2e-3
-    o = ops.gemm(A, W, out_dtype=torch.bfloat16, epilogue=L.EPI_RELU_MASK, aux=R.bfloat16())
-    assert _rel(o.float(), base * (res.bfloat16().float() > 0)) < 1e-2
+    with ops.gemm_route(ROUTES[route]):
+        o = ops.gemm(A, W, out_dtype=torch.bfloat16)
+        assert _rel(o.float(), base) < 1e-2
+        o = ops.gemm(A, W, out_dtype=torch.bfloat16, epilogue=L.EPI_BIAS, bias=bi)
+        assert _rel(o.float(), base + bias) < 1e-2
+        o = ops.gemm(A, W, out_dtype=torch.bfloat16, epilogue=L.EPI_BIAS_RELU, bias=bi)
+        assert _rel(o.float(), torch.relu(base + bias)) < 1e-2
+        o = ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_BIAS_RESID, bias=bi, aux=R)
+        assert _rel(o, base + bias + res) < 2e-3
+        o = ops.gemm(A, W, out_dtype=torch.bfloat16, epilogue=L.EPI_RELU_MASK, aux=R.bfloat16())
+        assert _rel(o.float(), base * (res.bfloat16().float() > 0)) < 1e-2
+        o = ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_RELU_MASK, aux=R)
+        assert _rel(o, base * (res > 0)) < 2e-3
+        # dropout + residual epilogue: the same keep mask on every route
+        o = ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_BIAS_RESID, bias=bi, aux=R, drop=(7, 3, 0.1))
+        kept = (o.cpu() - res) != 0
+        frac = kept.float().mean().item()
+        assert 0.88 < frac < 0.92, frac
+        assert _rel(torch.where(kept, o.cpu(), torch.zeros(())), torch.where(kept, (base + bias) / 0.9 + res,
+                                                                             torch.zeros(()))) < 2e-3
+
+
+def test_gemm_routes_bitwise_mask_and_layout():
+    """The persistent tile's bf16 store widening (16-lane swaps) against the
+    per-tile kernel: identical bf16 outputs, bitwise, on a shape with several
+    tiles per workgroup (M tail, 2 K-steps)."""
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 2 * 256 * 256 + 40, 512, 128
+    a = torch.randn(M, K, generator=g).bfloat16().to(dev)
+    w = torch.randn(N, K, generator=g).bfloat16().to(dev)
+    with ops.gemm_route(L.ROUTE_DEFAULT):
+        p = ops.gemm(a, w, out_dtype=torch.bfloat16)
+    with ops.gemm_route(L.ROUTE_TILE256):
+        q = ops.gemm(a, w, out_dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    assert torch.equal(p, q)
 
 
 def test_gemm_batched_strided():

@@ -32,7 +32,7 @@ def main():
     M = 32 * 2054
     shapes = [("qkv", 3072, 1024), ("proj", 1024, 1024), ("ffn1", 4096, 1024), ("ffn2", 1024, 4096), ("lm", 17920, 1024)]
     g = torch.Generator(device=dev).manual_seed(0)
-    print(f"{'shape':6s} {'kind':4s} {'msq ms':>8s} {'TF/s':>7s} {'blas ms':>8s} {'TF/s':>7s}")
+    print(f"{'shape':6s} {'kind':4s} {'msq ms':>8s} {'TF/s':>7s} {'t256 ms':>8s} {'TF/s':>7s} {'blas ms':>8s} {'TF/s':>7s}")
     for name, N, K in shapes:
         x = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
         w = torch.randn(N, K, device=dev, dtype=torch.bfloat16, generator=g) * 0.02
@@ -62,8 +62,11 @@ def main():
             ]
         for kind, a, b in cases:
             ta_ = timeit(a)
+            with ops.gemm_route(L.ROUTE_TILE256):
+                tt_ = timeit(a)
             tb_ = timeit(b)
-            print(f"{name:6s} {kind:4s} {ta_:8.3f} {fl / ta_ / 1e9:7.1f} {tb_:8.3f} {fl / tb_ / 1e9:7.1f}", flush=True)
+            print(f"{name:6s} {kind:4s} {ta_:8.3f} {fl / ta_ / 1e9:7.1f} {tt_:8.3f} {fl / tt_ / 1e9:7.1f} "
+                  f"{tb_:8.3f} {fl / tb_ / 1e9:7.1f}", flush=True)
         # correctness spot check of fwd against BLAS
         ops.gemm(x, w, out=y)
         ref = torch.matmul(x, w.t())
