@@ -95,10 +95,18 @@ CLASSIFY = {
     "msq_embed_fwd": lambda a: ("embed", None, None), "msq_embed_bwd": lambda a: ("embed", None, None),
     # SSD scan (SURVEY.md §8(d) cfg 3): bf16 x, B, C, dt in + y out = 8 512 B per token per layer (d_inner 2048)
     "msq_mamba_ssd_fwd_state": lambda a: ("ssd_fwd", None, (4 * a[14] + 4 * 64 + 2 * a[15]) * float(a[12] * a[13])),
-    "msq_mamba_ssd_bwd": lambda a: ("ssd_bwd", None, None),
-    "msq_mamba_conv_fwd": lambda a: ("mamba_conv", None, None), "msq_mamba_conv_bwd": lambda a: ("mamba_conv", None, None),
-    "msq_mamba_gnorm_fwd": lambda a: ("mamba_gnorm", None, None),
-    "msq_mamba_gnorm_bwd": lambda a: ("mamba_gnorm", None, None),
+    # the rest of the Mamba2 mixer, bytes per token per layer as the kernels move
+    # them (Mamba byte model; N = 64 states, conv_dim = di + 128):
+    # ssd_bwd: dy f32 + xc bf16 + dt + chunk states f32 (H P N 4 / 64 tokens) in,
+    #          dxc f32 + ddt out
+    "msq_mamba_ssd_bwd": lambda a: ("ssd_bwd", None, float(a[17] * a[18]) * (
+        4 * a[19] + 2 * (a[19] + 128) + 2 * a[20] + a[20] * 64 * 64 * 4 / 64 + 4 * (a[19] + 128) + 2 * a[20])),
+    # conv fwd: xBC bf16 in, xc bf16 out; bwd: dxc f32 + xBC bf16 in, dxBC bf16 out
+    "msq_mamba_conv_fwd": lambda a: ("mamba_conv", None, float(a[7] * a[8]) * 4 * (a[9] + 128)),
+    "msq_mamba_conv_bwd": lambda a: ("mamba_conv", None, float(a[10] * a[11]) * 8 * (a[12] + 128)),
+    # gated RMSNorm fwd: y f32 + z bf16 in, yn bf16 + rstd out; bwd: y f32, z, dyn f32 in, dy f32, dz out
+    "msq_mamba_gnorm_fwd": lambda a: ("mamba_gnorm", None, float(a[9]) * (4 * a[10] + 2 * a[10] + 2 * a[10] + 4)),
+    "msq_mamba_gnorm_bwd": lambda a: ("mamba_gnorm", None, float(a[12]) * (4 + 2 + 4 + 4 + 2) * a[13]),
 }
 
 
@@ -201,11 +209,14 @@ def cpu_baseline():
     reference ratio measured in the build container on the same cores for both
     (tools/calibrate_cpu.py -> profiles/r2/cpu_calibration.json) gives the
     reference-equivalent rate beside it."""
-    threads = min(16, os.cpu_count() or 1)
+    nproc = os.cpu_count() or 1
+    # at most 16 threads: the GPU box gives a job a 16-CPU share of a larger
+    # host (os.cpu_count() reports the whole machine)
+    threads = min(16, nproc)
     torch.set_num_threads(threads)
     v2, n2 = _oracle_train_rate(dict(n_embd=1024, n_heads=8, n_layer=8, block_len=2048), 1, 2048, 15.0, 3)
     v1, n1 = _oracle_train_rate(dict(n_embd=128, n_heads=8, n_layer=2, block_len=256), 2, 256, 5.0, 30)
-    out = {"value": round(v2, 2), "unit": "MIDI tokens/s", "cores": threads, "kind": "port",
+    out = {"value": round(v2, 2), "unit": "MIDI tokens/s", "cores": threads, "host_cpus": nproc, "kind": "port",
            "sample": f"oracle/ fp32 train step (fwd+filtered CE+bwd+Adam), default model, B=1, T=2048, {n2} steps",
            "cfg1": {"value": round(v1, 1), "unit": "MIDI tokens/s",
                     "sample": f"oracle/ fp32 train step, 2 layers d=128 h=8, B=2, T=256, {n1} steps"}}
@@ -254,6 +265,12 @@ def _group(world):
     return True if world > 1 else None
 
 
+def _fwd_flops(cfg, T):
+    """algorithmic forward FLOPs of one sequence (SURVEY.md §8(d) cfg 2)"""
+    S, d = T + 6, cfg.n_embd
+    return cfg.n_layer * (24 * S * d * d + 3 * d * S * (S + 1)) + 2 * T * d * cfg.vocab_size
+
+
 def decode_leg(dev, rank, world, steps=3, B=64, T=2048):
     """Config 5: B=64 composer-conditioned prompts of 2048 tokens per GPU
     (the global batch of world x 64 rows sharded by row: generate(group=...),
@@ -266,8 +283,14 @@ def decode_leg(dev, rank, world, steps=3, B=64, T=2048):
     src, _, meta = SyntheticMIDI(B, T, dev, rank, n_batches=1).batches[0]
     el = timed(lambda: generate(m, T, src, meta, num_tokens=1, rng=random.Random(0), device=dev,
                                 group=_group(world)), steps, 1, world, dev)
+    flops = B * _fwd_flops(m.cfg, T)  # SURVEY.md §8(d) cfg 5: 64 x F_fwd = 37.9 TFLOP per step
     del m
+    ach = flops / (el / steps) / 1e12
     return {"value": round(world * B * steps / el, 2), "unit": "new tokens/s", "ms_per_token_step": round(el / steps * 1e3, 3),
+            "roofline": {"kernel": "whole decode step (full forward of the window + filtered logit + sampler)",
+                         "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "algorithmic_work_per_step": flops},
             "config": {"workload": "cfg 5 exact sliding-window decode (full fwd per step)", "batch_per_gpu": B,
                        "context": T}}
 
@@ -353,10 +376,25 @@ def decode_cached_leg(dev, rank, world, B=64, T=2048, K=32, steps=2):
                              mode="cached", return_tensor=True, group=_group(world))
     el_pre = timed(lambda: run(1), steps, 1, world, dev)
     el_all = timed(lambda: run(1 + K), steps, 1, world, dev)
+    cfg = m.cfg
     del m
     ms_step = (el_all - el_pre) / (steps * K) * 1e3
+    # HBM bytes of one cached step: every layer's K / V ring of the
+    # window (bf16), the bf16 weights once (layers + lm_head), the logits rows of
+    # the one or two 64-row ring blocks whose LSE partials are recomputed, the new
+    # row written
+    d, L_, Vp = cfg.n_embd, cfg.n_layer, cfg.v_pad
+    kv = L_ * B * (T + 6) * d * 2 * 2
+    wts = (L_ * 12 * d * d + Vp * d) * 2
+    ring = 1.5 * 64 * B * Vp * 2 + B * Vp * 2
+    nbytes = kv + wts + ring
+    ach = nbytes / (ms_step * 1e-3) / 1e9
     return {"value": round(world * B / (ms_step * 1e-3), 1), "unit": "new tokens/s",
             "ms_per_token_step": round(ms_step, 3), "prefill_ms": round(el_pre / steps * 1e3, 2),
+            "roofline": {"kernel": "whole cached step (graph-replayed)", "bound": "hbm", "achieved": round(ach, 1),
+                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
+                         "algorithmic_bytes_per_step": int(nbytes),
+                         "bytes_model": "K/V ring L*B*(T+6)*d*2*2 + bf16 weights + 1.5 ring blocks of 64 rows + new row"},
             "config": {"workload": "cfg 5 Transformer cached decode (KV ring, approximation of the exact window)",
                        "batch_per_gpu": B, "context": T, "new_tokens": K}}
 

@@ -1,12 +1,11 @@
 // Relative-position flash attention backward, key/value-major pass, v4.
 // (model_transformer.py:54-90 differentiated; P recomputed from the forward's
-// row log-sum-exp.):
+// row log-sum-exp.)  Same outputs as v3 (attn_bwd3.hip):
 //   P_ij  = exp(scale (q_i.k_j + q_i.R[S-1-i+j]) - lse_i)
 //   dS_ij = P_ij (dO_i.v_j - D_i) scale,           D_i = dO_i.O_i
 //   dV_j  = sum_i P_ij dO_i,  dK_j = sum_i dS_ij q_i   (accumulated here)
-//   dS written once, r-indexed (dQR, r = S-1-i+j), for the dq product (which
-//   reads it for both of its terms) and the dR product; metadata-block
-//   entries j > i go to meta_ds.
+//   dS written j-indexed (dSj) and r-indexed (dQR, r = S-1-i+j) for the dq / dR
+//   products; metadata-block entries j > i go to meta_ds.
 //
 // One workgroup = 4 waves (one per SIMD, the whole register file each) = 128
 // keys of one (b, h); a wave owns 32 keys on the lanes of v_mfma_f32_32x32x16
@@ -90,7 +89,7 @@ constexpr int O_M = O_D + NB * KB * 4;      // metadata-block BD table
 // vector memory ops per thread: NDMA per staged tile (Q 2, dO 2, R 2, one
 // 4-byte piece: lse / D on waves 0-1, keep words or a dummy on waves 2-3),
 // NST dS stores per tile
-constexpr int NDMA = 7, NST = 2;
+constexpr int NDMA = 7, NST = 4;
 // dS staging for the coalesced row stores: 32 query rows x 128 keys bf16
 constexpr int T_PITCH = 272, T_BYTES = QT * T_PITCH;
 constexpr int O_T = O_M + 64 * 4;
@@ -170,8 +169,8 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
                                                               const float* __restrict__ Dv,
                                                               const bf16* __restrict__ dout, int64_t ldo,
                                                               bf16* __restrict__ dqkv, int64_t ldd,
-                                                              bf16* __restrict__ dqr, int64_t ldr,
-                                                              float* __restrict__ meta_ds) {
+                                                              bf16* __restrict__ dqr, bf16* __restrict__ dsj,
+                                                              int64_t ldr, float* __restrict__ meta_ds) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sR = smem + O_R;
     const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, c32 = lane & 31;
@@ -191,6 +190,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
     const __amdgpu_buffer_rsrc_t rl = make_rsrc(Lp, (uint32_t)(S * 4));
     const __amdgpu_buffer_rsrc_t rd = make_rsrc(Dp, (uint32_t)(S * 4));
     bf16* qr_rows = dqr + ((int64_t)h * a.B + b) * S * ldr;
+    bf16* sj_rows = dsj + ((int64_t)h * a.B + b) * S * ldr;
     float* mbd = (float*)(smem + O_M);
     const int nm = (int)min<int64_t>(a.n_meta, S);
     const float c2 = a.scale * LOG2E;
@@ -396,23 +396,27 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
 
     // dS of a tile (j <= i, else 0) is staged in LDS and stored in the NEXT
     // iteration after that iteration's prefetch, as whole rows: thread t writes
-    // 8 keys of query rows t/16 and 16 + t/16, r-indexed (dQR, r = S-1-i+j:
-    // 2-byte aligned rows, unaligned 16-B chunks; entries j > i are zeros and
-    // land at r >= S, in the zeroed row padding, ldr >= S + 136). The 2 stores
-    // per thread are the youngest vector memory ops at the next tile's wait
-    // (vmcnt(2)); invalid rows use the out-of-range offset, so the count is exact.
+    // 8 keys of query rows t/16 and 16 + t/16, once j-indexed (dSj, aligned
+    // 16-B chunks) and once r-indexed (dQR, r = S-1-i+j: 2-byte aligned rows,
+    // unaligned 16-B chunks; entries j > i land at r >= S, in the row padding,
+    // ldr >= S + 128, that no reader touches). The 4 stores per thread are the
+    // youngest vector memory ops at the next tile's wait (vmcnt(4)); invalid
+    // rows use the out-of-range offset, so the count is exact.
     const uint32_t ds_bytes = (uint32_t)min<int64_t>((int64_t)S * ldr * 2, OOB - 1);
     auto store_ds = [&](int ip, int sbuf) {
         // descriptors rebuilt here from readfirstlane'd halves: kept live across
         // the loop they ended up in VGPRs and every store ran a waterfall loop
         const __amdgpu_buffer_rsrc_t rqr = make_rsrc(qr_rows, ds_bytes);
+        const __amdgpu_buffer_rsrc_t rsj = make_rsrc(sj_rows, ds_bytes);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const int row = (tid >> 4) + 16 * k, ch = tid & 15;
             const u32x4 v = *(const u32x4*)(smem + O_T + sbuf * T_BYTES + row * T_PITCH + ch * 16);
             const int i = ip + row, j = j0 + 8 * ch;
             const bool in = i < S;
+            const uint32_t os = in ? (uint32_t)(((int64_t)i * ldr + j) * 2) : OOB;
             const uint32_t oq = in ? (uint32_t)(((int64_t)i * ldr + (S - 1 - i + j)) * 2) : OOB;
+            __builtin_amdgcn_raw_buffer_store_b128(v, rsj, os, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b128(v, rqr, oq, 0, 0);
         }
     };
@@ -657,7 +661,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
 }  // namespace
 
 int flash_bwd_kv4(const AttnArgs& a, const float* lse, const float* Dv, const bf16* dout, int64_t ldo, bf16* dqkv,
-                  int64_t ldd, bf16* dqr, int64_t ldr, float* meta_ds, hipStream_t s) {
+                  int64_t ldd, bf16* dqr, bf16* dsj, int64_t ldr, float* meta_ds, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)flash_bwd_kv4_kernel<false>,
@@ -668,13 +672,13 @@ int flash_bwd_kv4(const AttnArgs& a, const float* lse, const float* Dv, const bf
     }
     if (a.S * a.ldq * 2 >= (int64_t)OOB || a.S * ldo * 2 >= (int64_t)OOB || a.n_meta > 8) return -1;
     if (a.colmask && mask_bh_bytes(a.mask_ld) >= (int64_t)OOB) return -1;
-    if (ldr < a.S + 136) return -1;
+    if (ldr < a.S + 128) return -1;
     const dim3 grid((unsigned)((a.S + KB - 1) / KB), (unsigned)a.H, (unsigned)a.B);
     if (a.colmask)
         hipLaunchKernelGGL(flash_bwd_kv4_kernel<true>, grid, dim3(NT), LDS_BYTES, s, a, lse, Dv, dout, ldo, dqkv, ldd,
-                           dqr, ldr, meta_ds);
+                           dqr, dsj, ldr, meta_ds);
     else
         hipLaunchKernelGGL(flash_bwd_kv4_kernel<false>, grid, dim3(NT), LDS_BYTES, s, a, lse, Dv, dout, ldo, dqkv, ldd,
-                           dqr, ldr, meta_ds);
+                           dqr, dsj, ldr, meta_ds);
     return 0;
 }

@@ -15,10 +15,10 @@
 //     added by the single wave that sees tile (0, 0).
 // Backward (flash_bwd below):
 //   pre : D_i = sum_d dO.O
-//   kv  : per 128-key block (attn_bwd4.hip): recompute S, P; dP = dO.V^T;
+//   kv  : per 128-key block (attn_bwd3.hip): recompute S, P; dP = dO.V^T;
 //         dS = P (dP - D) scale; dK, dV accumulated in registers; dS written
-//         once, r-indexed dQR[h][b][i][r = S-1-i+j];
-//   dq  : dq = dQR(j-view) . K + dQR . R (attn_dq.hip);
+//         r-indexed dQR[h][b][i][r = S-1-i+j] and j-indexed dSj[h][b][i][j];
+//   dq  : dq = dSj . K + dQR . R (attn_dq.hip);
 //   GEMM: dR += dQR^T . Q (batched over heads, split-K partials);
 //   fix : meta-block terms (j > i inside the metadata prefix).
 #include "attn_tiles.h"
@@ -255,8 +255,8 @@ __global__ void flash_bwd_meta_kernel(AttnArgs a, const float* __restrict__ meta
 namespace {
 // zero the part of dQR[h][b][i][r] that the consumers read but the key/value
 // pass does not write: r in [S-1-i-DQR_BAND, S-1-i) (below the written band)
-// and the row pad [S, ldr). The dq kernel and the dR product never read further
-// below the band.
+// and the row pad [S, ldr); and the row pad of dSj. The dq kernel and the dR
+// product never read further below the band.
 constexpr int DQR_BAND = 256;
 // one wave per row; ldr % 8 == 0 (flash_dqr_ld), so the row starts are 16-B
 // aligned: ragged ends with 2-B stores, the body with 16-B stores
@@ -269,7 +269,8 @@ __device__ __forceinline__ void zero_span(bf16* __restrict__ p, int64_t lo, int6
     for (int64_t r = a + 8 * lane; r < e; r += 512) *(u32x4*)(p + r) = z;
 }
 
-__global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, int64_t ldr, int64_t S, int64_t rows) {
+__global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, bf16* __restrict__ dsj, int64_t ldr, int64_t S,
+                                     int64_t rows) {
     const int64_t row = blockIdx.x * 4LL + (threadIdx.x >> 6);  // (h, b, i) flattened
     if (row >= rows) return;
     const int lane = threadIdx.x & 63;
@@ -277,16 +278,16 @@ __global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, int64_t ldr, int64_
     bf16* p = dqr + row * ldr;
     zero_span(p, max<int64_t>(0, S - 1 - i - DQR_BAND), S - 1 - i, lane);
     zero_span(p, S, ldr, lane);
+    zero_span(dsj + row * ldr, S, ldr, lane);
 }
 }  // namespace
 
-// dQR row pitch: >= S + 136 so that the key/value pass's whole-row dS stores
-// of a 128-key block never reach the next row (dQR entries j > i, zeros, fall
-// at r = S-1-i+j in [S, S+127)) and the dq kernel's j-view runs of the first
-// rows of a query tile (r <= S + 133) stay inside the zeroed row padding
-int64_t flash_dqr_ld(int64_t S) { return (S + 136 + 7) / 8 * 8; }
+// dQR / dSj row pitch: >= S + 128 so that the key/value pass's whole-row dS
+// stores of a 128-key block never reach the next row (dQR entries j > i fall
+// at r = S-1-i+j in [S, S+127): padding no reader touches)
+int64_t flash_dqr_ld(int64_t S) { return (S + 128 + 7) / 8 * 8; }
 
-// workspace: dQR bf16 [H][B][S][ldr] | D f32 [B][H][S] | meta_ds f32 [B][H][8][8]
+// workspace: dQR bf16 [H][B][S][ldr] | dSj bf16 [H][B][S][ldr] | D f32 [B][H][S] | meta_ds f32 [B][H][8][8]
 //            | dR split-K partials f32 [ksplit][H][S][HS]
 static size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 static size_t dr_ws_bytes(int64_t B, int64_t S, int64_t H) {
@@ -295,7 +296,7 @@ static size_t dr_ws_bytes(int64_t B, int64_t S, int64_t H) {
 
 size_t flash_bwd_workspace(int64_t B, int64_t S, int64_t H) {
     const int64_t ldr = flash_dqr_ld(S);
-    return align256((size_t)H * B * S * ldr * 2) + align256((size_t)B * H * S * 4) +
+    return 2 * align256((size_t)H * B * S * ldr * 2) + align256((size_t)B * H * S * 4) +
            align256((size_t)B * H * 64 * 4) + align256(dr_ws_bytes(B, S, H));
 }
 
@@ -311,6 +312,8 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     char* p = (char*)ws;
     bf16* dqr = (bf16*)p;
     p += align256((size_t)H * B * S * ldr * 2);
+    bf16* dsj = (bf16*)p;
+    p += align256((size_t)H * B * S * ldr * 2);
     float* Dv = (float*)p;
     p += align256((size_t)B * H * S * 4);
     float* meta_ds = (float*)p;
@@ -321,8 +324,8 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     // (their dS entries there are 0 by the mask), so a workspace that already
     // served this (B, S, H) keeps them (ws_ready)
     if (!ws_ready)
-        hipLaunchKernelGGL(dqr_band_zero_kernel, dim3((unsigned)((H * B * S + 3) / 4)), dim3(256), 0, s, dqr, ldr, S,
-                           H * B * S);
+        hipLaunchKernelGGL(dqr_band_zero_kernel, dim3((unsigned)((H * B * S + 3) / 4)), dim3(256), 0, s, dqr, dsj, ldr,
+                           S, H * B * S);
     hipMemsetAsync(meta_ds, 0, (size_t)B * H * 64 * 4, s);
     if (ldo % 8 == 0 && ((uintptr_t)dout % 16) == 0 && ((uintptr_t)out % 16) == 0)
         hipLaunchKernelGGL(flash_bwd_pre_vec_kernel, dim3((unsigned)((B * S * H + 15) / 16)), dim3(256), 0, s, a, dout,
@@ -330,12 +333,18 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     else
         hipLaunchKernelGGL(flash_bwd_pre_kernel, dim3((unsigned)((B * S * H + 3) / 4)), dim3(256), 0, s, a, dout, ldo,
                            out, Dv);
-    // key/value pass: dK, dV, and dS (r-indexed, once)
-    if (S * ldr * 2 >= 0xFFFF0000LL ||
-        flash_bwd_kv4(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, ldr, meta_ds, s))
+    // key/value pass: dK, dV, and dS in both layouts (v4; MSQ_ATTN_BWD_KV=3
+    // selects the v3 pass, kept for A/B measurements)
+    static const bool use_v3 = [] {
+        const char* e = getenv("MSQ_ATTN_BWD_KV");
+        return e && e[0] == '3';
+    }();
+    const int kv_rc = use_v3 ? flash_bwd_kv3(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s)
+                             : flash_bwd_kv4(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s);
+    if (kv_rc)
         return msq_set_error(MSQ_ERR_UNSUPPORTED, "flash_bwd: shape outside the key/value pass (n_meta > 8 or > 4 GB)");
-    // dq (bf16, q columns of dqkv) = dQR(j-view) . K + dQR . R
-    flash_bwd_dq(a, dqr, ldr, dqkv, ldd, s);
+    // dq (bf16, q columns of dqkv) = dSj . K + dQR . R
+    flash_bwd_dq(a, dsj, dqr, ldr, dqkv, ldd, s);
     // dR[h][r] += sum_{b,i} dQR[h][b,i][r] q_{b,i}   (batched over heads; per batch
     // segment only i >= S-1-r contributes: tri 2, split over segments)
     // (a strided-batched hipBLASLt product over the whole K range, 2x the

@@ -55,13 +55,18 @@ class _CallLog:
     def __init__(self, n=12):
         self.names, self.n = [], n
 
-    trace = bool(os.environ.get("MSQ_TRACE_CALLS"))  # diagnostics: synchronise after every launch
+    path = os.environ.get("MSQ_TRACE_CALLS")  # diagnostics: a file; synchronise after every launch
 
     def __call__(self, name, args, launch):
         self.names = (self.names + [name])[-self.n:]
+        if self.path:
+            with open(f"{self.path}.{os.environ.get('RANK')}", "a") as f:
+                f.write(name + " " + " ".join(str(getattr(x, "value", x)) for x in args[:12]) + "\n")
         r = launch()
-        if self.trace:
+        if self.path:
             torch.cuda.synchronize()
+            with open(f"{self.path}.{os.environ.get('RANK')}", "a") as f:
+                f.write("  ok\n")
         return r
 
 
