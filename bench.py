@@ -63,9 +63,10 @@ def flops_per_token(cfg, T):
 
 
 def _gemm_class(a):
-    """msq_gemm / msq_gemm_ex / msq_gemm_dropout args -> (class, FLOPs)."""
+    """msq_gemm / msq_gemm_ex / msq_gemm_dropout args -> (class, FLOPs); the
+    dX products are labelled by their caller (ops.gemm(role="gemm_dX"))."""
     ta, tb, M, N, K, batch, epi = a[1], a[2], a[3], a[4], a[5], a[16], a[17]
-    cls = "gemm_dW" if epi == L.EPI_ACCUM else ("gemm_dX" if (tb and not ta) else "gemm_fwd")
+    cls = "gemm_dW" if epi == L.EPI_ACCUM else (L.ROLE or ("gemm_dX" if (tb and not ta) else "gemm_fwd"))
     return cls, 2.0 * M * N * K * batch, None
 
 

@@ -45,7 +45,8 @@ SIGNATURES = {
     "msq_window_gather": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _p, _i64, _i64, _i, _p, _p]),
     "msq_midi_decode": (_i, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "msq_relattn_decode": (_i, [_i, _p, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
-                                _f, _p]),
+                                _f, _p, _sz, _p]),
+    "msq_relattn_decode_workspace": (_sz, [_i64, _i64, _i64]),
     "msq_midi_encode": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _p, _i64, _p, _p, _p, _p, _p]),
     "msq_dropout_attn_mask": (_i, [_p, _p, _i64, _i64, _i64, _u32, _u32, _f, _p]),
     "msq_relattn_fwd_dropout": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64, _p, _p,
@@ -68,7 +69,7 @@ SIGNATURES = {
     "msq_gemm_set_route": (_i, [_i]),
     "msq_ring_step": (_i, [_p, _p, _p, _i, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p]),
     "msq_relattn_decode_pos": (_i, [_i, _p, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _f,
-                                    _p]),
+                                    _p, _sz, _p]),
     "msq_ring_lse": (_i, [_p, _p, _p, _i, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p]),
     "msq_filtered_ce_bias": (_i, [_p, _p, _i64, _p, _p, _i, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
                                   _f, _p, _p, _p]),
@@ -116,8 +117,10 @@ def lib():
 
 
 # optional launch observer (bench.py's per-class HIP-event timing):
-# TAP(name, args, launch) must call launch() and return its result
+# TAP(name, args, launch) must call launch() and return its result; ROLE is
+# the caller's label of the launch in flight (ops.gemm(role=...)), or None
 TAP = None
+ROLE = None
 
 
 def call(name, *args):

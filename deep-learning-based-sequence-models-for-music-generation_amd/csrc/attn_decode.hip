@@ -11,157 +11,125 @@
 // n_meta + first_mod, so slot s (>= n_meta) is window position
 // n_meta + (s - n_meta - first_mod) mod ctx.
 //
-// Memory-bound (per (b, h): K, V of S keys from HBM, R rows from L2/MALL,
-// ~1.5 KB of loads per key against 3 x 256 FLOP): one workgroup of 4 waves per
-// (b, h); scores with the key on the thread (16-B row loads, q from LDS), a
-// workgroup softmax, then P.V with the dimension on the lane (coalesced 256-B
-// V rows, one wave per key residue class) and a 4-wave combine. The new
-// token's k / v come from the QKV row (and are written to its slot here).
+// HBM-bound (per (b, h) the K and V rows of S keys, 2 x 256 B each at hs 128;
+// the R rows are shared by every b and come from L2 / MALL). Split over the
+// keys (flash decoding): one workgroup per (128-key chunk, h, b), i.e. ~8.7k
+// workgroups at B 64, H 8, ctx 2048 instead of 512 — every K, R and V row of
+// the chunk is requested up front (24 16-B loads per lane in flight), then
+// scores, a chunk-local softmax (max m, sum l) and the unnormalised P.V go to
+// a workspace partial; decode_combine_kernel merges a (b, h)'s chunks.
+// A key row (hs <= 128 values) is spread over a 16-lane group, 8 values per
+// lane, so one wave load instruction covers 4 consecutive rows (1 KB).
 #include "common.h"
 
 namespace {
 
-constexpr int NT = 256, HS = 128, MAXS = 4096;
+constexpr int NT = 256, HS = 128, MAXS = 4096, CH = 128, NSTEP = CH / 16;
 
-// dot of 8 consecutive elements with q (fp32 in LDS)
-__device__ __forceinline__ float dot8(const bf16* p, const float* q) {
-    const bf16x8 a = *(const bf16x8*)p;
-    float s = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s = fmaf((float)a[e], q[e], s);
-    return s;
-}
-__device__ __forceinline__ float dot8(const float* p, const float* q) {
-    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
-    float s = 0.f;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) s = fmaf(a[e], q[e], s);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) s = fmaf(b[e], q[4 + e], s);
-    return s;
-}
-__device__ __forceinline__ void copy8(bf16* d, const bf16* s) { *(bf16x8*)d = *(const bf16x8*)s; }
-__device__ __forceinline__ void copy8(float* d, const float* s) {
-    *(f32x4*)d = *(const f32x4*)s;
-    *(f32x4*)(d + 4) = *(const f32x4*)(s + 4);
-}
-__device__ __forceinline__ f32x2 load2(const bf16* p) {
-    const bf16x2 v = *(const bf16x2*)p;
-    return (f32x2){(float)v[0], (float)v[1]};
-}
-__device__ __forceinline__ f32x2 load2(const float* p) { return *(const f32x2*)p; }
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+template <typename T> struct RowT;
+template <> struct RowT<bf16> { typedef bf16x8 type; };
+template <> struct RowT<float> { typedef f32x8 type; };
 
-__device__ __forceinline__ void load8(const bf16* p, float (&x)[8]) {
-    const bf16x8 a = *(const bf16x8*)p;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) x[e] = (float)a[e];
-}
-__device__ __forceinline__ void load8(const float* p, float (&x)[8]) {
-    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) x[e] = a[e], x[4 + e] = b[e];
-}
-
-// T = bf16 (the MFMA engine) or float (the exact fp32 engine). A key's row
-// (hs <= 128 values) is spread over a 16-lane group, 8 values per lane, so a
-// wave reads 4 whole rows per load instruction (coalesced) and keeps 4 row
-// loads of every kind in flight per unrolled step.
 template <typename T>
-__global__ __launch_bounds__(NT) void relattn_decode_kernel(T* __restrict__ out, int64_t ldo,
-                                                            const T* __restrict__ qkv, int64_t ldq,
-                                                            T* __restrict__ kc, T* __restrict__ vc,
-                                                            const T* __restrict__ R, int64_t S_max, int H,
-                                                            int S_ring, int n_meta, int n_tok, int new_slot,
-                                                            int first_mod, float scale, int hs,
-                                                            const int64_t* __restrict__ posp) {
-    __shared__ float q_s[HS];
-    __shared__ float p_s[MAXS];
-    __shared__ float red[NT / 64];
-    __shared__ float part[4][HS];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int l16 = lane & 15, grp = w * 4 + (lane >> 4);  // 16 key groups per block
-    const int h = blockIdx.x, b = blockIdx.y;
-    const int ctx = S_ring - n_meta;
-    if (posp) {  // the step's position from device memory (graph-replayed steps)
+__device__ __forceinline__ typename RowT<T>::type ld_row(const T* p) { return *(const typename RowT<T>::type*)p; }
+__device__ __forceinline__ void copy8(bf16* d, const bf16* s) { *(bf16x8*)d = *(const bf16x8*)s; }
+__device__ __forceinline__ void copy8(float* d, const float* s) { *(f32x8*)d = *(const f32x8*)s; }
+
+struct Pos {
+    int n_tok, new_slot, first_mod;
+};
+// the step's window from device memory (graph-replayed steps) or the host arguments
+__device__ __forceinline__ Pos window_pos(const int64_t* posp, int ctx, int n_meta, int n_tok, int new_slot,
+                                          int first_mod) {
+    if (posp) {
         const int64_t pos = *posp;
         n_tok = (int)min<int64_t>(pos + 1, ctx);
         new_slot = n_meta + (int)(pos % ctx);
         first_mod = (int)((pos + 1 - n_tok) % ctx);
     }
-    const int S = n_meta + n_tok;
-    const T* qrow = qkv + (int64_t)b * ldq + (int64_t)h * hs;
+    return {n_tok, new_slot, first_mod};
+}
+
+struct DecArgs {
+    int64_t ldq, S_max;
+    int H, S_ring, n_meta, n_tok, new_slot, first_mod, hs, nsplit;
+    float scale;
+    const int64_t* posp;
+};
+
+template <typename T>
+__global__ __launch_bounds__(NT) void relattn_decode_part_kernel(DecArgs a, const T* __restrict__ qkv,
+                                                                 T* __restrict__ kc, T* __restrict__ vc,
+                                                                 const T* __restrict__ R, float* __restrict__ po,
+                                                                 float* __restrict__ pml) {
+    __shared__ float part[4][HS];
+    __shared__ float wm[4], wl[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int l16 = lane & 15, grp = w * 4 + (lane >> 4);  // 16 key groups per workgroup
+    const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int H = a.H, hs = a.hs, n_meta = a.n_meta, ctx = a.S_ring - n_meta;
+    const Pos p = window_pos(a.posp, ctx, n_meta, a.n_tok, a.new_slot, a.first_mod);
+    const int S = n_meta + p.n_tok, s0 = c * CH;
+    if (s0 >= S) return;  // chunk past the window (uniform over the workgroup)
+    const T* qrow = qkv + (int64_t)b * a.ldq + (int64_t)h * hs;
     const T* knew = qrow + (int64_t)H * hs;
     const T* vnew = knew + (int64_t)H * hs;
-    T* kcb = kc + ((int64_t)b * H + h) * S_ring * hs;
-    T* vcb = vc + ((int64_t)b * H + h) * S_ring * hs;
-    const T* Rh = R + (int64_t)h * S_max * hs;
-    if (tid < hs) q_s[tid] = (float)qrow[tid];
-    // the new token's key / value into its slot (read back below from qkv)
-    if (tid < hs / 8) {
-        copy8(kcb + (int64_t)new_slot * hs + tid * 8, knew + tid * 8);
-        copy8(vcb + (int64_t)new_slot * hs + tid * 8, vnew + tid * 8);
+    T* kcb = kc + ((int64_t)b * H + h) * a.S_ring * hs;
+    T* vcb = vc + ((int64_t)b * H + h) * a.S_ring * hs;
+    const T* Rh = R + (int64_t)h * a.S_max * hs;
+    // the new token's key / value into its slot (this chunk reads them from qkv)
+    if (p.new_slot >= s0 && p.new_slot < s0 + CH && tid < hs / 8) {
+        copy8(kcb + (int64_t)p.new_slot * hs + tid * 8, knew + tid * 8);
+        copy8(vcb + (int64_t)p.new_slot * hs + tid * 8, vnew + tid * 8);
     }
-    __syncthreads();
     const int d0 = 8 * l16;
     const bool dok = d0 < hs;
-    float q[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) q[e] = dok ? q_s[d0 + e] : 0.f;
 
-    // scores: group g takes slots g, g + 16, ...; lane l16 the dims 8 l16 ..
-    float mx = -INFINITY;
-#pragma unroll 4
-    for (int s = grp; s < S; s += 16) {
-        const int jw = s < n_meta ? s : n_meta + (s - n_meta - first_mod + ctx) % ctx;
-        const T* kr = s == new_slot ? knew : kcb + (int64_t)s * hs;
-        float kx[8], rx[8];
-        if (dok) {
-            load8(kr + d0, kx);
-            load8(Rh + (int64_t)jw * hs + d0, rx);
+    // every row of the chunk requested before any is used
+    typename RowT<T>::type kx[NSTEP], rx[NSTEP], vx[NSTEP], qx;
+    if (dok) {
+        qx = ld_row(qrow + d0);
+#pragma unroll
+        for (int st = 0; st < NSTEP; ++st) {
+            const int s = min(s0 + st * 16 + grp, S - 1);  // rows past the window: masked below
+            const int jw = s < n_meta ? s : n_meta + (s - n_meta - p.first_mod + ctx) % ctx;
+            kx[st] = ld_row((s == p.new_slot ? knew : kcb + (int64_t)s * hs) + d0);
+            rx[st] = ld_row(Rh + (int64_t)jw * hs + d0);
+            vx[st] = ld_row((s == p.new_slot ? vnew : vcb + (int64_t)s * hs) + d0);
         }
+    }
+    float sc[NSTEP];
+    float m = -INFINITY;
+#pragma unroll
+    for (int st = 0; st < NSTEP; ++st) {
         float acc = 0.f;
         if (dok) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) acc = fmaf(kx[e] + rx[e], q[e], acc);
+            for (int e = 0; e < 8; ++e) acc = fmaf((float)kx[st][e] + (float)rx[st][e], (float)qx[e], acc);
         }
 #pragma unroll
         for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-        acc *= scale;
-        if (l16 == 0) p_s[s] = acc;
-        mx = fmaxf(mx, acc);
+        sc[st] = s0 + st * 16 + grp < S ? acc * a.scale : -INFINITY;
+        m = fmaxf(m, sc[st]);
     }
-    mx = wave_max(mx);
-    if (lane == 0) red[w] = mx;
-    __syncthreads();
-    mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    __syncthreads();
-    float sum = 0.f;
-    for (int s = tid; s < S; s += NT) {
-        const float p = __expf(p_s[s] - mx);
-        p_s[s] = p;
-        sum += p;
-    }
-    sum = wave_sum(sum);
-    if (lane == 0) red[w] = sum;
-    __syncthreads();
-    const float inv = 1.f / (red[0] + red[1] + red[2] + red[3]);
-
-    // P.V: group g takes slots g, g + 16, ...; lane l16 accumulates dims 8 l16 ..
-    float o[8];
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));  // the wave's max (>= one valid key unless the wave has none)
+    float l = 0.f, o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = 0.f;
-#pragma unroll 4
-    for (int s = grp; s < S; s += 16) {
-        const T* vr = s == new_slot ? vnew : vcb + (int64_t)s * hs;
-        if (dok) {
-            float vx[8];
-            load8(vr + d0, vx);
-            const float p = p_s[s];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = fmaf(p, vx[e], o[e]);
+    for (int st = 0; st < NSTEP; ++st) {
+        const float pe = sc[st] == -INFINITY ? 0.f : __expf(sc[st] - m);
+        l += pe;
+        if (dok) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = fmaf(pe, (float)vx[st][e], o[e]);
         }
     }
-    // the 4 groups of the wave, then the 4 waves
+    // the 4 key groups of the wave (l is uniform inside a group)
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         o[e] += __shfl_xor(o[e], 16, 64);
@@ -171,19 +139,75 @@ __global__ __launch_bounds__(NT) void relattn_decode_kernel(T* __restrict__ out,
 #pragma unroll
         for (int e = 0; e < 8; ++e) part[w][d0 + e] = o[e];
     }
+    if (lane == 0) wm[w] = m, wl[w] = l;
     __syncthreads();
-    if (tid < hs) {
-        const float r = (part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]) * inv;
-        out[(int64_t)b * ldo + (int64_t)h * hs + tid] = (T)r;
+    // the 4 waves (the chunk holds >= 1 valid key, so M is finite)
+    const float M = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+    float f[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = wm[i] == -INFINITY ? 0.f : __expf(wm[i] - M);
+    const int64_t pi = ((int64_t)b * H + h) * a.nsplit + c;
+    if (tid < hs) po[pi * HS + tid] = f[0] * part[0][tid] + f[1] * part[1][tid] + f[2] * part[2][tid] + f[3] * part[3][tid];
+    if (tid == 0) {
+        pml[2 * pi] = M;
+        pml[2 * pi + 1] = f[0] * wl[0] + f[1] * wl[1] + f[2] * wl[2] + f[3] * wl[3];
     }
+}
+
+// out[b, h] = sum_c e^(m_c - M) o_c / sum_c e^(m_c - M) l_c over the chunks of the window
+template <typename T>
+__global__ __launch_bounds__(HS) void decode_combine_kernel(DecArgs a, T* __restrict__ out, int64_t ldo,
+                                                            const float* __restrict__ po,
+                                                            const float* __restrict__ pml) {
+    const int tid = threadIdx.x, h = blockIdx.x, b = blockIdx.y;
+    const int ctx = a.S_ring - a.n_meta;
+    const Pos p = window_pos(a.posp, ctx, a.n_meta, a.n_tok, a.new_slot, a.first_mod);
+    const int nc = (a.n_meta + p.n_tok + CH - 1) / CH;
+    const int64_t base = ((int64_t)b * a.H + h) * a.nsplit;
+    float M = -INFINITY;
+    for (int c = 0; c < nc; ++c) M = fmaxf(M, pml[2 * (base + c)]);
+    float L = 0.f, acc = 0.f;
+    for (int c = 0; c < nc; ++c) {
+        const float f = __expf(pml[2 * (base + c)] - M);
+        L = fmaf(f, pml[2 * (base + c) + 1], L);
+        if (tid < a.hs) acc = fmaf(f, po[(base + c) * HS + tid], acc);
+    }
+    if (tid < a.hs) out[(int64_t)b * ldo + (int64_t)h * a.hs + tid] = (T)(acc / L);
+}
+
+int64_t n_split(int64_t S_ring) { return (S_ring + CH - 1) / CH; }
+
+int launch(int dtype, void* out, int64_t ldo, const void* qkv, void* kcache, void* vcache, const void* R, int64_t B,
+           const DecArgs& a, void* ws, size_t ws_bytes, hipStream_t s) {
+    const size_t need = msq_relattn_decode_workspace(B, a.H, a.S_ring);
+    MSQ_CHECK_ARG(ws && ws_bytes >= need && ((uintptr_t)ws & 15) == 0,
+                  "msq_relattn_decode: workspace of %zu bytes (16-B aligned) needed, %zu given", need, ws_bytes);
+    float* po = (float*)ws;
+    float* pml = po + B * a.H * a.nsplit * HS;
+    const dim3 grid((unsigned)a.nsplit, (unsigned)a.H, (unsigned)B), cgrid((unsigned)a.H, (unsigned)B);
+    if (dtype == MSQ_BF16) {
+        hipLaunchKernelGGL(relattn_decode_part_kernel<bf16>, grid, dim3(NT), 0, s, a, (const bf16*)qkv, (bf16*)kcache,
+                           (bf16*)vcache, (const bf16*)R, po, pml);
+        hipLaunchKernelGGL(decode_combine_kernel<bf16>, cgrid, dim3(HS), 0, s, a, (bf16*)out, ldo, po, pml);
+    } else {
+        hipLaunchKernelGGL(relattn_decode_part_kernel<float>, grid, dim3(NT), 0, s, a, (const float*)qkv,
+                           (float*)kcache, (float*)vcache, (const float*)R, po, pml);
+        hipLaunchKernelGGL(decode_combine_kernel<float>, cgrid, dim3(HS), 0, s, a, (float*)out, ldo, po, pml);
+    }
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
 }
 
 }  // namespace
 
+extern "C" size_t msq_relattn_decode_workspace(int64_t B, int64_t H, int64_t S_ring) {
+    return (size_t)(B * H * n_split(S_ring)) * (HS + 2) * sizeof(float);
+}
+
 extern "C" int msq_relattn_decode(int dtype, void* out, int64_t ldo, const void* qkv, int64_t ldq, void* kcache, void* vcache,
                                   const void* R, int64_t S_max, int64_t B, int64_t H, int64_t hs, int64_t S_ring,
                                   int64_t n_meta, int64_t n_tok, int64_t new_slot, int64_t first_mod, float scale,
-                                  void* stream) {
+                                  void* ws, size_t ws_bytes, void* stream) {
     MSQ_CHECK_ARG(out && qkv && kcache && vcache && R, "msq_relattn_decode: null pointer");
     MSQ_CHECK_ARG(hs > 0 && hs <= HS && hs % 8 == 0, "msq_relattn_decode: head size %lld (8 | hs <= 128)",
                   (long long)hs);
@@ -195,17 +219,9 @@ extern "C" int msq_relattn_decode(int dtype, void* out, int64_t ldo, const void*
                   "msq_relattn_decode: bad slot");
     MSQ_CHECK_ARG(ldq >= 3 * H * hs && ldo >= H * hs, "msq_relattn_decode: bad leading dims");
     MSQ_CHECK_ARG(dtype == MSQ_BF16 || dtype == MSQ_F32, "msq_relattn_decode: dtype %d", dtype);
-    const dim3 grid((unsigned)H, (unsigned)B);
-    if (dtype == MSQ_BF16)
-        hipLaunchKernelGGL(relattn_decode_kernel<bf16>, grid, dim3(NT), 0, (hipStream_t)stream, (bf16*)out, ldo,
-                           (const bf16*)qkv, ldq, (bf16*)kcache, (bf16*)vcache, (const bf16*)R, S_max, (int)H,
-                           (int)S_ring, (int)n_meta, (int)n_tok, (int)new_slot, (int)first_mod, scale, (int)hs, nullptr);
-    else
-        hipLaunchKernelGGL(relattn_decode_kernel<float>, grid, dim3(NT), 0, (hipStream_t)stream, (float*)out, ldo,
-                           (const float*)qkv, ldq, (float*)kcache, (float*)vcache, (const float*)R, S_max, (int)H,
-                           (int)S_ring, (int)n_meta, (int)n_tok, (int)new_slot, (int)first_mod, scale, (int)hs, nullptr);
-    MSQ_LAUNCH_CHECK();
-    return MSQ_OK;
+    const DecArgs a{ldq, S_max, (int)H, (int)S_ring, (int)n_meta, (int)n_tok, (int)new_slot, (int)first_mod, (int)hs,
+                    (int)n_split(S_ring), scale, nullptr};
+    return launch(dtype, out, ldo, qkv, kcache, vcache, R, B, a, ws, ws_bytes, (hipStream_t)stream);
 }
 
 // msq_relattn_decode with the step's position read from device memory: n_tok =
@@ -214,7 +230,8 @@ extern "C" int msq_relattn_decode(int dtype, void* out, int64_t ldo, const void*
 // decode step replays unchanged from step to step.
 extern "C" int msq_relattn_decode_pos(int dtype, void* out, int64_t ldo, const void* qkv, int64_t ldq, void* kcache,
                                       void* vcache, const void* R, int64_t S_max, int64_t B, int64_t H, int64_t hs,
-                                      int64_t S_ring, int64_t n_meta, const int64_t* pos, float scale, void* stream) {
+                                      int64_t S_ring, int64_t n_meta, const int64_t* pos, float scale, void* ws,
+                                      size_t ws_bytes, void* stream) {
     MSQ_CHECK_ARG(out && qkv && kcache && vcache && R && pos, "msq_relattn_decode_pos: null pointer");
     MSQ_CHECK_ARG(hs > 0 && hs <= HS && hs % 8 == 0, "msq_relattn_decode_pos: head size %lld (8 | hs <= 128)",
                   (long long)hs);
@@ -222,15 +239,7 @@ extern "C" int msq_relattn_decode_pos(int dtype, void* out, int64_t ldo, const v
                   "msq_relattn_decode_pos: bad sizes");
     MSQ_CHECK_ARG(ldq >= 3 * H * hs && ldo >= H * hs, "msq_relattn_decode_pos: bad leading dims");
     MSQ_CHECK_ARG(dtype == MSQ_BF16 || dtype == MSQ_F32, "msq_relattn_decode_pos: dtype %d", dtype);
-    const dim3 grid((unsigned)H, (unsigned)B);
-    if (dtype == MSQ_BF16)
-        hipLaunchKernelGGL(relattn_decode_kernel<bf16>, grid, dim3(NT), 0, (hipStream_t)stream, (bf16*)out, ldo,
-                           (const bf16*)qkv, ldq, (bf16*)kcache, (bf16*)vcache, (const bf16*)R, S_max, (int)H,
-                           (int)S_ring, (int)n_meta, 1, (int)n_meta, 0, scale, (int)hs, pos);
-    else
-        hipLaunchKernelGGL(relattn_decode_kernel<float>, grid, dim3(NT), 0, (hipStream_t)stream, (float*)out, ldo,
-                           (const float*)qkv, ldq, (float*)kcache, (float*)vcache, (const float*)R, S_max, (int)H,
-                           (int)S_ring, (int)n_meta, 1, (int)n_meta, 0, scale, (int)hs, pos);
-    MSQ_LAUNCH_CHECK();
-    return MSQ_OK;
+    const DecArgs a{ldq, S_max, (int)H, (int)S_ring, (int)n_meta, 1, (int)n_meta, 0, (int)hs,
+                    (int)n_split(S_ring), scale, pos};
+    return launch(dtype, out, ldo, qkv, kcache, vcache, R, B, a, ws, ws_bytes, (hipStream_t)stream);
 }

@@ -123,7 +123,11 @@ bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dt
 bool gemm256p_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s);
 // skinny-M weight-streaming kernel of the decode steps (gemm_skinny.hip):
 // false when the problem is not M <= 64 / ta = tb = 0 / a forward epilogue
-bool gemm_skinny_launch(const GemmArgs& g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s);
+bool gemm_skinny_launch(const GemmArgs& g, int ta, int tb, int epi, int c_dtype, int aux_dtype, size_t ws_bytes,
+                        hipStream_t s);
+// K slices of a split-K skinny product (1: none) and the fp32 partial bytes it needs in ws
+int skinny_ksplit(int64_t M, int64_t N, int64_t K, int64_t* kper);
+size_t skinny_ws_bytes(int64_t M, int64_t N, int64_t K);
 // 256 tile with the column sums of C (epilogue NONE / RELU_MASK, C bf16,
 // N % 4 == 0): dbias[n] (+)= sum_m C[m][n] (fp32, before C's rounding);
 // ws >= gemm256_colsum_ws_bytes(M, N); false when the 256 tile does not apply

@@ -541,6 +541,7 @@ extern "C" int64_t msq_gemm_workspace_size(int dtype, int ta, int tb, int64_t M,
                                            int64_t lda, int64_t ldb, int64_t batch, int epilogue) {
     if (dtype != MSQ_BF16 || M <= 0 || N <= 0 || K <= 0 || batch <= 0) return 0;
     if (epilogue != MSQ_EPI_ACCUM) {  // the split-K tail of a wave-quantisation split
+        if (M <= 64 && !ta && !tb && batch == 1) return (int64_t)skinny_ws_bytes(M, N, K);  // skinny split-K
         if (batch != 1 || M % 256 == 0 || M <= 256 || M <= 64) return 0;
         const TailPlan tp = plan_tail(M % 256, N, K);
         return tp.ksplit > 1 ? (int64_t)(tp.tmp_bytes + tp.part_bytes) : 0;
@@ -613,7 +614,7 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
     g.ws = (float*)ws;
     hipStream_t s = (hipStream_t)stream;
     if (dtype == MSQ_BF16 && M <= 64 && !getenv("MSQ_GEMM_NOSKINNY") &&
-        gemm_skinny_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, s)) {
+        gemm_skinny_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, (size_t)ws_bytes, s)) {
         MSQ_LAUNCH_CHECK();
         return MSQ_OK;
     }

@@ -12,7 +12,8 @@
 //   * MFMA roles: W rows are the MFMA A-operand (output rows), activation rows
 //     the B-operand, so a lane ends with C[m][n..n+3] (4 consecutive n of one
 //     row m), the layout epi_apply takes.
-// Bound: HBM bytes of W (2 N K) per launch; grid = N / 16 blocks.
+// Bound: HBM bytes of W (2 N K) per launch; grid = N / 16 blocks (x K slices
+// when N / 16 alone would leave most CUs idle, skinny_ksplit).
 #include "gemm.h"
 
 #include <algorithm>
@@ -22,15 +23,17 @@ namespace {
 
 constexpr int SK_WAVES = 16, SK_U = 4;
 
-template <int EPI, typename TC, typename TX, int MT>
+template <int EPI, typename TC, typename TX, int MT, bool PART>
 __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(GemmArgs g) {
     __shared__ f32x4 red[SK_WAVES - 1][MT][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t n0 = (int64_t)blockIdx.x * 16;
     const bf16* W = (const bf16*)g.B;
     const bf16* A = (const bf16*)g.A;
-    const int64_t kper = (g.K + SK_WAVES * 32 - 1) / (SK_WAVES * 32) * 32;
-    const int64_t kb = w * kper, ke = min<int64_t>(g.K, kb + kper);
+    // PART: K slice blockIdx.y of g.kper (split-K over workgroups, fp32 partials to g.ws)
+    const int64_t k0 = PART ? (int64_t)blockIdx.y * g.kper : 0, k1 = PART ? min<int64_t>(g.K, k0 + g.kper) : g.K;
+    const int64_t kper = (k1 - k0 + SK_WAVES * 32 - 1) / (SK_WAVES * 32) * 32;
+    const int64_t kb = k0 + w * kper, ke = min<int64_t>(k1, kb + kper);
     const int64_t wn = n0 + (lane & 15);
     const bool wok = wn < g.N;
     const bf16* wrow = W + (wok ? wn : 0) * g.ldb;
@@ -76,8 +79,22 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(GemmArgs g) 
 #pragma unroll
         for (int q = 0; q < SK_WAVES - 1; ++q) v += red[q][mt][lane];
         const int64_t m = mt * 16 + (lane & 15), n = n0 + 4 * (lane >> 4);
-        if (m < g.M && n < g.N) epi_apply<EPI, TC, TX>(g, C, X, m, n, v);
+        if (m < g.M && n < g.N) {
+            if (PART) store4(g.ws + ((int64_t)blockIdx.y * g.M + m) * g.N + n, v);  // N % 4 == 0
+            else epi_apply<EPI, TC, TX>(g, C, X, m, n, v);
+        }
     }
+}
+
+// C = epi(sum_s ws[s]) of a split-K skinny product (fixed summation order)
+template <int EPI, typename TC, typename TX>
+__global__ __launch_bounds__(256) void skinny_reduce_kernel(GemmArgs g, int ks) {
+    const int64_t nq = g.N / 4, e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= g.M * nq) return;
+    const int64_t m = e / nq, n = (e - m * nq) * 4, MN = g.M * g.N;
+    f32x4 v = load4(g.ws + m * g.N + n);
+    for (int s = 1; s < ks; ++s) v += load4(g.ws + s * MN + m * g.N + n);
+    epi_apply<EPI, TC, TX>(g, (TC*)g.C, (const TX*)g.aux, m, n, v);
 }
 
 // Persistent variant for K <= SK_WAVES * 2 * 32 = 1024: a wave's K slice of
@@ -156,8 +173,17 @@ void launch_pk(const GemmArgs& g, hipStream_t s) {
     else hipLaunchKernelGGL((gemm_skinny_pk_kernel<EPI, TC, TX, MT, 2>), grid, dim3(64 * SK_WAVES), 0, s, g, ntiles);
 }
 
+template <int EPI, typename TC, typename TX, bool PART>
+void launch_plain(const GemmArgs& g, int mt, int ks, hipStream_t s) {
+    const dim3 grid((unsigned)((g.N + 15) / 16), (unsigned)ks);
+    if (mt == 1) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TC, TX, 1, PART>), grid, dim3(64 * SK_WAVES), 0, s, g);
+    else if (mt == 2) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TC, TX, 2, PART>), grid, dim3(64 * SK_WAVES), 0, s, g);
+    else if (mt == 3) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TC, TX, 3, PART>), grid, dim3(64 * SK_WAVES), 0, s, g);
+    else hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TC, TX, 4, PART>), grid, dim3(64 * SK_WAVES), 0, s, g);
+}
+
 template <int EPI, typename TC, typename TX>
-void launch_mt(const GemmArgs& g, hipStream_t s) {
+void launch_mt(GemmArgs g, size_t ws_bytes, hipStream_t s) {
     const int mt = (int)((g.M + 15) / 16);
     if (g.K <= SK_WAVES * 2 * 32 && !getenv("MSQ_SKINNY_NOPK")) {
         if (mt == 1) launch_pk<EPI, TC, TX, 1>(g, s);
@@ -166,22 +192,27 @@ void launch_mt(const GemmArgs& g, hipStream_t s) {
         else launch_pk<EPI, TC, TX, 4>(g, s);
         return;
     }
-    const dim3 grid((unsigned)((g.N + 15) / 16));
-    if (mt == 1) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TC, TX, 1>), grid, dim3(64 * SK_WAVES), 0, s, g);
-    else if (mt == 2) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TC, TX, 2>), grid, dim3(64 * SK_WAVES), 0, s, g);
-    else if (mt == 3) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TC, TX, 3>), grid, dim3(64 * SK_WAVES), 0, s, g);
-    else hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TC, TX, 4>), grid, dim3(64 * SK_WAVES), 0, s, g);
+    int64_t kper;
+    const int ks = skinny_ksplit(g.M, g.N, g.K, &kper);
+    if (ks > 1 && g.ws && ws_bytes >= skinny_ws_bytes(g.M, g.N, g.K)) {
+        g.kper = kper;
+        launch_plain<EPI, TC, TX, true>(g, mt, ks, s);
+        hipLaunchKernelGGL((skinny_reduce_kernel<EPI, TC, TX>), dim3((unsigned)((g.M * (g.N / 4) + 255) / 256)),
+                           dim3(256), 0, s, g, ks);
+        return;
+    }
+    launch_plain<EPI, TC, TX, false>(g, mt, 1, s);
 }
 
 template <typename TC>
-bool launch_epi(const GemmArgs& g, int epi, int aux_dtype, hipStream_t s) {
+bool launch_epi(const GemmArgs& g, int epi, int aux_dtype, size_t wsb, hipStream_t s) {
     switch (epi) {
-        case MSQ_EPI_NONE: launch_mt<MSQ_EPI_NONE, TC, float>(g, s); return true;
-        case MSQ_EPI_BIAS: launch_mt<MSQ_EPI_BIAS, TC, float>(g, s); return true;
-        case MSQ_EPI_BIAS_RELU: launch_mt<MSQ_EPI_BIAS_RELU, TC, float>(g, s); return true;
+        case MSQ_EPI_NONE: launch_mt<MSQ_EPI_NONE, TC, float>(g, wsb, s); return true;
+        case MSQ_EPI_BIAS: launch_mt<MSQ_EPI_BIAS, TC, float>(g, wsb, s); return true;
+        case MSQ_EPI_BIAS_RELU: launch_mt<MSQ_EPI_BIAS_RELU, TC, float>(g, wsb, s); return true;
         case MSQ_EPI_BIAS_RESID:
-            if (aux_dtype == MSQ_BF16) launch_mt<MSQ_EPI_BIAS_RESID, TC, bf16>(g, s);
-            else launch_mt<MSQ_EPI_BIAS_RESID, TC, float>(g, s);
+            if (aux_dtype == MSQ_BF16) launch_mt<MSQ_EPI_BIAS_RESID, TC, bf16>(g, wsb, s);
+            else launch_mt<MSQ_EPI_BIAS_RESID, TC, float>(g, wsb, s);
             return true;
         default: return false;  // ACCUM / RELU_MASK / dropout: not decode shapes
     }
@@ -189,11 +220,32 @@ bool launch_epi(const GemmArgs& g, int epi, int aux_dtype, hipStream_t s) {
 
 }  // namespace
 
+// split-K of a skinny product whose K > 1024 (the per-slice kernel, not the
+// persistent one) and whose 16-row W slices alone would leave most CUs idle
+// (the decode FFN2, N 1024 x K 4096: 64 slices -> 4 K slices of 1024 each)
+int skinny_ksplit(int64_t M, int64_t N, int64_t K, int64_t* kper) {
+    const int64_t ntiles = (N + 15) / 16;
+    *kper = K;
+    if (M > 64 || K <= SK_WAVES * 2 * 32 || ntiles >= 128 || N % 4 || getenv("MSQ_SKINNY_NOSPLIT")) return 1;
+    const int64_t want = std::min<int64_t>((256 + ntiles - 1) / ntiles, K / 1024);
+    if (want <= 1) return 1;
+    const int64_t q = SK_WAVES * 32;  // whole k-steps for every wave of a slice
+    *kper = ((K + want - 1) / want + q - 1) / q * q;
+    return (int)((K + *kper - 1) / *kper);
+}
+size_t skinny_ws_bytes(int64_t M, int64_t N, int64_t K) {
+    int64_t kper;
+    const int ks = skinny_ksplit(M, N, K, &kper);
+    return ks > 1 ? (size_t)ks * M * N * 4 : 0;
+}
+
 // M <= 64, A [M][K] and W [N][K] bf16 (ta = tb = 0), one batch; false when
 // the problem is outside these conditions (the caller then uses the tiles)
-bool gemm_skinny_launch(const GemmArgs& g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s) {
+bool gemm_skinny_launch(const GemmArgs& g, int ta, int tb, int epi, int c_dtype, int aux_dtype, size_t ws_bytes,
+                        hipStream_t s) {
     if (ta || tb || g.batch != 1 || g.M > 64 || g.K % 8 || g.lda % 8 || g.ldb % 8) return false;
     if (epi != MSQ_EPI_NONE && epi != MSQ_EPI_BIAS && epi != MSQ_EPI_BIAS_RELU && epi != MSQ_EPI_BIAS_RESID)
         return false;
-    return c_dtype == MSQ_BF16 ? launch_epi<bf16>(g, epi, aux_dtype, s) : launch_epi<float>(g, epi, aux_dtype, s);
+    return c_dtype == MSQ_BF16 ? launch_epi<bf16>(g, epi, aux_dtype, ws_bytes, s)
+                                : launch_epi<float>(g, epi, aux_dtype, ws_bytes, s);
 }

@@ -133,14 +133,37 @@ def generate(model, context_len, token_ids, meta_ids, num_tokens=1000, device="c
     cache = None
     ldz = (V + 3) // 4 * 4
     z = torch.empty(B, 1, ldz, device=dev, dtype=torch.float32)
+    # host <-> device staging of the per-step host work (pinned: the copies
+    # stay asynchronous and ordered on their streams)
+    kt_host = torch.empty(B, dtype=torch.int32, pin_memory=True)
+    kt = torch.empty(B, dtype=torch.int32, device=dev)
+    u_host = torch.empty(nrow, dtype=torch.float32, pin_memory=True)
+    u_dev = torch.empty(nrow, dtype=torch.float32, device=dev)
+    # Cached steps are pipelined (unsharded): the sampled tokens of step s go
+    # to the host on a side stream while step s+1's recurrent / cached forward
+    # (which reads them on the device) already runs, so the host-side k choice
+    # (Python's random, as in the reference) overlaps the device work instead
+    # of following it
+    pipelined = shard is None
+    tok_host = torch.empty(B, dtype=torch.int64, pin_memory=True)
+    side = torch.cuda.Stream(device=dev) if pipelined else None
+    prefetched = False
+
+    def cached_at(c):
+        return cached and cache is not None and (c <= context_len or slides)
+
+    def launch_step():
+        # one recurrent position: the token sampled last step (out_tok) at row cur-1
+        lg = eng.step(out_tok, cache)
+        call("msq_filtered_logit_step", ptr(z), ldz, ptr(cache.lse), ptr(lg), dt(lg), lg.stride(0),
+             ptr(out_tok), ptr(wtab), b[0], b[1], b[2], b[3], B, V, stream())
+
     for step in range(num_tokens):
         cur = T0 + step
         W = min(cur, context_len)
-        if cached and cache is not None and (cur <= context_len or slides):
-            # one recurrent position: the token sampled last step (out_tok) at row cur-1
-            logits = eng.step(out_tok, cache)
-            call("msq_filtered_logit_step", ptr(z), ldz, ptr(cache.lse), ptr(logits), dt(logits), logits.stride(0),
-                 ptr(out_tok), ptr(wtab), b[0], b[1], b[2], b[3], B, V, stream())
+        if cached_at(cur):
+            if not prefetched:
+                launch_step()
         else:
             window = hist[:, cur - W:cur].contiguous()
             if cached and cache is None and (cur <= context_len or slides):  # prefill, states left in the cache
@@ -154,9 +177,13 @@ def generate(model, context_len, token_ids, meta_ids, num_tokens=1000, device="c
             ws = workspace(L.lib().msq_filtered_workspace(B, W, V), dev, "loss")
             call("msq_filtered_logit", ptr(z), ldz, ptr(A.logits), dt(A.logits), cfg.v_pad, ptr(window), ptr(wtab),
                  b[0], b[1], b[2], b[3], B, W, V, W - 1, ptr(col_lse), ptr(ws), stream())
+            del logits
+        prefetched = False
         ks = choose_k(last_host, start, rng)
         if uniforms is not None:
-            u = torch.tensor([next(uniforms) for _ in range(nrow)], dtype=torch.float32).to(dev)
+            u_host.numpy()[:] = [next(uniforms) for _ in range(nrow)]
+            u_dev.copy_(u_host, non_blocking=True)
+            u = u_dev
         else:
             if gen is None:
                 # the reference samples with torch.multinomial, i.e. from torch's
@@ -168,11 +195,26 @@ def generate(model, context_len, token_ids, meta_ids, num_tokens=1000, device="c
             u = torch.rand(nrow, device=dev, generator=gen)
         if shard:
             ks, u = ks[shard.lo:shard.hi], u[shard.lo:shard.hi].contiguous()
-        kt = torch.tensor(ks, dtype=torch.int32).to(dev)
+        kt_host.numpy()[:] = ks
+        kt.copy_(kt_host, non_blocking=True)
         call("msq_decode_sample", ptr(hist), ldh, cur, ptr(z), ldz, B, V, ptr(kt), ptr(u), ptr(out_tok),
              start["dyn"], start["length"], start["time"], start["tempo"], stream())
-        # the one device->host sync per step (host-side k choice); sharded: all ranks' rows
-        last_host = shard.gather(out_tok) if shard else out_tok.tolist()
-        del logits
+        # the one device->host transfer per step (host-side k choice); sharded: all ranks' rows
+        if shard:
+            last_host = shard.gather(out_tok)
+            continue
+        main = torch.cuda.current_stream(dev)
+        sampled = torch.cuda.Event()
+        sampled.record(main)
+        side.wait_event(sampled)
+        with torch.cuda.stream(side):
+            tok_host.copy_(out_tok, non_blocking=True)
+            landed = torch.cuda.Event()
+            landed.record(side)
+        if step + 1 < num_tokens and cached_at(cur + 1):
+            launch_step()
+            prefetched = True
+        landed.synchronize()
+        last_host = tok_host.tolist()
     seq = hist[:, :T0 + num_tokens]
     return seq if return_tensor else seq.tolist()

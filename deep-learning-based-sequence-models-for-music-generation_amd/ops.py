@@ -20,9 +20,11 @@ def _mat(t, trans):
 
 
 def gemm(A, B, *, ta=False, tb=False, out=None, out_dtype=None, epilogue=L.EPI_NONE, bias=None, aux=None,
-         drop=None):
+         drop=None, role=None):
     """C = op(A) . op(B).  ta: A stored [K,M]; tb: B stored [K,N] (else [N,K]).
-    drop=(seed, site, p): epilogue BIAS_RESID becomes aux + dropout(acc + bias)."""
+    drop=(seed, site, p): epilogue BIAS_RESID becomes aux + dropout(acc + bias).
+    role: what the product is for (e.g. "gemm_dX"), seen by launch observers
+    (midiseq._lib.TAP, bench.py's per-class timing); no effect on the launch."""
     ar, ac, lda, sA, ba = _mat(A, ta)
     br, bc, ldb, sB, bb = _mat(B, tb)
     M, K = (ac, ar) if ta else (ar, ac)
@@ -48,9 +50,13 @@ def gemm(A, B, *, ta=False, tb=False, out=None, out_dtype=None, epilogue=L.EPI_N
     # split-K partials (weight gradients) / the split-K tail of a wave-quantisation split
     nws = L.lib().msq_gemm_workspace_size(dt(A), int(ta), int(tb), M, N, K, lda, ldb, batch, epilogue)
     ws = _splitk_ws(A.device, nws) if nws > 0 else None
-    call("msq_gemm_ex", dt(A), int(ta), int(tb), M, N, K, ptr(A), lda, sA, ptr(B), ldb, sB, ptr(out), dt(out),
-         ldc, sC, batch, epilogue, ptr(bias), ptr(aux), axd, ldx, sX, seed, site, p, ptr(ws),
-         nws if ws is not None else 0, stream())
+    L.ROLE = role
+    try:
+        call("msq_gemm_ex", dt(A), int(ta), int(tb), M, N, K, ptr(A), lda, sA, ptr(B), ldb, sB, ptr(out), dt(out),
+             ldc, sC, batch, epilogue, ptr(bias), ptr(aux), axd, ldx, sX, seed, site, p, ptr(ws),
+             nws if ws is not None else 0, stream())
+    finally:
+        L.ROLE = None
     return out
 
 

@@ -232,6 +232,9 @@ class TransformerDecodeCache:
         self.nblk = (context + self.RB - 1) // self.RB
         self.part = e(B, self.nblk, cfg.vocab_size, dt=f32)
         self.part_valid = False
+        # partials of the split decode attention (msq_relattn_decode)
+        self.attn_ws = torch.empty(L.lib().msq_relattn_decode_workspace(B, H, self.S_ring), device=device,
+                                   dtype=torch.uint8)
         self.length = 0  # tokens absorbed (sequence positions 0 .. length-1)
         # graph-replayed steps (TransformerEngine.step): the position of the
         # next step on the device (advanced by msq_ring_step), the logits row of
@@ -246,8 +249,8 @@ def dx_gemm(dy, W, Wt, name, out):
     transposed copy Wt[name] (tb = 0) when the engine keeps one (bf16), else
     W itself (tb = 1)."""
     if Wt is not None:
-        return ops.gemm(dy, Wt[name], out=out)
-    return ops.gemm(dy, W[name], tb=True, out=out)
+        return ops.gemm(dy, Wt[name], out=out, role="gemm_dX")
+    return ops.gemm(dy, W[name], tb=True, out=out, role="gemm_dX")
 
 
 class TransformerEngine:
@@ -465,7 +468,7 @@ class TransformerEngine:
         def attn(l):
             call("msq_relattn_decode_pos", dt(cache.qkv), ptr(cache.o), cache.o.stride(0), ptr(cache.qkv),
                  cache.qkv.stride(0), ptr(cache.k[l]), ptr(cache.v[l]), ptr(W[f"{l}.R"]), cfg.s_max, B, H, hs,
-                 cache.S_ring, N_META, ptr(cache.pos_dev), float(scale), s)
+                 cache.S_ring, N_META, ptr(cache.pos_dev), float(scale), ptr(cache.attn_ws), cache.attn_ws.numel(), s)
         self._layers_step(cache.x, cache, attn)
         ops.gemm(cache.f, W["lm_w"], out=cache.row_buf, epilogue=L.EPI_BIAS, bias=P["lm_b"])
         call("msq_ring_step", ptr(cache.lse), ptr(cache.part), ptr(cache.ring), dt(cache.ring), cfg.v_pad, B, cache.ctx,
@@ -487,7 +490,8 @@ class TransformerEngine:
         def attn(l):
             call("msq_relattn_decode", dt(cache.qkv), ptr(cache.o), cache.o.stride(0), ptr(cache.qkv),
                  cache.qkv.stride(0), ptr(cache.k[l]), ptr(cache.v[l]), ptr(W[f"{l}.R"]), cfg.s_max, B, H, hs,
-                 cache.S_ring, N_META, n_tok, N_META + slot, first % ctx, float(scale), s)
+                 cache.S_ring, N_META, n_tok, N_META + slot, first % ctx, float(scale), ptr(cache.attn_ws),
+                 cache.attn_ws.numel(), s)
         self._layers_step(cache.x, cache, attn)
         # the new row goes straight into its ring slot, over the row that leaves
         # the window (or the empty slot); the LSE below leaves that slot out

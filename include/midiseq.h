@@ -389,14 +389,18 @@ int msq_midi_decode(const int64_t* rows, int64_t B, int64_t L, int64_t ld, const
  * MSQ_F32 for every tensor (out [B, ldo] too).                              */
 int msq_relattn_decode(int dtype, void* out, int64_t ldo, const void* qkv, int64_t ldq, void* kcache, void* vcache, const void* R,
                        int64_t S_max, int64_t B, int64_t H, int64_t hs, int64_t S_ring, int64_t n_meta, int64_t n_tok,
-                       int64_t new_slot, int64_t first_mod, float scale, void* stream);
+                       int64_t new_slot, int64_t first_mod, float scale, void* ws, size_t ws_bytes, void* stream);
+/* Bytes of the workspace msq_relattn_decode(_pos) needs (16-B aligned): the
+ * per-(b, h, 128-key chunk) partials of the split (flash-decoding) pass.   */
+size_t msq_relattn_decode_workspace(int64_t B, int64_t H, int64_t S_ring);
 /* msq_relattn_decode with the step's sequence position read from device
  * memory (*pos, int64): n_tok = min(pos + 1, S_ring - n_meta), new_slot =
  * n_meta + pos % ctx, first_mod = (pos + 1 - n_tok) % ctx; for a captured
  * (graph-replayed) decode step whose launch arguments stay fixed.          */
 int msq_relattn_decode_pos(int dtype, void* out, int64_t ldo, const void* qkv, int64_t ldq, void* kcache, void* vcache,
                            const void* R, int64_t S_max, int64_t B, int64_t H, int64_t hs, int64_t S_ring,
-                           int64_t n_meta, const int64_t* pos, float scale, void* stream);
+                           int64_t n_meta, const int64_t* pos, float scale, void* ws, size_t ws_bytes,
+                           void* stream);
 
 /* Note -> token encode of a batch of songs (replaces processing/processing.py
  * :129-152 encode + :111-126 adjust_note_time, the preprocessing step of

@@ -97,11 +97,14 @@ def test_gemm_colsum_bias_grad(M, N, K, epi):
 
 
 @pytest.mark.parametrize("M", [1, 5, 16, 33, 64])
-@pytest.mark.parametrize("N,K", [(17, 64), (1024, 1032), (4384, 1024), (1024, 2048)])
+@pytest.mark.parametrize("N,K", [(17, 64), (1024, 1032), (4384, 1024), (1024, 2048), (1024, 4096), (1020, 3000),
+                                 (1022, 4096)])
 def test_gemm_skinny_decode_shapes(M, N, K):
     """M <= 64 rows (decode steps) take the weight-streaming kernel
     (gemm_skinny.hip): row / column / K edges and every forward epilogue,
-    A with a padded leading dimension, fp32 and bf16 outputs."""
+    A with a padded leading dimension, fp32 and bf16 outputs; N 1024 / 1020
+    at K 4096 / 3000 split K over workgroups (fp32 partials in the ops.gemm
+    workspace + skinny_reduce_kernel), N 1022 (N % 4 != 0) does not."""
     g = torch.Generator().manual_seed(M * 31 + N + K)
     a = torch.randn(M, K, generator=g).bfloat16()
     w = torch.randn(N, K, generator=g).bfloat16()
