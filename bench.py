@@ -381,13 +381,16 @@ def decode_cached_leg(dev, rank, world, B=64, T=2048, K=32, steps=2):
     del m
     ms_step = (el_all - el_pre) / (steps * K) * 1e3
     # HBM bytes of one cached step: every layer's K / V ring of the
-    # window (bf16), the bf16 weights once (layers + lm_head), the logits rows of
-    # the one or two 64-row ring blocks whose LSE partials are recomputed, the new
-    # row written
-    d, L_, Vp = cfg.n_embd, cfg.n_layer, cfg.v_pad
+    # window (bf16), the bf16 weights once (layers + lm_head), and the
+    # incremental ring LSE (msq_ring_step): per (b, v) the merged other blocks,
+    # the prefix (read + write), one suffix-table entry, the new row and the
+    # LSE out (22 B), plus the block entry every 64 steps amortised (32 block
+    # partials, 64 rows, 64 suffix entries: ~8 B)
+    d, L_, Vp, V = cfg.n_embd, cfg.n_layer, cfg.v_pad, cfg.vocab_size
     kv = L_ * B * (T + 6) * d * 2 * 2
     wts = (L_ * 12 * d * d + Vp * d) * 2
-    ring = 1.5 * 64 * B * Vp * 2 + B * Vp * 2
+    nblk = (T + 63) // 64
+    ring = B * V * (22 + (nblk * 4 + 64 * 2 + 64 * 4) / 64) + B * Vp * 2
     nbytes = kv + wts + ring
     ach = nbytes / (ms_step * 1e-3) / 1e9
     return {"value": round(world * B / (ms_step * 1e-3), 1), "unit": "new tokens/s",
@@ -395,7 +398,7 @@ def decode_cached_leg(dev, rank, world, B=64, T=2048, K=32, steps=2):
             "roofline": {"kernel": "whole cached step (graph-replayed)", "bound": "hbm", "achieved": round(ach, 1),
                          "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
                          "algorithmic_bytes_per_step": int(nbytes),
-                         "bytes_model": "K/V ring L*B*(T+6)*d*2*2 + bf16 weights + 1.5 ring blocks of 64 rows + new row"},
+                         "bytes_model": "K/V ring L*B*(T+6)*d*2*2 + bf16 weights + incremental ring LSE (~30 B per (b, v)) + new row"},
             "config": {"workload": "cfg 5 Transformer cached decode (KV ring, approximation of the exact window)",
                        "batch_per_gpu": B, "context": T, "new_tokens": K}}
 

@@ -67,7 +67,8 @@ SIGNATURES = {
                              _i64, _p]),
     "msq_transpose_bf16": (_i, [_p, _i64, _p, _i64, _i64, _i64, _p]),
     "msq_gemm_set_route": (_i, [_i]),
-    "msq_ring_step": (_i, [_p, _p, _p, _i, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p]),
+    "msq_ring_step": (_i, [_p, _p, _p, _p, _i, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p]),
+    "msq_ring_state_bytes": (_sz, [_i64, _i64, _i64]),
     "msq_relattn_decode_pos": (_i, [_i, _p, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _f,
                                     _p, _sz, _p]),
     "msq_ring_lse": (_i, [_p, _p, _p, _i, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p]),

@@ -805,19 +805,99 @@ __global__ __launch_bounds__(NT) void ring_block_lse_kernel(const T* __restrict_
     ring_block_lse<T>(ring, ld, ctx, V, rb, blockIdx.y, blk0 + blockIdx.z, skip, v, part, nblk);
 }
 
-// graph-replayed decode step (msq_ring_step): the position comes from *pos.
-// z = 0: the new row's block without the new row; z = 1: the previous row's
-// block when it is another one (that row joined the ring last step)
+// Graph-replayed decode step (msq_ring_step), position from *pos, slot j =
+// pos % ctx in block c (row jj of it). The LSE of the window's other rows is
+//   lae(O_c, P, Q_c[jj]):  O_c = the blocks other than c (their partials),
+//   P = the rows of block c before j (this ring cycle's new rows, kept as a
+//   running prefix), Q_c[jj] = the rows of block c after j (last cycle's rows,
+//   a suffix table built when the step enters block c).
+// Blocks other than c do not change while the slot walks through c, so a
+// step reads ~22 B per (b, v) instead of re-reading a 64-row block and
+// merging every block partial (~2.3 KB at ctx 2048). A step entering a block
+// (slot jj = 0, or cur_blk != c: also the first step, cur_blk = -1 after
+// msq_ring_lse filled every partial) stores the finished prefix as the left
+// block's partial, merges O_c and scans block c's rows once for the suffix
+// table and the prefix.
+__device__ __forceinline__ void lse_acc(float& m, float& sm, float x) {  // running (max, scaled sum)
+    if (x == -INFINITY) return;
+    if (x > m) {
+        sm = (m == -INFINITY ? 0.f : sm * expf(m - x)) + 1.f;
+        m = x;
+    } else {
+        sm += expf(x - m);
+    }
+}
+__device__ __forceinline__ float lse_val(float m, float sm) { return m == -INFINITY ? -INFINITY : m + logf(sm); }
+
 template <typename T>
-__global__ __launch_bounds__(NT) void ring_step_lse_kernel(const T* __restrict__ ring, int64_t ld, int64_t ctx,
-                                                           int64_t V, int64_t rb, const int64_t* __restrict__ posp,
-                                                           float* __restrict__ part, int64_t nblk) {
-    const int64_t v = ((int64_t)blockIdx.x * NT + threadIdx.x) * VecOf<T>::N;
-    const int64_t pos = *posp, slot = pos % ctx, blk = slot / rb;
-    const int64_t prev = ((pos - 1 + ctx) % ctx) / rb;
-    if (v >= V || (blockIdx.z == 1 && (prev == blk || pos == 0))) return;
-    if (blockIdx.z == 0) ring_block_lse<T>(ring, ld, ctx, V, rb, blockIdx.y, blk, slot, v, part, nblk);
-    else ring_block_lse<T>(ring, ld, ctx, V, rb, blockIdx.y, prev, -1, v, part, nblk);
+__global__ __launch_bounds__(NT) void ring_inc_kernel(const T* __restrict__ ring, int64_t ld, int64_t ctx, int64_t V,
+                                                      int64_t rb, int64_t nblk, const int64_t* __restrict__ posp,
+                                                      float* __restrict__ part, float* __restrict__ others,
+                                                      float* __restrict__ pre, float* __restrict__ suf,
+                                                      const int64_t* __restrict__ cur_blk,
+                                                      float* __restrict__ col_lse) {
+    constexpr int N = VecOf<T>::N;
+    const int64_t v = ((int64_t)blockIdx.x * NT + threadIdx.x) * N, b = blockIdx.y;
+    if (v >= V) return;
+    const int nv = (int)min<int64_t>(N, V - v);
+    const int64_t j = *posp % ctx, c = j / rb, jj = j - c * rb, t_end = min(ctx, c * rb + rb);
+    const int64_t cb = *cur_blk;
+    const T* rb_ = ring + b * ctx * ld + v;
+    float* pp = pre + b * V + v;
+    float* op = others + b * V + v;
+    float* sp = suf + b * rb * V + v;
+    float P[N], O[N], Q[N];
+    if (cb != c || jj == 0) {  // entering block c (also: the ring wrapped onto the same block)
+        float m[N], sm[N], x[N];
+        for (int i = 0; i < nv; ++i) P[i] = pp[i];
+        if (cb >= 0)  // the block just left: its finished prefix is its partial
+            for (int i = 0; i < nv; ++i) part[(b * nblk + cb) * V + v + i] = P[i];
+        for (int i = 0; i < N; ++i) m[i] = -INFINITY, sm[i] = 0.f;
+        for (int64_t k = 0; k < nblk; ++k) {
+            if (k == c) continue;
+            for (int i = 0; i < nv; ++i) lse_acc(m[i], sm[i], k == cb ? P[i] : part[(b * nblk + k) * V + v + i]);
+        }
+        for (int i = 0; i < nv; ++i) op[i] = O[i] = lse_val(m[i], sm[i]);
+        // suffix table: Q[i'] = rows c*rb + i' + 1 .. t_end - 1, for i' = t_end-1-c*rb down to jj
+        for (int i = 0; i < N; ++i) m[i] = -INFINITY, sm[i] = 0.f;
+        for (int64_t t = t_end - 1; t >= j; --t) {
+            for (int i = 0; i < nv; ++i) sp[(t - c * rb) * V + i] = lse_val(m[i], sm[i]);
+            if (t == j) break;
+            ldv<T, N>(rb_ + t * ld, x);
+            for (int i = 0; i < nv; ++i) lse_acc(m[i], sm[i], x[i]);
+        }
+        for (int i = 0; i < nv; ++i) Q[i] = lse_val(m[i], sm[i]);
+        // prefix: rows c*rb .. j-1
+        for (int i = 0; i < N; ++i) m[i] = -INFINITY, sm[i] = 0.f;
+        for (int64_t t = c * rb; t < j; ++t) {
+            ldv<T, N>(rb_ + t * ld, x);
+            for (int i = 0; i < nv; ++i) lse_acc(m[i], sm[i], x[i]);
+        }
+        for (int i = 0; i < nv; ++i) P[i] = lse_val(m[i], sm[i]);
+    } else {
+        for (int i = 0; i < nv; ++i) P[i] = pp[i], O[i] = op[i], Q[i] = sp[jj * V + i];
+    }
+    float x[N];
+    ldv<T, N>(rb_ + j * ld, x);  // the new row (ring_put_kernel ran before)
+    for (int i = 0; i < nv; ++i) {
+        float m = -INFINITY, sm = 0.f;
+        lse_acc(m, sm, O[i]);
+        lse_acc(m, sm, P[i]);
+        lse_acc(m, sm, Q[i]);
+        col_lse[b * V + v + i] = lse_val(m, sm);
+        m = -INFINITY, sm = 0.f;  // the prefix of the next step takes the new row
+        lse_acc(m, sm, P[i]);
+        lse_acc(m, sm, x[i]);
+        pp[i] = lse_val(m, sm);
+    }
+}
+
+// after the step's last reader of *pos: the block the tables now describe, and the next position
+__global__ void ring_advance_kernel(int64_t* __restrict__ pos, int64_t* __restrict__ cur_blk, int64_t ctx, int64_t rb) {
+    if (threadIdx.x == 0) {
+        *cur_blk = (*pos % ctx) / rb;
+        *pos += 1;
+    }
 }
 
 // the new logits row into its ring slot and its token into the token ring
@@ -834,10 +914,8 @@ __global__ __launch_bounds__(NT) void ring_put_kernel(T* __restrict__ ring, int6
 }
 
 __global__ void ring_lse_merge_kernel(const float* __restrict__ part, int64_t B, int64_t nblk, int64_t V,
-                                      float* __restrict__ col_lse, int64_t* __restrict__ pos_inc) {
+                                      float* __restrict__ col_lse) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    // the step's last reader of *pos ran before this launch: advance it
-    if (pos_inc && e == 0) *pos_inc += 1;
     if (e >= B * V) return;
     const int64_t b = e / V, v = e % V;
     const float* p = part + b * nblk * V + v;
@@ -1028,38 +1106,47 @@ extern "C" int msq_ring_lse(float* col_lse, float* part, const void* ring, int d
     blocks(blk_lo, blk_hi - blk_lo, skip_row);
     if (blk_extra >= 0 && (blk_extra < blk_lo || blk_extra >= blk_hi)) blocks(blk_extra, 1, -1);
     hipLaunchKernelGGL(ring_lse_merge_kernel, dim3((unsigned)((B * V + 255) / 256)), dim3(256), 0, s, part, B, nblk, V,
-                       col_lse, nullptr);
+                       col_lse);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }
 
-extern "C" int msq_ring_step(float* col_lse, float* part, void* ring, int dtype, int64_t ld, int64_t B, int64_t ctx,
-                             int64_t V, int64_t rows_per_block, const void* row, int64_t ld_row, int64_t* tokens,
-                             const int64_t* tok, int64_t* pos, void* stream) {
+extern "C" size_t msq_ring_state_bytes(int64_t B, int64_t V, int64_t rows_per_block) {
+    // others | pre | suf (fp32) | 16-B aligned int64 block id in the last 16 bytes
+    return ((size_t)B * V * (2 + rows_per_block) * 4 + 15) / 16 * 16 + 16;
+}
+
+extern "C" int msq_ring_step(float* col_lse, float* part, void* state, void* ring, int dtype, int64_t ld, int64_t B,
+                             int64_t ctx, int64_t V, int64_t rows_per_block, const void* row, int64_t ld_row,
+                             int64_t* tokens, const int64_t* tok, int64_t* pos, void* stream) {
     const int64_t nblk = rows_per_block > 0 ? (ctx + rows_per_block - 1) / rows_per_block : 0;
-    MSQ_CHECK_ARG(col_lse && part && ring && row && tokens && tok && pos, "msq_ring_step: null pointer");
+    MSQ_CHECK_ARG(col_lse && part && state && ring && row && tokens && tok && pos, "msq_ring_step: null pointer");
     MSQ_CHECK_ARG(B > 0 && ctx > 0 && V > 0 && ld >= V && ld % 8 == 0 && ld_row >= ld && ld_row % 8 == 0 &&
-                      rows_per_block > 0 && ((uintptr_t)ring % 16) == 0 && ((uintptr_t)row % 16) == 0,
-                  "msq_ring_step: bad sizes (ld %% 8 == 0, 16-B aligned ring / row)");
+                      rows_per_block > 0 && ((uintptr_t)ring % 16) == 0 && ((uintptr_t)row % 16) == 0 &&
+                      ((uintptr_t)state % 16) == 0,
+                  "msq_ring_step: bad sizes (ld %% 8 == 0, 16-B aligned ring / row / state)");
     MSQ_CHECK_ARG(dtype == MSQ_BF16 || dtype == MSQ_F32, "msq_ring_step: dtype %d", dtype);
     hipStream_t s = (hipStream_t)stream;
     const bool bfl = dtype == MSQ_BF16;
     const int N = bfl ? 8 : 4;
+    float* others = (float*)state;
+    float* pre = others + B * V;
+    float* suf = pre + B * V;
+    int64_t* cur_blk = (int64_t*)((char*)state + msq_ring_state_bytes(B, V, rows_per_block) - 16);
     const dim3 gp((unsigned)((ld + NT * N - 1) / (NT * N)), (unsigned)B);
-    const dim3 gl((unsigned)((V + NT * N - 1) / (NT * N)), (unsigned)B, 2u);
+    const dim3 gl((unsigned)((V + NT * N - 1) / (NT * N)), (unsigned)B);
     if (bfl) {
         hipLaunchKernelGGL(ring_put_kernel<bf16>, gp, dim3(NT), 0, s, (bf16*)ring, ld, ctx, (const bf16*)row, ld_row,
                            tokens, tok, pos);
-        hipLaunchKernelGGL(ring_step_lse_kernel<bf16>, gl, dim3(NT), 0, s, (const bf16*)ring, ld, ctx, V,
-                           rows_per_block, pos, part, nblk);
+        hipLaunchKernelGGL(ring_inc_kernel<bf16>, gl, dim3(NT), 0, s, (const bf16*)ring, ld, ctx, V, rows_per_block,
+                           nblk, pos, part, others, pre, suf, cur_blk, col_lse);
     } else {
         hipLaunchKernelGGL(ring_put_kernel<float>, gp, dim3(NT), 0, s, (float*)ring, ld, ctx, (const float*)row,
                            ld_row, tokens, tok, pos);
-        hipLaunchKernelGGL(ring_step_lse_kernel<float>, gl, dim3(NT), 0, s, (const float*)ring, ld, ctx, V,
-                           rows_per_block, pos, part, nblk);
+        hipLaunchKernelGGL(ring_inc_kernel<float>, gl, dim3(NT), 0, s, (const float*)ring, ld, ctx, V,
+                           rows_per_block, nblk, pos, part, others, pre, suf, cur_blk, col_lse);
     }
-    hipLaunchKernelGGL(ring_lse_merge_kernel, dim3((unsigned)((B * V + 255) / 256)), dim3(256), 0, s, part, B, nblk, V,
-                       col_lse, pos);
+    hipLaunchKernelGGL(ring_advance_kernel, dim3(1), dim3(64), 0, s, pos, cur_blk, ctx, rows_per_block);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }

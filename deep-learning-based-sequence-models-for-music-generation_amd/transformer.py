@@ -232,6 +232,11 @@ class TransformerDecodeCache:
         self.nblk = (context + self.RB - 1) // self.RB
         self.part = e(B, self.nblk, cfg.vocab_size, dt=f32)
         self.part_valid = False
+        # incremental state of msq_ring_step (other blocks merged, the slot
+        # block's prefix and suffix table; the block id in the last 16 bytes)
+        nst = L.lib().msq_ring_state_bytes(B, cfg.vocab_size, self.RB)
+        self.ring_state = torch.empty(nst, device=device, dtype=torch.uint8)
+        self.ring_blk = self.ring_state[nst - 16:nst - 8].view(torch.int64)
         # partials of the split decode attention (msq_relattn_decode)
         self.attn_ws = torch.empty(L.lib().msq_relattn_decode_workspace(B, H, self.S_ring), device=device,
                                    dtype=torch.uint8)
@@ -471,9 +476,14 @@ class TransformerEngine:
                  cache.S_ring, N_META, ptr(cache.pos_dev), float(scale), ptr(cache.attn_ws), cache.attn_ws.numel(), s)
         self._layers_step(cache.x, cache, attn)
         ops.gemm(cache.f, W["lm_w"], out=cache.row_buf, epilogue=L.EPI_BIAS, bias=P["lm_b"])
-        call("msq_ring_step", ptr(cache.lse), ptr(cache.part), ptr(cache.ring), dt(cache.ring), cfg.v_pad, B, cache.ctx,
-             cfg.vocab_size, cache.RB, ptr(cache.row_buf), cache.row_buf.stride(0), ptr(cache.tokens), ptr(tok),
-             ptr(cache.pos_dev), s)
+        self._ring_step(tok, cache)
+
+    def _ring_step(self, tok, cache):
+        """the new row into the logits ring, cache.lse over the window's other rows, pos_dev += 1"""
+        cfg = self.cfg
+        call("msq_ring_step", ptr(cache.lse), ptr(cache.part), ptr(cache.ring_state), ptr(cache.ring), dt(cache.ring),
+             cfg.v_pad, cache.B, cache.ctx, cfg.vocab_size, cache.RB, ptr(cache.row_buf), cache.row_buf.stride(0),
+             ptr(cache.tokens), ptr(tok), ptr(cache.pos_dev), stream())
 
     def _step_host(self, tok, cache):
         cfg, P, W = self.cfg, self.P, self.W
@@ -493,24 +503,17 @@ class TransformerEngine:
                  cache.S_ring, N_META, n_tok, N_META + slot, first % ctx, float(scale), ptr(cache.attn_ws),
                  cache.attn_ws.numel(), s)
         self._layers_step(cache.x, cache, attn)
-        # the new row goes straight into its ring slot, over the row that leaves
-        # the window (or the empty slot); the LSE below leaves that slot out
-        row = cache.ring[:, slot]
-        ops.gemm(cache.f, W["lm_w"], out=row, epilogue=L.EPI_BIAS, bias=P["lm_b"])
-        V, rb = cfg.vocab_size, cache.RB
-        blk = slot // rb
-        if not cache.part_valid:  # first step: every block of the prefilled window
-            lo, hi, extra = 0, cache.nblk, -1
+        ops.gemm(cache.f, W["lm_w"], out=cache.row_buf, epilogue=L.EPI_BIAS, bias=P["lm_b"])
+        if not cache.part_valid:  # first step: every block partial of the prefilled window
+            call("msq_ring_lse", ptr(cache.lse), ptr(cache.part), ptr(cache.ring), dt(cache.ring), cfg.v_pad, B, ctx,
+                 cfg.vocab_size, cache.RB, 0, cache.nblk, slot, -1, s)
+            cache.ring_blk.fill_(-1)
             cache.part_valid = True
-        else:  # this slot's block, and the block holding the previous step's row
-            prev_blk = ((pos - 1) % ctx) // rb
-            lo, hi, extra = blk, blk + 1, (prev_blk if prev_blk != blk else -1)
-        call("msq_ring_lse", ptr(cache.lse), ptr(cache.part), ptr(cache.ring), dt(cache.ring), cfg.v_pad, B, ctx, V,
-             rb, lo, hi, slot, extra, s)
-        cache.tokens[:, slot].copy_(tok)
+        cache.pos_dev.fill_(pos)
+        self._ring_step(tok, cache)
         cache.length = pos + 1
-        cache.logits = row
-        return row
+        cache.logits = cache.row_buf
+        return cache.row_buf
 
     # ------------------------------------------------------------ backward
     def backward(self, dlogits, grads, head_bias_done=False):

@@ -241,16 +241,22 @@ int msq_filtered_colstats(float* col_lse, const void* logits, int dtype, int64_t
 int msq_ring_lse(float* col_lse, float* part, const void* ring, int dtype, int64_t ld, int64_t B, int64_t ctx,
                  int64_t V, int64_t rows_per_block, int64_t blk_lo, int64_t blk_hi, int64_t skip_row,
                  int64_t blk_extra, void* stream);
-/* One graph-replayable cached-decode step of the ring (the same computation as
- * writing the new logits row into slot pos % ctx and calling msq_ring_lse for
- * that slot's block and the previous row's block): copies row [B][ld_row] into
- * ring slot pos % ctx and tok[b] into tokens [B][ctx], recomputes those two
- * blocks' partials, merges col_lse and advances *pos by one. pos: int64 on the
- * device (>= 1, the sequence position of the new row), so the launch arguments
- * do not change from step to step. scripts/generate.py:29-33 per new token. */
-int msq_ring_step(float* col_lse, float* part, void* ring, int dtype, int64_t ld, int64_t B, int64_t ctx, int64_t V,
-                  int64_t rows_per_block, const void* row, int64_t ld_row, int64_t* tokens, const int64_t* tok,
-                  int64_t* pos, void* stream);
+/* One graph-replayable cached-decode step of the ring: copies row [B][ld_row]
+ * into ring slot pos % ctx and tok[b] into tokens [B][ctx], writes col_lse =
+ * the LSE over the window's other rows (what msq_ring_lse gives for that
+ * slot) and advances *pos by one. pos: int64 on the device (the sequence
+ * position of the new row), so the launch arguments do not change from step
+ * to step. Incremental: state (msq_ring_state_bytes, 16-B aligned) holds the
+ * merged partials of the blocks other than the slot's, a running prefix of
+ * the slot's block and its suffix table, and (the int64 in its last 16
+ * bytes) the block they describe: set that int64 to -1 after msq_ring_lse
+ * has filled every block partial (the first step after a prefill); the step
+ * that enters a block re-derives the tables from part and the ring.
+ * scripts/generate.py:29-33 per new token. */
+size_t msq_ring_state_bytes(int64_t B, int64_t V, int64_t rows_per_block);
+int msq_ring_step(float* col_lse, float* part, void* state, void* ring, int dtype, int64_t ld, int64_t B, int64_t ctx,
+                  int64_t V, int64_t rows_per_block, const void* row, int64_t ld_row, int64_t* tokens,
+                  const int64_t* tok, int64_t* pos, void* stream);
 /* loss (fp32 scalar, device) = mean over B*T of the row CE of Z. If dlogits
  * != NULL also writes grad_scale * d(sum of row CE)/dlogits (so grad_scale =
  * 1/(B*T) gives the gradient of the mean).                                  */
