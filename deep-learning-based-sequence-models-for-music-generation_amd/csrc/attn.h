@@ -15,6 +15,8 @@ struct AttnArgs {
     const uint32_t* colmask = nullptr;
     int64_t mask_ld = 0;
     float keep_scale = 1.f;
+    // XCD-aware block order in the flash kernels (xcd_blk3); MSQ_ATTN_NO_XCD=1 clears it
+    int xcd = 1;
 };
 
 __device__ __forceinline__ float keep_bit(const AttnArgs& a, int64_t bh, int64_t i, int64_t j) {

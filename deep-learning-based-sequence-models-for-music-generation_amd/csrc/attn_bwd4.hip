@@ -177,8 +177,9 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int S = (int)a.S, H = (int)a.H;
     const int64_t ldq = a.ldq;
-    const int kb = (int)blockIdx.x;  // 0 = keys 0..127 (the heaviest block)
-    const int h = blockIdx.y, b = blockIdx.z;
+    const Blk3 blk = xcd_blk3(a.xcd);
+    const int kb = blk.x;  // 0 = keys 0..127 (the heaviest block)
+    const int h = blk.y, b = blk.z;
     const int j0 = kb * KB, jw0 = j0 + 32 * w, jk = jw0 + c32;  // this lane's key
     const bf16* qkv_b = (const bf16*)a.qkv + (int64_t)b * S * ldq;
     const bf16* dout_b = dout + (int64_t)b * S * ldo;

@@ -70,8 +70,9 @@ __global__ __launch_bounds__(NT, BK == 64 ? 2 : 4) void flash_bwd_dq_kernel(Attn
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int64_t S = a.S, H = a.H, ldq = a.ldq;
     const int nqt = (int)((S + BM - 1) / BM);
-    const int qt = nqt - 1 - (int)blockIdx.x;  // the longest K ranges first
-    const int64_t h = blockIdx.y, b = blockIdx.z;
+    const Blk3 blk = xcd_blk3(a.xcd);
+    const int qt = nqt - 1 - blk.x;  // the longest K ranges first
+    const int64_t h = blk.y, b = blk.z;
     const int64_t i0 = (int64_t)qt * BM, ilast = min<int64_t>(S - 1, i0 + BM - 1);
     const int64_t rows = ((h * a.B + b) * S) * ldr;
     const bf16* A0 = dsj + rows;

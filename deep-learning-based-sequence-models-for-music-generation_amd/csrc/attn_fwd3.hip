@@ -80,8 +80,9 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int S = (int)a.S, H = (int)a.H;
     const int64_t ldq = a.ldq;
-    const int qb = (int)blockIdx.x;  // 0 = last (heaviest) 256 queries
-    const int h = blockIdx.y, b = blockIdx.z;
+    const Blk3 blk = xcd_blk3(a.xcd);
+    const int qb = blk.x;  // 0 = last (heaviest) 256 queries
+    const int h = blk.y, b = blk.z;
     const int qhi = S - QB * qb, i0 = qhi - QB;  // queries [max(i0, 0), qhi)
     const bf16* qkv_b = (const bf16*)a.qkv + (int64_t)b * S * ldq;
     const __amdgpu_buffer_rsrc_t rq = make_rsrc(qkv_b, (uint32_t)((int64_t)S * ldq * 2));

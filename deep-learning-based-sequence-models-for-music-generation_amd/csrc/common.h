@@ -68,6 +68,28 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
     const int q = nblk / 8, r = nblk % 8, xcd = bid % 8, loc = bid / 8;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
+// the same for a 3-D grid: the hardware hands workgroups to the 8 XCDs round
+// robin in x-fastest dispatch order; logical ids are contiguous per XCD and
+// decoded x fastest, so the x-blocks of one (y, z) run on one XCD and meet its
+// L2 (the attention kernels: the key / query blocks of one (b, h) re-read the
+// same Q, dO, K, V, R rows). remap = false: the plain (blockIdx.x, .y, .z).
+struct Blk3 {
+    int x, y, z;
+};
+__device__ __forceinline__ Blk3 xcd_blk3(bool remap) {
+    Blk3 r;
+    if (!remap) {
+        r.x = blockIdx.x; r.y = blockIdx.y; r.z = blockIdx.z;
+        return r;
+    }
+    const int nx = gridDim.x, ny = gridDim.y;
+    const int lin = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+    const int L = __builtin_amdgcn_readfirstlane(xcd_remap(lin, nx * ny * (int)gridDim.z));
+    r.x = L % nx;
+    r.y = (L / nx) % ny;
+    r.z = L / (nx * ny);
+    return r;
+}
 
 // ---- dropout (nn.Dropout, model_transformer.py:51,80,101) ----
 // Counter-based keep mask: element (row, col) of dropout site `site` under the

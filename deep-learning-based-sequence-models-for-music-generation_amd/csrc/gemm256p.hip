@@ -52,10 +52,15 @@ __device__ __forceinline__ f32x4 p_aux_load(__amdgpu_buffer_rsrc_t rx, uint32_t 
 }
 
 // epilogue of one tile: exactly p_stores<TC>() buffer stores per lane
-template <int EPI, typename TC, typename TX>
+// CS: also the column sums of the written values (fp32, before the rounding
+// to TC) over the tile's rows, one partial row per (M-tile, wave-row) into
+// g.cs_ws[(m0 / 256) * 2 + wr][n] (the layout gemm256_kernel's CS variant
+// writes; colsum_partials_kernel reduces it in a fixed order): 4 more buffer
+// stores per lane, rows / lanes that do not write get the dropped offset
+template <int EPI, typename TC, typename TX, bool CS = false>
 __device__ __forceinline__ void p_epilogue(const GemmArgs& g, __amdgpu_buffer_rsrc_t rc, __amdgpu_buffer_rsrc_t rx,
-                                           __amdgpu_buffer_rsrc_t rbias, int64_t m0, int64_t n0, int wr, int wc,
-                                           int lane, f32x4 (&acc)[2][2][4][2]) {
+                                           __amdgpu_buffer_rsrc_t rbias, __amdgpu_buffer_rsrc_t rcs, int64_t m0,
+                                           int64_t n0, int wr, int wc, int lane, f32x4 (&acc)[2][2][4][2]) {
     constexpr bool HAS_BIAS = EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID ||
                               EPI == MSQ_EPI_BIAS_DROP_RESID;
     const int r = lane & 15, gq = lane >> 4;
@@ -71,6 +76,11 @@ __device__ __forceinline__ void p_epilogue(const GemmArgs& g, __amdgpu_buffer_rs
                     f32x4, __builtin_amdgcn_raw_buffer_load_b128(rbias, n < g.N ? (uint32_t)(n * 4) : OOB, 0, 0));
             }
         }
+    f32x4 csum[2][2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) csum[b][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     // aux rows in groups of 2 of the lane's 8 rows (4 x 16-B loads in flight
     // per row; a whole half-tile's 64 VGPRs of aux would spill beside acc)
 #pragma unroll
@@ -114,6 +124,7 @@ __device__ __forceinline__ void p_epilogue(const GemmArgs& g, __amdgpu_buffer_rs
                         for (int e = 0; e < 4; ++e) t[e] = xp[i][b][j][e] > 0.f ? t[e] : 0.f;
                     }
                     v[j] = t;
+                    if (CS && m < g.M) csum[b][j] += t;
                 }
                 if (sizeof(TC) == 2) {
                     uint32_t p0x = pack_bf16(v[0][0], v[0][1]), p0y = pack_bf16(v[0][2], v[0][3]);
@@ -136,13 +147,28 @@ __device__ __forceinline__ void p_epilogue(const GemmArgs& g, __amdgpu_buffer_rs
             }
         }
     }
+    if (CS) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f32x4 v = csum[b][j];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) v[t] += __shfl_xor(v[t], o, 64);
+                const int64_t n = n0 + b * 128 + wc * 32 + j * 16 + 4 * gq;
+                const uint32_t off = (r == 0 && n < g.N) ? (uint32_t)((((m0 >> 8) * 2 + wr) * g.N + n) * 4) : OOB;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rcs, off, 0, 0);
+            }
+    }
 }
 
-template <int TA, int TB, int EPI, typename TC, typename TX>
+template <int TA, int TB, int EPI, typename TC, typename TX, bool CS = false>
 __global__ __launch_bounds__(NT, 1) void gemm256p_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     lds_t* smem = (lds_t*)smem_raw;
-    constexpr int S = p_stores<TC>();
+    constexpr int S = p_stores<TC>() + (CS ? 4 : 0);
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = w >> 2, wc = w & 3;
@@ -167,6 +193,8 @@ __global__ __launch_bounds__(NT, 1) void gemm256p_kernel(GemmArgs g) {
     const __amdgpu_buffer_rsrc_t rx = make_rsrc((const char*)(g.aux ? g.aux : g.C), g.aux ? g.x_ext : 0u);
     const __amdgpu_buffer_rsrc_t rbias =
         make_rsrc((const char*)(g.bias ? (const void*)g.bias : g.C), g.bias ? (uint32_t)(g.N * 4) : 0u);
+    const __amdgpu_buffer_rsrc_t rcs =
+        make_rsrc((const char*)(CS ? (const void*)g.cs_ws : g.C), CS ? (uint32_t)(g.tiles_m * 2 * g.N * 4) : 0u);
 
     int loA[4], loB[4];
     {
@@ -314,7 +342,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256p_kernel(GemmArgs g) {
             prologue(m1, n1);
         }
         order_fence();
-        p_epilogue<EPI, TC, TX>(g, rc, rx, rbias, m0, n0, wr, wc, lane, acc);
+        p_epilogue<EPI, TC, TX, CS>(g, rc, rx, rbias, rcs, m0, n0, wr, wc, lane, acc);
         order_fence();
         if (!more) break;
         id = nid;
@@ -337,10 +365,10 @@ int num_cus() {
     return n;
 }
 
-template <int TA, int TB, int EPI, typename TC, typename TX>
+template <int TA, int TB, int EPI, typename TC, typename TX, bool CS = false>
 void launch_p(const GemmArgs& g, hipStream_t s) {
     static bool attr = false;
-    auto k = gemm256p_kernel<TA, TB, EPI, TC, TX>;
+    auto k = gemm256p_kernel<TA, TB, EPI, TC, TX, CS>;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * HALF);
         attr = true;
@@ -373,7 +401,8 @@ void dispatch_p(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hipSt
 }
 }  // namespace
 
-bool gemm256p_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s) {
+// C / aux / bias preconditions of the persistent tile and its descriptor extents
+static bool p_prepare(GemmArgs& g, int ta, int tb, int epi, int c_dtype, int aux_dtype) {
     if (epi == MSQ_EPI_ACCUM || g.batch != 1) return false;
     const int esz = c_dtype == MSQ_BF16 ? 2 : 4, xsz = aux_dtype == MSQ_BF16 ? 2 : 4;
     // 16-B C pieces (bf16: 8 columns, fp32: 4), 16-B aligned rows
@@ -386,8 +415,32 @@ bool gemm256p_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_d
     if (!gemm256_plan(g, ta, tb, epi) || g.ksplit != 1) return false;
     g.c_ext = (uint32_t)cext;
     g.x_ext = (uint32_t)xext;
+    return true;
+}
+
+bool gemm256p_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s) {
+    if (!p_prepare(g, ta, tb, epi, c_dtype, aux_dtype)) return false;
     if (c_dtype == MSQ_BF16) dispatch_p<bf16>(g, ta, tb, epi, aux_dtype, s);
     else dispatch_p<float>(g, ta, tb, epi, aux_dtype, s);
+    return true;
+}
+
+// the persistent tile with the column-sum partials (bf16 C, epilogue NONE /
+// RELU_MASK, A / B not transposed or B transposed); the caller reduces g.cs_ws
+bool gemm256p_colsum_launch(GemmArgs g, int ta, int tb, int epi, int aux_dtype, hipStream_t s) {
+    if (ta != 0 || (epi != MSQ_EPI_NONE && epi != MSQ_EPI_RELU_MASK)) return false;
+    if (!p_prepare(g, ta, tb, epi, MSQ_BF16, aux_dtype)) return false;
+    if ((int64_t)g.tiles_m * 2 * g.N * 4 >= (int64_t)OOB) return false;
+    const bool bx = aux_dtype == MSQ_BF16;
+    if (tb == 0) {
+        if (epi == MSQ_EPI_NONE) launch_p<0, 0, MSQ_EPI_NONE, bf16, float, true>(g, s);
+        else if (bx) launch_p<0, 0, MSQ_EPI_RELU_MASK, bf16, bf16, true>(g, s);
+        else launch_p<0, 0, MSQ_EPI_RELU_MASK, bf16, float, true>(g, s);
+    } else {
+        if (epi == MSQ_EPI_NONE) launch_p<0, 1, MSQ_EPI_NONE, bf16, float, true>(g, s);
+        else if (bx) launch_p<0, 1, MSQ_EPI_RELU_MASK, bf16, bf16, true>(g, s);
+        else launch_p<0, 1, MSQ_EPI_RELU_MASK, bf16, float, true>(g, s);
+    }
     return true;
 }
 
