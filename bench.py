@@ -86,6 +86,10 @@ CLASSIFY = {
     # filtered CE: 3 reads of the logits + 1 write of dlogits ([B, T, ld] of the act dtype)
     "msq_filtered_ce": lambda a: ("loss", None, 4.0 * a[13] * a[14] * a[5] * (2 if a[4] == L.BF16 else 4)),
     "msq_filtered_ce_bias": lambda a: ("loss", None, 4.0 * a[14] * a[15] * a[6] * (2 if a[5] == L.BF16 else 4)),
+    # the same with the column statistics from the lm_head epilogue: 2 reads of the logits + 1 write
+    "msq_filtered_ce_bias_part": lambda a: ("loss", None, 3.0 * a[14] * a[15] * a[6] * (2 if a[5] == L.BF16 else 4)),
+    # lm_head forward with the column (max, sum exp) partials in its epilogue
+    "msq_gemm_bias_colstats": lambda a: ("gemm_fwd", 2.0 * a[1] * a[2] * a[3], None),
     "msq_layernorm_fwd": lambda a: ("layernorm", None, None),
     "msq_layernorm_bwd": lambda a: ("layernorm", None, None),
     "msq_layernorm_bwd_dropout": lambda a: ("layernorm", None, None),
@@ -111,12 +115,14 @@ CLASSIFY = {
 }
 
 
-def pmc_traffic(cls):
+PMC_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r3")
+
+
+def pmc_traffic(cls, name="pmc_traffic.json"):
     """HBM bytes per launch of a kernel class from the committed PMC passes
-    (tools/pmc_traffic.py), or None."""
-    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2", "pmc_traffic.json")
+    (tools/pmc_traffic.py, profiles/r3/<name>), or None."""
     try:
-        with open(p) as f:
+        with open(os.path.join(PMC_DIR, name)) as f:
             c = json.load(f)["classes"].get(cls)
         return round(c["hbm_bytes_per_launch"]) if c else None
     except (OSError, ValueError, KeyError):
@@ -427,8 +433,10 @@ def mamba_leg(dev, rank, world, timer, steps=3, B=8, T=4096):
         r = table["ssd_fwd"]
         out["roofline"] = {"kernel": "SSD scan forward (msq_mamba_ssd_fwd_state: state + pass + out kernels)",
                            "bound": "hbm", "achieved": r["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                           "frac": r["frac"], "traffic": None, "avg_launch_ms": r["avg_launch_ms"],
-                           "algorithmic_bytes": int(r["work_per_launch"])}
+                           "frac": r["frac"], "traffic": pmc_traffic("ssd_fwd", "pmc_mamba_traffic.json"),
+                           "avg_launch_ms": r["avg_launch_ms"], "algorithmic_bytes": int(r["work_per_launch"]),
+                           "traffic_source": "profiles/r3/pmc_mamba_traffic.json (FETCH_SIZE x2 + WRITE_SIZE passes "
+                                             "of bench.py --only mamba)"}
     return out
 
 
@@ -447,6 +455,8 @@ def main():
                     help="weight-gradient GEMMs on a second stream (default: main stream; measured no faster, "
                          "and per-class times then sum to the step)")
     ap.add_argument("--serial", action="store_true", help="the default (kept for old command lines)")
+    ap.add_argument("--only", choices=["mamba"], default=None,
+                    help="run only the cfg 3 Mamba train leg (--steps timed steps after one warm-up; PMC passes)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU check of the launch: init gloo ranks, verify the world size, print, exit")
     args = ap.parse_args()
@@ -465,6 +475,14 @@ def main():
         return
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.only == "mamba":
+        timer = ClassTimer()
+        L.TAP = timer
+        r = mamba_leg(dev, rank, world, timer, steps=args.steps)
+        L.TAP = None
+        if rank == 0:
+            print(json.dumps({"mamba_train": r}), flush=True)
+        return
     cfg = TransformerConfig(n_layer=args.layers, block_len=args.seq, precision="bf16", dropout=args.dropout)
     model = Transformer(cfg).to(dev)
     model.engine.overlap_dw = args.overlap
@@ -544,7 +562,7 @@ def main():
                          "bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"],
                          "frac": r["frac"], "traffic": pmc_traffic(dom), "avg_launch_ms": r["avg_launch_ms"],
                          "algorithmic_work_per_launch": r["work_per_launch"],
-                         "traffic_source": "profiles/r2/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
+                         "traffic_source": "profiles/r3/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
                                            "passes of this step, bytes per class launch)"},
             "classes": classes,
         }

@@ -66,6 +66,10 @@ SIGNATURES = {
     "msq_gemm_colsum": (_i, [_i, _i, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _i64, _i, _p, _i, _i64, _p, _i, _p,
                              _i64, _p]),
     "msq_transpose_bf16": (_i, [_p, _i64, _p, _i64, _i64, _i64, _p]),
+    "msq_gemm_colstats_bytes": (_sz, [_i64, _i64]),
+    "msq_gemm_bias_colstats": (_i, [_i, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _p]),
+    "msq_filtered_ce_bias_part": (_i, [_p, _p, _i64, _p, _p, _i, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
+                                       _i64, _i64, _f, _p, _p, _i64, _i64, _p, _p]),
     "msq_gemm_set_route": (_i, [_i]),
     "msq_ring_step": (_i, [_p, _p, _p, _p, _i, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p]),
     "msq_ring_state_bytes": (_sz, [_i64, _i64, _i64]),

@@ -21,6 +21,7 @@ struct GemmArgs {
     // 2 = K is nseg segments of seg rows, tile rows m = r need k%seg >= seg-1-r (dR)
     int tri;
     int64_t seg;
+    int drorder;  // tri 2: M tiles of one K slice adjacent (gemm_bf16_tri, MSQ_DR_ORDER=0 clears it)
     // MSQ_EPI_BIAS_DROP_RESID: drop_base = drop_base(seed, site), keep iff bits >= drop_thr
     uint32_t drop_base, drop_thr;
     float drop_scale;
@@ -124,6 +125,10 @@ bool gemm256p_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_d
 // persistent tile with the column-sum partials of gemm256_colsum_launch (g.cs_ws set,
 // reduced by the caller); false when it does not apply
 bool gemm256p_colsum_launch(GemmArgs g, int ta, int tb, int epi, int aux_dtype, hipStream_t s);
+// persistent tile, bias epilogue + column (max, sum exp) partials of the stored bf16
+// C per (256-row tile, wave-row) p: part[2p][n] = max, part[2p+1][n] = sum (row stride
+// pld); false when it does not apply
+bool gemm256p_colstats_launch(GemmArgs g, int ta, int tb, float* part, int64_t pld, hipStream_t s);
 // skinny-M weight-streaming kernel of the decode steps (gemm_skinny.hip):
 // false when the problem is not M <= 64 / ta = tb = 0 / a forward epilogue
 bool gemm_skinny_launch(const GemmArgs& g, int ta, int tb, int epi, int c_dtype, int aux_dtype, size_t ws_bytes,

@@ -138,10 +138,21 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int tiles = g.tiles_m * g.tiles_n;
     int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int kslice = bid % g.ksplit;  // slices of one tile are adjacent (same XCD group)
-    bid /= g.ksplit;
-    const int bz = bid / tiles;
-    bid -= bz * tiles;
+    int kslice, bz;
+    if (g.tri == 2 && g.drorder) {
+        // dR product: the M tiles of one (head, K slice) adjacent, so the XCD
+        // running them reads that slice's Q rows (the B operand, shared by
+        // every M tile) from its L2 instead of once per M tile
+        const int t = bid % tiles, rest = bid / tiles;
+        kslice = rest % g.ksplit;
+        bz = rest / g.ksplit;
+        bid = t;
+    } else {
+        kslice = bid % g.ksplit;  // slices of one tile are adjacent (same XCD group)
+        bid /= g.ksplit;
+        bz = bid / tiles;
+        bid -= bz * tiles;
+    }
     // grouped ordering: 8 M-tiles share each sweep over N (L2 reuse of B)
     const int GROUP = 8;
     const int per_group = GROUP * g.tiles_n;
@@ -447,6 +458,11 @@ int gemm_bf16_tri(int tri, int64_t seg, int ta, int tb, int64_t M, int64_t N, in
     g.vec = 0;
     g.tri = tri;
     g.seg = seg;
+    static const int drorder = [] {
+        const char* e = getenv("MSQ_DR_ORDER");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    g.drorder = drorder;
     g.ksplit = 1;
     g.kper = ((K + BK - 1) / BK) * BK;
     // tri 2: split the segments over blocks (gemm_bf16_tri_ksplit)
@@ -737,4 +753,36 @@ extern "C" int msq_gemm_colsum(int ta, int tb, int64_t M, int64_t N, int64_t K, 
                          aux_dtype, ld_aux, 0, 0u, 0u, 0.f, nullptr, 0, stream);
     if (rc) return rc;
     return msq_colsum(dbias, accumulate, C, MSQ_BF16, M, N, ldc, ws, stream);
+}
+
+// lm_head forward with the time-axis column statistics of the filtered loss
+// (model_transformer.py:147 + train.py:133-138): C = A.op(B) + bias (bf16) and,
+// per 256-row tile and wave-row p (128 rows), part[2p][n] = max_m C[m][n],
+// part[2p+1][n] = sum_m exp(C[m][n] - max) over the stored bf16 values, row
+// stride pld. Rows of one sequence of T rows (T % 256 == 0) are partials
+// p = b * (T / 128) .. (b + 1) * (T / 128) - 1: msq_filtered_ce_bias_part's colpart.
+extern "C" size_t msq_gemm_colstats_bytes(int64_t M, int64_t N) {
+    return (size_t)((M + 255) / 256) * 4 * ((N + 3) / 4 * 4) * 4;
+}
+
+extern "C" int msq_gemm_bias_colstats(int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                                      const void* B, int64_t ldb, void* C, int64_t ldc, const float* bias, float* part,
+                                      int64_t pld, void* stream) {
+    MSQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && part && pld >= N && pld % 4 == 0 && M % 256 == 0,
+                  "msq_gemm_bias_colstats: sizes (M %% 256 == 0, pld >= N, pld %% 4 == 0)");
+    MSQ_CHECK_ARG(lda >= K && ldb >= (tb ? N : K) && ldc >= N && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0 &&
+                      ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0 && ((uintptr_t)C % 16) == 0,
+                  "msq_gemm_bias_colstats: leading dims / alignment (ld %% 8 == 0, 16-B aligned)");
+    GemmArgs g{};
+    g.M = M; g.N = N; g.K = K;
+    g.A = A; g.lda = lda;
+    g.B = B; g.ldb = ldb;
+    g.C = C; g.ldc = ldc;
+    g.bias = bias;
+    g.batch = 1;
+    g.vec = 1;
+    if (!gemm256p_colstats_launch(g, 0, tb, part, pld, (hipStream_t)stream))
+        return msq_set_error(MSQ_ERR_UNSUPPORTED, "msq_gemm_bias_colstats: shape outside the persistent 256 tile");
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
 }

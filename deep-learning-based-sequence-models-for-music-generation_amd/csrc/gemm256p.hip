@@ -57,12 +57,13 @@ __device__ __forceinline__ f32x4 p_aux_load(__amdgpu_buffer_rsrc_t rx, uint32_t 
 // g.cs_ws[(m0 / 256) * 2 + wr][n] (the layout gemm256_kernel's CS variant
 // writes; colsum_partials_kernel reduces it in a fixed order): 4 more buffer
 // stores per lane, rows / lanes that do not write get the dropped offset
-template <int EPI, typename TC, typename TX, bool CS = false>
+template <int EPI, typename TC, typename TX, int CSM = 0>
 __device__ __forceinline__ void p_epilogue(const GemmArgs& g, __amdgpu_buffer_rsrc_t rc, __amdgpu_buffer_rsrc_t rx,
                                            __amdgpu_buffer_rsrc_t rbias, __amdgpu_buffer_rsrc_t rcs, int64_t m0,
                                            int64_t n0, int wr, int wc, int lane, f32x4 (&acc)[2][2][4][2]) {
     constexpr bool HAS_BIAS = EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID ||
                               EPI == MSQ_EPI_BIAS_DROP_RESID;
+    constexpr bool CS = CSM == 1, ST = CSM == 2;
     const int r = lane & 15, gq = lane >> 4;
     f32x4 bv[2][2];
 #pragma unroll
@@ -81,6 +82,34 @@ __device__ __forceinline__ void p_epilogue(const GemmArgs& g, __amdgpu_buffer_rs
     for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int j = 0; j < 2; ++j) csum[b][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // ST: the column max over the wave's 128 rows of the values as stored
+    // (bias added, rounded to TC), first over the lane's 8 rows, then over the
+    // 16 row-lanes; rows past M do not count
+    constexpr float L2E = 1.4426950408889634f;
+    f32x4 cmax[2][2];
+    if (ST) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f32x4 mx = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int64_t m = m0 + a * 128 + wr * 64 + i * 16 + r;
+                        if (m < g.M) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) mx[e] = fmaxf(mx[e], (float)(TC)(acc[a][b][i][j][e] + bv[b][j][e]));
+                        }
+                    }
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) mx[e] = fmaxf(mx[e], __shfl_xor(mx[e], o, 64));
+                cmax[b][j] = mx;
+            }
+    }
     // aux rows in groups of 2 of the lane's 8 rows (4 x 16-B loads in flight
     // per row; a whole half-tile's 64 VGPRs of aux would spill beside acc)
 #pragma unroll
@@ -125,6 +154,12 @@ __device__ __forceinline__ void p_epilogue(const GemmArgs& g, __amdgpu_buffer_rs
                     }
                     v[j] = t;
                     if (CS && m < g.M) csum[b][j] += t;
+                    if (ST && m < g.M) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (cmax[b][j][e] != -INFINITY)
+                                csum[b][j][e] += __builtin_amdgcn_exp2f(((float)(TC)t[e] - cmax[b][j][e]) * L2E);
+                    }
                 }
                 if (sizeof(TC) == 2) {
                     uint32_t p0x = pack_bf16(v[0][0], v[0][1]), p0y = pack_bf16(v[0][2], v[0][3]);
@@ -147,6 +182,27 @@ __device__ __forceinline__ void p_epilogue(const GemmArgs& g, __amdgpu_buffer_rs
             }
         }
     }
+    if (ST) {
+        // partial (max, sum exp) rows per (M-tile, wave-row) p = (m0 / 256) * 2 + wr:
+        // cs_ws[(2 p) * ldx + n] = max, cs_ws[(2 p + 1) * ldx + n] = sum (ldx: the row stride)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f32x4 v = csum[b][j];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) v[t] += __shfl_xor(v[t], o, 64);
+                const int64_t n = n0 + b * 128 + wc * 32 + j * 16 + 4 * gq;
+                const int64_t p = (m0 >> 8) * 2 + wr;
+                const bool ok = r == 0 && n < g.N;
+                const uint32_t om = ok ? (uint32_t)(((2 * p) * g.ldx + n) * 4) : OOB;
+                const uint32_t os = ok ? (uint32_t)(((2 * p + 1) * g.ldx + n) * 4) : OOB;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, cmax[b][j]), rcs, om, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rcs, os, 0, 0);
+            }
+    }
     if (CS) {
 #pragma unroll
         for (int b = 0; b < 2; ++b)
@@ -164,11 +220,11 @@ __device__ __forceinline__ void p_epilogue(const GemmArgs& g, __amdgpu_buffer_rs
     }
 }
 
-template <int TA, int TB, int EPI, typename TC, typename TX, bool CS = false>
+template <int TA, int TB, int EPI, typename TC, typename TX, int CSM = 0>
 __global__ __launch_bounds__(NT, 1) void gemm256p_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     lds_t* smem = (lds_t*)smem_raw;
-    constexpr int S = p_stores<TC>() + (CS ? 4 : 0);
+    constexpr int S = p_stores<TC>() + (CSM == 1 ? 4 : CSM == 2 ? 8 : 0);
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = w >> 2, wc = w & 3;
@@ -190,11 +246,14 @@ __global__ __launch_bounds__(NT, 1) void gemm256p_kernel(GemmArgs g) {
     const __amdgpu_buffer_rsrc_t ra = make_rsrc((const char*)g.A, g.a_ext);
     const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)g.B, g.b_ext);
     const __amdgpu_buffer_rsrc_t rc = make_rsrc((const char*)g.C, g.c_ext);
-    const __amdgpu_buffer_rsrc_t rx = make_rsrc((const char*)(g.aux ? g.aux : g.C), g.aux ? g.x_ext : 0u);
     const __amdgpu_buffer_rsrc_t rbias =
         make_rsrc((const char*)(g.bias ? (const void*)g.bias : g.C), g.bias ? (uint32_t)(g.N * 4) : 0u);
-    const __amdgpu_buffer_rsrc_t rcs =
-        make_rsrc((const char*)(CS ? (const void*)g.cs_ws : g.C), CS ? (uint32_t)(g.tiles_m * 2 * g.N * 4) : 0u);
+    // CSM 1: colsum partials [tiles_m * 2][N]; 2: (max, sum) partials [tiles_m * 2][2][ldx]
+    const uint32_t cs_bytes =
+        CSM == 1 ? (uint32_t)(g.tiles_m * 2 * g.N * 4) : CSM == 2 ? (uint32_t)(g.tiles_m * 4 * g.ldx * 4) : 0u;
+    const __amdgpu_buffer_rsrc_t rx =
+        make_rsrc((const char*)(g.aux && CSM != 2 ? g.aux : g.C), g.aux && CSM != 2 ? g.x_ext : 0u);
+    const __amdgpu_buffer_rsrc_t rcs = make_rsrc((const char*)(CSM ? (const void*)g.cs_ws : g.C), cs_bytes);
 
     int loA[4], loB[4];
     {
@@ -342,7 +401,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256p_kernel(GemmArgs g) {
             prologue(m1, n1);
         }
         order_fence();
-        p_epilogue<EPI, TC, TX, CS>(g, rc, rx, rbias, rcs, m0, n0, wr, wc, lane, acc);
+        p_epilogue<EPI, TC, TX, CSM>(g, rc, rx, rbias, rcs, m0, n0, wr, wc, lane, acc);
         order_fence();
         if (!more) break;
         id = nid;
@@ -365,10 +424,10 @@ int num_cus() {
     return n;
 }
 
-template <int TA, int TB, int EPI, typename TC, typename TX, bool CS = false>
+template <int TA, int TB, int EPI, typename TC, typename TX, int CSM = 0>
 void launch_p(const GemmArgs& g, hipStream_t s) {
     static bool attr = false;
-    auto k = gemm256p_kernel<TA, TB, EPI, TC, TX, CS>;
+    auto k = gemm256p_kernel<TA, TB, EPI, TC, TX, CSM>;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * HALF);
         attr = true;
@@ -433,14 +492,28 @@ bool gemm256p_colsum_launch(GemmArgs g, int ta, int tb, int epi, int aux_dtype, 
     if ((int64_t)g.tiles_m * 2 * g.N * 4 >= (int64_t)OOB) return false;
     const bool bx = aux_dtype == MSQ_BF16;
     if (tb == 0) {
-        if (epi == MSQ_EPI_NONE) launch_p<0, 0, MSQ_EPI_NONE, bf16, float, true>(g, s);
-        else if (bx) launch_p<0, 0, MSQ_EPI_RELU_MASK, bf16, bf16, true>(g, s);
-        else launch_p<0, 0, MSQ_EPI_RELU_MASK, bf16, float, true>(g, s);
+        if (epi == MSQ_EPI_NONE) launch_p<0, 0, MSQ_EPI_NONE, bf16, float, 1>(g, s);
+        else if (bx) launch_p<0, 0, MSQ_EPI_RELU_MASK, bf16, bf16, 1>(g, s);
+        else launch_p<0, 0, MSQ_EPI_RELU_MASK, bf16, float, 1>(g, s);
     } else {
-        if (epi == MSQ_EPI_NONE) launch_p<0, 1, MSQ_EPI_NONE, bf16, float, true>(g, s);
-        else if (bx) launch_p<0, 1, MSQ_EPI_RELU_MASK, bf16, bf16, true>(g, s);
-        else launch_p<0, 1, MSQ_EPI_RELU_MASK, bf16, float, true>(g, s);
+        if (epi == MSQ_EPI_NONE) launch_p<0, 1, MSQ_EPI_NONE, bf16, float, 1>(g, s);
+        else if (bx) launch_p<0, 1, MSQ_EPI_RELU_MASK, bf16, bf16, 1>(g, s);
+        else launch_p<0, 1, MSQ_EPI_RELU_MASK, bf16, float, 1>(g, s);
     }
     return true;
 }
 
+
+// bias epilogue + per-(M-tile, wave-row) column (max, sum exp) partials of the
+// stored bf16 values into part (row stride pld): the lm_head forward feeding
+// the time-axis logsumexp of the filtered loss (train.py:133-138)
+bool gemm256p_colstats_launch(GemmArgs g, int ta, int tb, float* part, int64_t pld, hipStream_t s) {
+    if (ta != 0 || g.aux) return false;
+    if (!p_prepare(g, ta, tb, MSQ_EPI_BIAS, MSQ_BF16, MSQ_F32)) return false;
+    if (pld < g.N || pld % 4 || ((uintptr_t)part % 16) || (int64_t)g.tiles_m * 4 * pld * 4 >= (int64_t)OOB) return false;
+    g.cs_ws = part;
+    g.ldx = pld;
+    if (tb == 0) launch_p<0, 0, MSQ_EPI_BIAS, bf16, float, 2>(g, s);
+    else launch_p<0, 1, MSQ_EPI_BIAS, bf16, float, 2>(g, s);
+    return true;
+}

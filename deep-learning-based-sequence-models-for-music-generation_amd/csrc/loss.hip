@@ -365,8 +365,10 @@ __global__ __launch_bounds__(NT) void colstats2_kernel(LossArgs a, float* __rest
         }
 }
 
+// nts partials per sequence, (max, sum) rows of stride pst: part[((b nts + ts) 2) pst + v]
+// (colstats2: nts = TS2, pst = V; the lm_head GEMM epilogue: nts = T / 128, pst = its ld)
 __global__ void colstats2_merge_kernel(LossArgs a, const float* __restrict__ part, float* __restrict__ col_lse,
-                                       float* __restrict__ clp, int64_t Vp) {
+                                       float* __restrict__ clp, int64_t Vp, int nts, int64_t pst) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= a.B * Vp) return;
     const int64_t b = e / Vp, v = e % Vp;
@@ -375,11 +377,11 @@ __global__ void colstats2_merge_kernel(LossArgs a, const float* __restrict__ par
         return;
     }
     float m = -INFINITY;
-    for (int ts = 0; ts < TS2; ++ts) m = fmaxf(m, part[((b * TS2 + ts) * 2) * a.V + v]);
+    for (int ts = 0; ts < nts; ++ts) m = fmaxf(m, part[((b * nts + ts) * 2) * pst + v]);
     float s = 0.f;
-    for (int ts = 0; ts < TS2; ++ts) {
-        const float pm = part[((b * TS2 + ts) * 2) * a.V + v];
-        if (pm != -INFINITY) s += part[((b * TS2 + ts) * 2 + 1) * a.V + v] * expf(pm - m);
+    for (int ts = 0; ts < nts; ++ts) {
+        const float pm = part[((b * nts + ts) * 2) * pst + v];
+        if (pm != -INFINITY) s += part[((b * nts + ts) * 2 + 1) * pst + v] * expf(pm - m);
     }
     const float l = m + logf(s);
     col_lse[b * a.V + v] = l;
@@ -964,11 +966,11 @@ extern "C" int msq_filtered_ce(float* loss, void* dlogits, int64_t ldd, const vo
                                 grad_scale, col_lse, workspace, stream);
 }
 
-extern "C" int msq_filtered_ce_bias(float* loss, void* dlogits, int64_t ldd, float* dbias, const void* logits,
-                                    int dtype, int64_t ld, const int64_t* src, const int64_t* trg, const float* wtab,
-                                    int64_t b0, int64_t b1, int64_t b2, int64_t b3, int64_t B, int64_t T, int64_t V,
-                                    float grad_scale, float* col_lse, void* workspace, void* stream) {
-    LOSS_CHECK();
+static int filtered_ce_impl(float* loss, void* dlogits, int64_t ldd, float* dbias, const void* logits, int dtype,
+                            int64_t ld, const int64_t* src, const int64_t* trg, const float* wtab, int64_t b0,
+                            int64_t b1, int64_t b2, int64_t b3, int64_t B, int64_t T, int64_t V, float grad_scale,
+                            float* col_lse, void* workspace, void* stream, const float* colpart, int64_t nts,
+                            int64_t pld) {
     MSQ_CHECK_ARG(!dbias || dlogits, "msq_filtered_ce_bias: dbias needs dlogits");
     MSQ_CHECK_ARG(!dlogits || ldd % 4 == 0, "msq_filtered_ce: ldd %% 4 != 0");
     const LossArgs a = mk(logits, ld, src, trg, wtab, b0, b1, b2, b3, B, T, V);
@@ -1005,16 +1007,21 @@ extern "C" int msq_filtered_ce_bias(float* loss, void* dlogits, int64_t ldd, flo
         int* wrange = (int*)(wtp + 5 * Vp);
         hipLaunchKernelGGL(wrange_kernel, dim3(5), dim3(256), 0, s, wtp, Vp, V, wrange);
         // part2 carries, in turn: colstats2 partials, colsum partials, dbias partials
-        if (bfl) {
+        if (colpart) {  // column (max, sum) partials from the lm_head GEMM epilogue
+            hipLaunchKernelGGL(colstats2_merge_kernel, gm, dim3(256), 0, s, a, colpart, col_lse, clp, Vp, (int)nts, pld);
+        } else if (bfl) {
             hipLaunchKernelGGL(colstats2_kernel<bf16>, gc, dim3(NT), 0, s, a, part2);
-            hipLaunchKernelGGL(colstats2_merge_kernel, gm, dim3(256), 0, s, a, part2, col_lse, clp, Vp);
+            hipLaunchKernelGGL(colstats2_merge_kernel, gm, dim3(256), 0, s, a, part2, col_lse, clp, Vp, TS2, V);
+        } else {
+            hipLaunchKernelGGL(colstats2_kernel<float>, gc, dim3(NT), 0, s, a, part2);
+            hipLaunchKernelGGL(colstats2_merge_kernel, gm, dim3(256), 0, s, a, part2, col_lse, clp, Vp, TS2, V);
+        }
+        if (bfl) {
             hipLaunchKernelGGL(rowlse_kernel<bf16>, gr, dim3(256), 0, s, a, clp, wtp, (int)Vp, wrange, rows, row_lse);
             hipLaunchKernelGGL(cspart_kernel<bf16>, gc, dim3(NT), 0, s, a, clp, wtp, (int)Vp, row_lse, grad_scale, part2);
             hipLaunchKernelGGL(cs_reduce_kernel, gm, dim3(256), 0, s, part2, B, V, Vp, csp);
             hipLaunchKernelGGL((finish2_kernel<bf16, bf16>), gc, dim3(NT), 0, s, a, clp, wtp, (int)Vp, row_lse, csp, (bf16*)dlogits, ldd, grad_scale, dbias ? part2 : nullptr);
         } else {
-            hipLaunchKernelGGL(colstats2_kernel<float>, gc, dim3(NT), 0, s, a, part2);
-            hipLaunchKernelGGL(colstats2_merge_kernel, gm, dim3(256), 0, s, a, part2, col_lse, clp, Vp);
             hipLaunchKernelGGL(rowlse_kernel<float>, gr, dim3(256), 0, s, a, clp, wtp, (int)Vp, wrange, rows, row_lse);
             hipLaunchKernelGGL(cspart_kernel<float>, gc, dim3(NT), 0, s, a, clp, wtp, (int)Vp, row_lse, grad_scale, part2);
             hipLaunchKernelGGL(cs_reduce_kernel, gm, dim3(256), 0, s, part2, B, V, Vp, csp);
@@ -1042,6 +1049,29 @@ extern "C" int msq_filtered_ce_bias(float* loss, void* dlogits, int64_t ldd, flo
     hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(1024), 0, s, rows, B * T, loss);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
+}
+
+extern "C" int msq_filtered_ce_bias(float* loss, void* dlogits, int64_t ldd, float* dbias, const void* logits,
+                                    int dtype, int64_t ld, const int64_t* src, const int64_t* trg, const float* wtab,
+                                    int64_t b0, int64_t b1, int64_t b2, int64_t b3, int64_t B, int64_t T, int64_t V,
+                                    float grad_scale, float* col_lse, void* workspace, void* stream) {
+    LOSS_CHECK();
+    return filtered_ce_impl(loss, dlogits, ldd, dbias, logits, dtype, ld, src, trg, wtab, b0, b1, b2, b3, B, T, V,
+                            grad_scale, col_lse, workspace, stream, nullptr, 0, 0);
+}
+
+extern "C" int msq_filtered_ce_bias_part(float* loss, void* dlogits, int64_t ldd, float* dbias, const void* logits,
+                                         int dtype, int64_t ld, const int64_t* src, const int64_t* trg,
+                                         const float* wtab, int64_t b0, int64_t b1, int64_t b2, int64_t b3, int64_t B,
+                                         int64_t T, int64_t V, float grad_scale, float* col_lse, const float* colpart,
+                                         int64_t nts, int64_t pld, void* workspace, void* stream) {
+    LOSS_CHECK();
+    MSQ_CHECK_ARG(colpart && nts > 0 && pld >= V, "msq_filtered_ce_bias_part: colpart / nts / pld");
+    MSQ_CHECK_ARG(dlogits && ld % 8 == 0 && ldd % 8 == 0 && ((uintptr_t)logits % 16) == 0 &&
+                      ((uintptr_t)dlogits % 16) == 0,
+                  "msq_filtered_ce_bias_part: needs the streaming path (dlogits, ld / ldd %% 8, 16-B aligned)");
+    return filtered_ce_impl(loss, dlogits, ldd, dbias, logits, dtype, ld, src, trg, wtab, b0, b1, b2, b3, B, T, V,
+                            grad_scale, col_lse, workspace, stream, colpart, nts, pld);
 }
 
 extern "C" int msq_filtered_logit(float* z, int64_t ldz, const void* logits, int dtype, int64_t ld,

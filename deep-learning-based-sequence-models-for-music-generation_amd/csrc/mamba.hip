@@ -25,6 +25,9 @@ constexpr int LD = 68;  // LDS row stride (floats) for 64x64 tiles
 struct MambaArgs {
     int64_t B, L, d_inner, nheads, conv_dim, ldz;  // ldz: row stride of zxbcdt
     int64_t ldxc;                                  // row stride of the conv output (xBC)
+    // chunk kernels: XCD-aware block order, the heads of one (b, chunk) on one
+    // XCD (they share the chunk's B / C rows); MSQ_MAMBA_NO_XCD=1 clears it
+    int xcd;
 };
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + expf(-x)); }
@@ -751,6 +754,11 @@ MambaArgs mk(int64_t B, int64_t L, int64_t d_inner, int64_t nheads, int64_t ldz,
     MambaArgs a;
     a.B = B; a.L = L; a.d_inner = d_inner; a.nheads = nheads; a.conv_dim = d_inner + 2 * N; a.ldz = ldz;
     a.ldxc = ldxc;
+    static const int xcd = [] {
+        const char* e = getenv("MSQ_MAMBA_NO_XCD");
+        return e && e[0] == '1' ? 0 : 1;
+    }();
+    a.xcd = xcd;
     return a;
 }
 
@@ -844,10 +852,18 @@ struct Chunk {
 };
 __device__ __forceinline__ Chunk chunk_of(const MambaArgs& a, int nch) {
     Chunk k;
-    const int64_t bh = blockIdx.x / nch;
-    k.c = blockIdx.x % nch;
-    k.b = bh / a.nheads;
-    k.h = bh % a.nheads;
+    if (a.xcd) {  // logical id (h fastest, then chunk, then b), contiguous per XCD
+        const int64_t id = __builtin_amdgcn_readfirstlane(xcd_remap((int)blockIdx.x, (int)gridDim.x));
+        k.h = id % a.nheads;
+        const int64_t r = id / a.nheads;
+        k.c = r % nch;
+        k.b = r / nch;
+    } else {
+        const int64_t bh = blockIdx.x / nch;
+        k.c = blockIdx.x % nch;
+        k.b = bh / a.nheads;
+        k.h = bh % a.nheads;
+    }
     k.t0 = k.c * Q;
     k.nval = (int)min<int64_t>(Q, a.L - k.t0);
     return k;

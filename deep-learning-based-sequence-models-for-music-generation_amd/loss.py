@@ -31,11 +31,15 @@ def _ws(B, T, V, device):
     return workspace(L.lib().msq_filtered_workspace(B, T, V), device, "loss")
 
 
-def ce_forward_backward(src, logits, trg, V, grammar=None, dlogits=None, grad_scale=None, col_lse=None, dbias=None):
+def ce_forward_backward(src, logits, trg, V, grammar=None, dlogits=None, grad_scale=None, col_lse=None, dbias=None,
+                        colpart=None):
     """logits [B,T,ld] (fp32/bf16, ld >= V). Returns (loss scalar tensor,
     dlogits or None). grad_scale defaults to 1/(B*T) (gradient of the mean).
     dbias (fp32 [V], with dlogits): += column sums of dlogits (the output
-    layer's bias gradient) in the same pass."""
+    layer's bias gradient) in the same pass. colpart ([B*T/128, 2, ld] fp32,
+    with dlogits): the time-axis column (max, sum exp) partials the lm_head
+    GEMM epilogue produced (ops.gemm_bias_colstats); the loss then skips its
+    own pass over the logits for them."""
     grammar = grammar or Grammar()
     B, T = src.shape
     ld = logits.stride(1)
@@ -46,6 +50,12 @@ def ce_forward_backward(src, logits, trg, V, grammar=None, dlogits=None, grad_sc
         col_lse = torch.empty(B, V, device=logits.device, dtype=torch.float32)
     gs = (1.0 / (B * T)) if grad_scale is None else float(grad_scale)
     b = grammar.bounds
+    if colpart is not None:
+        assert dlogits is not None and colpart.shape[0] == B * T // 128
+        call("msq_filtered_ce_bias_part", ptr(loss), ptr(dlogits), dlogits.stride(1), ptr(dbias), ptr(logits),
+             dt(logits), ld, ptr(src), ptr(trg), ptr(wtab), b[0], b[1], b[2], b[3], B, T, V, gs, ptr(col_lse),
+             ptr(colpart), T // 128, colpart.stride(1), ptr(_ws(B, T, V, logits.device)), stream())
+        return loss, dlogits
     call("msq_filtered_ce_bias", ptr(loss), ptr(dlogits), dlogits.stride(1) if dlogits is not None else 0,
          ptr(dbias), ptr(logits), dt(logits), ld, ptr(src), ptr(trg), ptr(wtab), b[0], b[1], b[2], b[3], B, T, V, gs,
          ptr(col_lse), ptr(_ws(B, T, V, logits.device)), stream())

@@ -96,6 +96,22 @@ def gemm_colsum(A, B, out, dbias, *, ta=False, tb=False, epilogue=L.EPI_NONE, au
     return out
 
 
+def gemm_bias_colstats(A, W, out, bias, part):
+    """out = A . W^T + bias (bf16; W [N, K] as nn.Linear.weight) and the
+    column (max, sum exp) partials of out per 128 rows into part
+    (msq_gemm_bias_colstats; [M / 128, 2, ld] fp32). Returns False when the
+    shape is outside the kernel (the caller runs the plain GEMM)."""
+    M, K = A.shape
+    N = W.shape[0]
+    # the persistent 256 tile's preconditions (gemm256_plan: >= 128 tiles, K % 8)
+    if A.dtype != torch.bfloat16 or M % 256 or N % 8 or K % 8 or out.shape != (M, N) or \
+            (M // 256) * ((N + 255) // 256) < 128:
+        return False
+    call("msq_gemm_bias_colstats", 0, M, N, K, ptr(A), A.stride(0), ptr(W), W.stride(0), ptr(out), out.stride(0),
+         ptr(bias), ptr(part), part.stride(-2), stream())
+    return True
+
+
 _WS = {}
 
 

@@ -37,6 +37,8 @@ class TrainStep:
         self.grammar = grammar or Grammar()
         self.lm_bias_grad = self.eng.layout.views(self.grads)["lm_b"][:self.eng.cfg.vocab_size]
         self.step_no = 0
+        if hasattr(self.eng, "head_stats"):  # the loss's column statistics from the lm_head epilogue
+            self.eng.head_stats = os.environ.get("MSQ_NO_HEAD_STATS") != "1"
         self.buckets = None
         if dist.is_initialized() and dist.get_world_size(group) > 1:
             self.buckets = GradBuckets(self.grads, self.eng.bucket_ranges(), group)
@@ -55,7 +57,8 @@ class TrainStep:
         self.grads.zero_()
         # the output-bias gradient (column sums of dlogits) comes out of the loss pass
         loss, _ = ce_forward_backward(src, A.logits.view(B, T, cfg.v_pad), trg, cfg.vocab_size, self.grammar,
-                                      dlogits=dl.view(B, T, cfg.v_pad), dbias=self.lm_bias_grad)
+                                      dlogits=dl.view(B, T, cfg.v_pad), dbias=self.lm_bias_grad,
+                                      colpart=A.colpart if getattr(A, "colpart_valid", False) else None)
         eng.backward(dl, self.grads, head_bias_done=True)
         scale = self.buckets.finish() if self.buckets is not None else 1.0
         self.step_no += 1

@@ -170,6 +170,10 @@ class _Acts:
         self.f = e(B * T, d)
         self.stf = e(2, B * T, dt=f32)
         self.logits = e(B * T, cfg.v_pad)
+        # the lm_head epilogue's column (max, sum exp) partials per 128 rows
+        # (msq_gemm_bias_colstats), valid after a forward that produced them
+        self.colpart = None
+        self.colpart_valid = False
         self.gen = 0
         self._bwd = None
         self.drop = None      # (seed, p) of the last training forward
@@ -271,6 +275,8 @@ class TransformerEngine:
         self.act = torch.bfloat16 if cfg.precision == "bf16" else torch.float32
         self.bind(flat)
         self._acts = {}
+        # lm_head forward emits the loss's column statistics (set by TrainStep)
+        self.head_stats = False
 
     def bind(self, flat):
         self.flat = flat
@@ -394,8 +400,16 @@ class TransformerEngine:
         ops.layernorm_fwd(x_last, P["lnf_w"], P["lnf_b"], out=A.f, mean=A.stf[0], rstd=A.stf[1],
                           seg=(T, N_META))
         V = cfg.vocab_size
-        # full V_pad rows (pad rows of lm_w / lm_b are zero): 16-B aligned rows, 256-tile eligible
-        ops.gemm(A.f, W["lm_w"], out=A.logits, epilogue=L.EPI_BIAS, bias=P["lm_b"])
+        # full V_pad rows (pad rows of lm_w / lm_b are zero): 16-B aligned rows, 256-tile eligible.
+        # head_stats (the train step's streaming loss): the time-axis column
+        # statistics of filtered_logit come out of the GEMM epilogue
+        A.colpart_valid = False
+        if self.head_stats and cache is None and T % 256 == 0:
+            if A.colpart is None:
+                A.colpart = torch.empty(B * T // 128, 2, cfg.v_pad, device=self.device, dtype=torch.float32)
+            A.colpart_valid = ops.gemm_bias_colstats(A.f, W["lm_w"], A.logits, P["lm_b"], A.colpart)
+        if not A.colpart_valid:
+            ops.gemm(A.f, W["lm_w"], out=A.logits, epilogue=L.EPI_BIAS, bias=P["lm_b"])
         if cache is not None:
             if T > cache.ctx:
                 raise ValueError(f"prefill of {T} tokens exceeds the cache context {cache.ctx}")

@@ -153,6 +153,20 @@ size_t msq_gemm_colsum_workspace(int64_t M, int64_t N);
 int msq_gemm_colsum(int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
                     int64_t ldb, void* C, int64_t ldc, int epilogue, const void* aux, int aux_dtype, int64_t ld_aux,
                     float* dbias, int accumulate, void* ws, int64_t ws_bytes, void* stream);
+/* lm_head forward (model_transformer.py:147, nn.Linear with bias) in bf16:
+ * C[m][n] = sum_k A[m][k] B[n][k] + bias[n] (A [M, K] row-major; B stored
+ * [N, K] as msq_gemm's tb = 0, or [K, N] with tb = 1), and per 256-row tile / 128-row half p
+ * the column max and sum of exp(C - max) of the stored bf16 values:
+ * part[2p][n], part[2p+1][n] (row stride pld). The statistics are the
+ * time-axis logsumexp partials of filtered_logit (train.py:136) for rows
+ * ordered (b, t) with T % 256 == 0: pass part, T / 128 and pld to
+ * msq_filtered_ce_bias_part. M % 256 == 0; part holds
+ * msq_gemm_colstats_bytes(M, N) bytes at pld = N rounded up to 4. Returns
+ * MSQ_ERR_UNSUPPORTED for shapes outside the persistent 256 tile. */
+size_t msq_gemm_colstats_bytes(int64_t M, int64_t N);
+int msq_gemm_bias_colstats(int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
+                           int64_t ldb, void* C, int64_t ldc, const float* bias, float* part, int64_t pld,
+                           void* stream);
 /* dst[c][r] = src[r][c] for a bf16 [rows][cols] matrix (leading dims in
  * elements): the transposed weight copies the backward's dX products read
  * (autograd's x.grad = dy @ W of nn.Linear, model_transformer.py:47,95,97,147). */
@@ -271,6 +285,18 @@ int msq_filtered_ce_bias(float* loss, void* dlogits, int64_t ldd, float* dbias, 
                          int64_t ld, const int64_t* src, const int64_t* trg, const float* wtab, int64_t b0, int64_t b1,
                          int64_t b2, int64_t b3, int64_t B, int64_t T, int64_t V, float grad_scale, float* col_lse,
                          void* workspace, void* stream);
+/* msq_filtered_ce_bias with the time-axis column statistics supplied by the
+ * lm_head GEMM epilogue (msq_gemm_bias_colstats): colpart holds, per
+ * sequence b, nts (max, sum exp) partial row pairs of stride pld
+ * (colpart[((b * nts + ts) * 2) * pld + v] = max, the next row the sum), so the
+ * pass that re-reads the logits for col_lse (train.py:136, log_softmax over
+ * the time axis) is skipped. Needs the streaming path: bf16 / fp32 logits and
+ * dlogits with ld, ldd % 8 == 0 and 16-B aligned rows. */
+int msq_filtered_ce_bias_part(float* loss, void* dlogits, int64_t ldd, float* dbias, const void* logits, int dtype,
+                              int64_t ld, const int64_t* src, const int64_t* trg, const float* wtab, int64_t b0,
+                              int64_t b1, int64_t b2, int64_t b3, int64_t B, int64_t T, int64_t V, float grad_scale,
+                              float* col_lse, const float* colpart, int64_t nts, int64_t pld, void* workspace,
+                              void* stream);
 /* Z rows t_begin..T-1 (fp32, [B, T-t_begin, ldz]) = filtered_logit(src, logits). */
 int msq_filtered_logit(float* z, int64_t ldz, const void* logits, int dtype, int64_t ld, const int64_t* src,
                        const float* wtab, int64_t b0, int64_t b1, int64_t b2, int64_t b3, int64_t B, int64_t T,
