@@ -20,10 +20,6 @@ struct AttnArgs {
     // forward: waves 4-7 (the second half of the 8-wave workgroup) at s_setprio 1
     // for the whole loop (MI355X_MICROARCH 'Two waves per SIMD' item 4); MSQ_ATTN_FWD_PRIO=0 clears it
     int fwd_prio = 1;
-    // backward: dS stored once (r-indexed dQR only; the dq kernel reads the
-    // j-indexed view of each dQR row by unaligned 16-B buffer loads); the key /
-    // value pass then sends its dSj stores to a dropped offset. MSQ_ATTN_DS1=1
-    int ds1 = 0;
 };
 
 __device__ __forceinline__ float keep_bit(const AttnArgs& a, int64_t bh, int64_t i, int64_t j) {

@@ -415,9 +415,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv4_kernel(AttnArgs a, const 
             const u32x4 v = *(const u32x4*)(smem + O_T + sbuf * T_BYTES + row * T_PITCH + ch * 16);
             const int i = ip + row, j = j0 + 8 * ch;
             const bool in = i < S;
-            // a.ds1: no dSj copy (the store goes to the dropped offset, so the
-            // per-tile store count the vmcnt waits rely on is unchanged)
-            const uint32_t os = (in && !a.ds1) ? (uint32_t)(((int64_t)i * ldr + j) * 2) : OOB;
+            const uint32_t os = in ? (uint32_t)(((int64_t)i * ldr + j) * 2) : OOB;
             const uint32_t oq = in ? (uint32_t)(((int64_t)i * ldr + (S - 1 - i + j)) * 2) : OOB;
             __builtin_amdgcn_raw_buffer_store_b128(v, rsj, os, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b128(v, rqr, oq, 0, 0);

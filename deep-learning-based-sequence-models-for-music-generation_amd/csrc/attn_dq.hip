@@ -2,9 +2,8 @@
 // differentiated w.r.t. q):
 //   dq_i = sum_j dS_ij k_j  +  sum_j dS_ij R[S-1-i+j]
 //        = sum_j dSj[i][j] K[j]  +  sum_r dQR[i][r] R[r]          (r = S-1-i+j)
-// The key/value pass (attn_bwd4.hip) writes dS twice: j-indexed (dSj, zero for
-// j > i inside the tiles it visits) and r-indexed (dQR), or only dQR in the
-// dS-once mode (a.ds1, below). Both products are plain
+// The key/value pass (attn_bwd3.hip) writes dS twice: j-indexed (dSj, zero for
+// j > i inside the tiles it visits) and r-indexed (dQR). Both products are plain
 // contractions over one K axis, so one kernel runs them back to back into the
 // same accumulators: a 128-query x 128-dim output tile per (b, h), K range
 // j in [0, i0+128) then r in [S-1-i_last rounded down to 64, S) (rows below
@@ -82,42 +81,12 @@ __global__ __launch_bounds__(NT, BK == 64 ? 2 : 4) void flash_bwd_dq_kernel(Attn
     const bf16* B1 = (const bf16*)a.R + h * a.S_max * HSZ;
     const int64_t ke0 = min<int64_t>(S, i0 + BM);        // j range [0, ke0)
     const int64_t kb1 = (S - 1 - ilast) / BK * BK;       // r range [kb1, S)
-    const int n0 = (int)((ke0 + BK - 1) / BK), n1 = (int)((S - kb1 + BK - 1) / BK), nt = n0 + n1;
-    // dS-once mode (a.ds1): both A ranges come from dQR. Row i's j-view run
-    // starting at key j is the dQR run starting at r = S-1-i+j: a 16-B buffer
-    // load at a 2-byte aligned offset (the key / value pass stores the same
-    // runs with unaligned 16-B buffer stores). The descriptor covers this
-    // (b, h)'s S rows; every run stays inside its row (r <= S + 190 < ldr,
-    // flash_dqr_ld), where entries past the diagonal are zeros (the row
-    // padding), so no per-element mask is needed; rows past S read the
-    // dropped offset. The two ranges are walked interleaved (K-step t of each
-    // back to back): at equal t they read nearly the same dQR runs, so the
-    // second read of a run is mostly an L2 hit.
-    const __amdgpu_buffer_rsrc_t rA = [&] {
-        const uint64_t ab = (uint64_t)(dqr + rows);
-        void* p = (void*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ab >> 32)) << 32) |
-                          __builtin_amdgcn_readfirstlane((uint32_t)ab));
-        return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane((uint32_t)(S * ldr * 2)),
-                                                 0x00020000);
-    }();
-    const bool ds1 = a.ds1;
-    const int nmin = min(n0, n1);
+    const int n0 = (int)((ke0 + BK - 1) / BK), nt = n0 + (int)((S - kb1 + BK - 1) / BK);
 
     u32x4 ra[NU], rb[NU];
     auto load = [&](int t) {
-        bool s1;
-        int idx;
-        if (!ds1) {
-            s1 = t >= n0;
-            idx = s1 ? t - n0 : t;
-        } else if (t < 2 * nmin) {
-            s1 = t & 1;
-            idx = t >> 1;
-        } else {
-            s1 = n1 > n0;
-            idx = nmin + (t - 2 * nmin);
-        }
-        const int64_t k0 = s1 ? kb1 + (int64_t)idx * BK : (int64_t)idx * BK;
+        const bool s1 = t >= n0;
+        const int64_t k0 = s1 ? kb1 + (int64_t)(t - n0) * BK : (int64_t)t * BK;
         const int64_t kend = s1 ? S : ke0;
         const bf16* A = s1 ? A1 : A0;
         const bf16* B = s1 ? B1 : B0;
@@ -128,14 +97,8 @@ __global__ __launch_bounds__(NT, BK == 64 ? 2 : 4) void flash_bwd_dq_kernel(Attn
             {  // A [128 rows][BK k]
                 const int row = c / CPR, ch = c % CPR;
                 const int64_t gi = i0 + row, gk = k0 + ch * 8;
-                if (ds1) {
-                    const int64_t r = s1 ? gk : S - 1 - gi + gk;
-                    const uint32_t off = gi < S ? (uint32_t)((gi * ldr + r) * 2) : 0xFFFF0000u;
-                    ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rA, off, 0, 0);
-                } else {
-                    const int valid = gi < S ? (int)min<int64_t>(8, kend - gk) : 0;
-                    ra[u] = load_chunk(A + gi * ldr + gk, valid);
-                }
+                const int valid = gi < S ? (int)min<int64_t>(8, kend - gk) : 0;
+                ra[u] = load_chunk(A + gi * ldr + gk, valid);
             }
             {  // B [BK k][128 d]
                 const int kr = c >> 4, ch = c & 15;

@@ -218,11 +218,6 @@ static AttnArgs mk(int64_t B, int64_t S, int64_t H, int64_t hs, int64_t S_max, i
         return e && e[0] == '0' ? 0 : 1;
     }();
     a.fwd_prio = prio;
-    static const int ds1 = [] {
-        const char* e = getenv("MSQ_ATTN_DS1");
-        return e && e[0] == '1' ? 1 : 0;
-    }();
-    a.ds1 = ds1;
     return a;
 }
 

@@ -285,10 +285,7 @@ __global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, bf16* __restrict__ 
 // dQR / dSj row pitch: >= S + 128 so that the key/value pass's whole-row dS
 // stores of a 128-key block never reach the next row (dQR entries j > i fall
 // at r = S-1-i+j in [S, S+127): padding no reader touches)
-// (and >= S + 200 for the dq kernel's j-view reads of dQR rows in the dS-once
-// mode: a 128-query x 64-key step reads r = S-1-i+j up to S + 190 of a row,
-// which must stay inside that row's zero padding)
-int64_t flash_dqr_ld(int64_t S) { return (S + 200 + 7) / 8 * 8; }
+int64_t flash_dqr_ld(int64_t S) { return (S + 128 + 7) / 8 * 8; }
 
 // workspace: dQR bf16 [H][B][S][ldr] | dSj bf16 [H][B][S][ldr] | D f32 [B][H][S] | meta_ds f32 [B][H][8][8]
 //            | dR split-K partials f32 [ksplit][H][S][HS]
