@@ -17,9 +17,6 @@ struct AttnArgs {
     float keep_scale = 1.f;
     // XCD-aware block order in the flash kernels (xcd_blk3); MSQ_ATTN_NO_XCD=1 clears it
     int xcd = 1;
-    // forward: waves 4-7 (the second half of the 8-wave workgroup) at s_setprio 1
-    // for the whole loop (MI355X_MICROARCH 'Two waves per SIMD' item 4); MSQ_ATTN_FWD_PRIO=0 clears it
-    int fwd_prio = 1;
 };
 
 __device__ __forceinline__ float keep_bit(const AttnArgs& a, int64_t bh, int64_t i, int64_t j) {

@@ -176,7 +176,6 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
     u32x4 gk, gv, gr;
     uint32_t gm = 0u;
 #endif
-    if (a.fwd_prio && w >= 4) __builtin_amdgcn_s_setprio(1);
     for (int kt = 0; kt < nkt; ++kt) {
         const int j0 = kt * KB, cur = kt & 1;
         // one barrier per tile: it publishes tile kt (DMA'd in the prologue,

@@ -21,7 +21,6 @@ struct GemmArgs {
     // 2 = K is nseg segments of seg rows, tile rows m = r need k%seg >= seg-1-r (dR)
     int tri;
     int64_t seg;
-    int drorder;  // tri 2: M tiles of one K slice adjacent (gemm_bf16_tri, MSQ_DR_ORDER=0 clears it)
     // MSQ_EPI_BIAS_DROP_RESID: drop_base = drop_base(seed, site), keep iff bits >= drop_thr
     uint32_t drop_base, drop_thr;
     float drop_scale;

@@ -138,21 +138,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int tiles = g.tiles_m * g.tiles_n;
     int bid = xcd_remap(blockIdx.x, gridDim.x);
-    int kslice, bz;
-    if (g.tri == 2 && g.drorder) {
-        // dR product: the M tiles of one (head, K slice) adjacent, so the XCD
-        // running them reads that slice's Q rows (the B operand, shared by
-        // every M tile) from its L2 instead of once per M tile
-        const int t = bid % tiles, rest = bid / tiles;
-        kslice = rest % g.ksplit;
-        bz = rest / g.ksplit;
-        bid = t;
-    } else {
-        kslice = bid % g.ksplit;  // slices of one tile are adjacent (same XCD group)
-        bid /= g.ksplit;
-        bz = bid / tiles;
-        bid -= bz * tiles;
-    }
+    const int kslice = bid % g.ksplit;  // slices of one tile are adjacent (same XCD group)
+    bid /= g.ksplit;
+    const int bz = bid / tiles;
+    bid -= bz * tiles;
     // grouped ordering: 8 M-tiles share each sweep over N (L2 reuse of B)
     const int GROUP = 8;
     const int per_group = GROUP * g.tiles_n;
@@ -458,11 +447,6 @@ int gemm_bf16_tri(int tri, int64_t seg, int ta, int tb, int64_t M, int64_t N, in
     g.vec = 0;
     g.tri = tri;
     g.seg = seg;
-    static const int drorder = [] {
-        const char* e = getenv("MSQ_DR_ORDER");
-        return e && e[0] == '0' ? 0 : 1;
-    }();
-    g.drorder = drorder;
     g.ksplit = 1;
     g.kper = ((K + BK - 1) / BK) * BK;
     // tri 2: split the segments over blocks (gemm_bf16_tri_ksplit)
