@@ -121,6 +121,8 @@ bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dt
 // persistent 256 tile (forward / dX products: no ACCUM, one batch, N % 8 == 0,
 // 16-B aligned C / aux / bias); false when it does not apply
 bool gemm256p_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s);
+// whether gemm256p_launch would take this product
+bool gemm256p_applies(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype);
 // persistent tile with the column-sum partials of gemm256_colsum_launch (g.cs_ws set,
 // reduced by the caller); false when it does not apply
 bool gemm256p_colsum_launch(GemmArgs g, int ta, int tb, int epi, int aux_dtype, hipStream_t s);

@@ -626,13 +626,19 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
             return (!nop && gemm256p_launch(a, ta, tb, epilogue, c_dtype, aux_dtype, s)) ||
                    gemm256_launch(a, ta, tb, epilogue, c_dtype, aux_dtype, wsb, s);
         };
-        // wave quantisation: M = B*S rows rarely divide by 256 (32 x 2054 =
-        // 256.75 tiles), and the partial last row of 256 tiles alone would
-        // take one more full round of the 256 tile on a few CUs. Run the
-        // whole 256-row tiles there and the tail rows with the 128 tile.
+        // wave quantisation of the per-tile kernel: M = B*S rows rarely divide
+        // by 256 (32 x 2054 = 256.75 tiles), and the partial last row of 256
+        // tiles alone would take one more full round of the 256 tile on a few
+        // CUs. Run the whole 256-row tiles there and the tail rows with the 128
+        // tile. The persistent kernel takes the partial tiles itself (measured
+        // 0.6 ms per step faster than this split at cfg 2; MSQ_GEMM_TAIL=1
+        // splits anyway).
         GemmArgs p = g;
         const bool split = batch == 1 && epilogue != MSQ_EPI_ACCUM && M % 256 != 0 && M > 256 &&
-                           !getenv("MSQ_GEMM_NOTAIL") && gemm256_plan(p, ta, tb, epilogue) &&
+                           !getenv("MSQ_GEMM_NOTAIL") &&
+                           (nop || getenv("MSQ_GEMM_TAIL") ||
+                            !gemm256p_applies(g, ta, tb, epilogue, c_dtype, aux_dtype)) &&
+                           gemm256_plan(p, ta, tb, epilogue) &&
                            (int64_t)p.tiles_m * p.tiles_n % 256 != 0 &&
                            (int64_t)p.tiles_m * p.tiles_n % 256 <= p.tiles_n;
         if (split) {

@@ -477,6 +477,10 @@ static bool p_prepare(GemmArgs& g, int ta, int tb, int epi, int c_dtype, int aux
     return true;
 }
 
+bool gemm256p_applies(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype) {
+    return p_prepare(g, ta, tb, epi, c_dtype, aux_dtype);
+}
+
 bool gemm256p_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s) {
     if (!p_prepare(g, ta, tb, epi, c_dtype, aux_dtype)) return false;
     if (c_dtype == MSQ_BF16) dispatch_p<bf16>(g, ta, tb, epi, aux_dtype, s);
