@@ -17,8 +17,6 @@ struct AttnArgs {
     float keep_scale = 1.f;
     // XCD-aware block order in the flash kernels (xcd_blk3); MSQ_ATTN_NO_XCD=1 clears it
     int xcd = 1;
-    // forward: waves 4-7 defer each key tile's P.V to the next tile (stagger); MSQ_ATTN_FWD_STAGGER=0 clears it
-    int fwd_stagger = 1;
 };
 
 __device__ __forceinline__ float keep_bit(const AttnArgs& a, int64_t bh, int64_t i, int64_t j) {

@@ -213,11 +213,6 @@ static AttnArgs mk(int64_t B, int64_t S, int64_t H, int64_t hs, int64_t S_max, i
         return e && e[0] == '1' ? 0 : 1;
     }();
     a.xcd = xcd;
-    static const int stagger = [] {
-        const char* e = getenv("MSQ_ATTN_FWD_STAGGER");
-        return e && e[0] == '0' ? 0 : 1;
-    }();
-    a.fwd_stagger = stagger;
     return a;
 }
 

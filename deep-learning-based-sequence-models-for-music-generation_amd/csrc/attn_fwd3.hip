@@ -23,9 +23,7 @@ using namespace attn;
 
 constexpr int NT = 512;
 constexpr int QB = 256, KB = 32, NCH = 10, RING = NCH * KB, SCR = 52;
-// V is triple-buffered: the staggered waves 4-7 read tile t-1's V while tile
-// t+1's is being loaded
-constexpr int O_K = 0, O_V = 2 * KB * 256, O_R = O_V + 3 * KB * 256, O_S = O_R + RING * 256;
+constexpr int O_K = 0, O_V = 2 * KB * 256, O_R = 4 * KB * 256, O_S = O_R + RING * 256;
 constexpr int O_M = O_S + 8 * 16 * SCR * 4;
 constexpr int O_D = O_M + 64 * 4;  // dropout keep words of the block's 256 queries, 2 tiles
 constexpr int LDS_BYTES = O_D + 2 * QB * 4;
@@ -178,28 +176,8 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
     u32x4 gk, gv, gr;
     uint32_t gm = 0u;
 #endif
-    // stagger (MI355X_MICROARCH 'Two waves per SIMD' item 9): waves 4-7 issue
-    // the P.V MFMAs of tile t at the start of tile t+1, so on each SIMD one
-    // wave's softmax VALU meets its partner's MFMAs instead of both waves
-    // running the same phase together. The accumulator sees the same
-    // operations in the same order (rescale by alpha(t) before P(t).V(t)),
-    // so the output is bitwise unchanged. MSQ_ATTN_FWD_STAGGER=0 turns it off.
-    const bool defer = a.fwd_stagger && w >= 4;
-    bf16x8 ppf[2] = {(bf16x8){}, (bf16x8){}};
-    auto pv = [&](const char* cV, const bf16x8 (&p)[2]) {
-#pragma unroll
-        for (int n = 0; n < 8; ++n) {
-            const bf16x8 vfr = cat8(tr_read(cV, vqo[n]), tr_read(cV, 4096 + vqo[n]));
-            if (LAB & 8) {
-                asm volatile("" ::"v"(vfr), "v"(p[0]), "v"(p[1]));
-            } else {
-                oacc[0][n] = mfma(vfr, p[0], oacc[0][n]);
-                oacc[1][n] = mfma(vfr, p[1], oacc[1][n]);
-            }
-        }
-    };
     for (int kt = 0; kt < nkt; ++kt) {
-        const int j0 = kt * KB, cur = kt & 1, vb = kt % 3;
+        const int j0 = kt * KB, cur = kt & 1;
         // one barrier per tile: it publishes tile kt (DMA'd in the prologue,
         // or written by every wave at the end of tile kt-1) and releases tile
         // kt-1's buffers
@@ -225,15 +203,14 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
         if (kt + 1 < nkt && !(LAB & 16)) {
             const int j1 = j0 + KB, c = kt + NCH - 1, r0 = rb0 + c * KB;
             dma32(rq, smem + O_K + (cur ^ 1) * KB * 256, offK, lrow, (uint32_t)j1 * ldq2, 0, S - j1, w);
-            dma32(rq, smem + O_V + ((kt + 1) % 3) * KB * 256, offV, lrow, (uint32_t)j1 * ldq2, 0, S - j1, w);
+            dma32(rq, smem + O_V + (cur ^ 1) * KB * 256, offV, lrow, (uint32_t)j1 * ldq2, 0, S - j1, w);
             dma32(rr, sR + (c % NCH) * KB * 256, offR, lrow, (uint32_t)(r0 * HS * 2), -r0, S - r0, w);
             stage_m(kt + 1, cur ^ 1);
         }
 #endif
         if (live) {
             const char* cK = smem + O_K + cur * KB * 256;
-            const char* cV = smem + O_V + vb * KB * 256;
-            if (defer && kt > 0) pv(smem + O_V + ((kt + 2) % 3) * KB * 256, ppf);  // tile kt-1
+            const char* cV = smem + O_V + cur * KB * 256;
             // S^T[key][query] = K . Q^T
             f32x4 sacc[2][2];
 #pragma unroll
@@ -345,18 +322,22 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
                 l_part[q2] += ps;
             }
             // O^T[d][query] += V^T[d][key] . P^T[key][query]
-            if (defer) {
-                ppf[0] = pf[0];
-                ppf[1] = pf[1];
-            } else {
-                pv(cV, pf);
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+                const bf16x8 vfr = cat8(tr_read(cV, vqo[n]), tr_read(cV, 4096 + vqo[n]));
+                if (LAB & 8) {
+                    asm volatile("" ::"v"(vfr), "v"(pf[0]), "v"(pf[1]));
+                } else {
+                    oacc[0][n] = mfma(vfr, pf[0], oacc[0][n]);
+                    oacc[1][n] = mfma(vfr, pf[1], oacc[1][n]);
+                }
             }
         }
 #if FWD3_REGSTAGE
         if (kt + 1 < nkt && !(LAB & 16)) {
             const int c = kt + NCH - 1;
             *(u32x4*)(smem + O_K + (cur ^ 1) * KB * 256 + w * 1024 + lane * 16) = gk;
-            *(u32x4*)(smem + O_V + ((kt + 1) % 3) * KB * 256 + w * 1024 + lane * 16) = gv;
+            *(u32x4*)(smem + O_V + (cur ^ 1) * KB * 256 + w * 1024 + lane * 16) = gv;
             *(u32x4*)(sR + (c % NCH) * KB * 256 + w * 1024 + lane * 16) = gr;
             if (DROP && w < 4) *(uint32_t*)(smem + O_D + (cur ^ 1) * QB * 4 + w * 256 + lane * 4) = gm;
         }
@@ -364,7 +345,6 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
     }
 
     if (!live) return;
-    if (defer && nkt > 0) pv(smem + O_V + ((nkt - 1) % 3) * KB * 256, ppf);  // the last tile
 #pragma unroll
     for (int q2 = 0; q2 < 2; ++q2) {
         const int iq = iw + 16 * q2 + il;
