@@ -452,9 +452,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the decode and Mamba legs")
     ap.add_argument("--overlap", action="store_true",
-                    help="weight-gradient GEMMs on a second stream (default: main stream; measured no faster, "
-                         "and per-class times then sum to the step)")
-    ap.add_argument("--serial", action="store_true", help="the default (kept for old command lines)")
+                    help="weight-gradient GEMMs on a second stream: the default (kept for old command lines)")
+    ap.add_argument("--serial", action="store_true",
+                    help="weight-gradient GEMMs on the main stream (per-class times then sum to the step)")
+    ap.add_argument("--class-steps", type=int, default=3,
+                    help="with the second stream, the per-class table comes from this many extra steps "
+                         "run serially after the timed ones (concurrent kernels inflate each other's times)")
     ap.add_argument("--only", choices=["mamba"], default=None,
                     help="run only the cfg 3 Mamba train leg (--steps timed steps after one warm-up; PMC passes)")
     ap.add_argument("--dry-run", action="store_true",
@@ -485,7 +488,8 @@ def main():
         return
     cfg = TransformerConfig(n_layer=args.layers, block_len=args.seq, precision="bf16", dropout=args.dropout)
     model = Transformer(cfg).to(dev)
-    model.engine.overlap_dw = args.overlap
+    overlap = not args.serial
+    model.engine.overlap_dw = overlap
     step = TrainStep(model)
     data = iter(SyntheticMIDI(args.batch, args.seq, dev, rank))
 
@@ -497,7 +501,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    timer.on = True
+    timer.on = not overlap
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step(*next(data))
@@ -515,7 +519,24 @@ def main():
     value = tokens / el
     ms_step = el / args.steps * 1e3
     fpt = flops_per_token(cfg, args.seq)
-    classes = timer.table(args.steps)
+    if overlap:
+        # per-class kernel times from serial steps: on two streams the weight-
+        # gradient GEMMs share the CUs with the main stream's kernels and both
+        # sides' event intervals stretch
+        model.engine.overlap_dw = False
+        timer.on = True
+        ncls = max(1, args.class_steps)
+        for _ in range(ncls):
+            step(*next(data))
+        torch.cuda.synchronize()
+        timer.on = False
+        model.engine.overlap_dw = True
+        classes = timer.table(ncls)
+        class_src = (f"{ncls} steps after the timed ones with the weight-gradient GEMMs on the main "
+                     "stream (the timed steps run them on a second stream)")
+    else:
+        classes = timer.table(args.steps)
+        class_src = "the timed steps (serial)"
     timer.rec.clear()
     loss_last = round(float(loss.item()), 4)
 
@@ -551,7 +572,8 @@ def main():
             "data": "synthetic grammar-cycled MIDI tokens, random-init weights",
             "config": {"workload": "configs/transformer default (d=1024, h=8, L=8, V=17914) train step, "
                                    f"filtered CE + Adam, dropout={args.dropout}"
-                                   + (", weight-gradient GEMMs on a second stream" if args.overlap else ""),
+                                   + (", weight-gradient GEMMs on a second stream" if overlap else
+                                      ", serial backward"),
                        "model": "Transformer", "global_batch": args.batch * world, "seq_len": args.seq,
                        "parallelism": f"dp{world}"},
             "model_tflops": round(value * fpt / 1e12, 1),
@@ -565,6 +587,7 @@ def main():
                          "traffic_source": "profiles/r3/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
                                            "passes of this step, bytes per class launch)"},
             "classes": classes,
+            "classes_source": class_src,
         }
         out.update(extra)
         if world == 1 and not args.no_cpu_baseline:

@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/$tag
 if [ "$which" != mamba ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 240 rocprofv3 --pmc $c --kernel-trace -d gpurun_out/$tag/$c -o run --output-format csv -- python -u bench.py --steps 3 --warmup 0 --no-cpu-baseline --no-extra > gpurun_out/$tag/$c.log 2>&1 || { echo "pass $c failed"; tail -5 gpurun_out/$tag/$c.log; exit 1; }
+    timeout -k 10 240 rocprofv3 --pmc $c --kernel-trace -d gpurun_out/$tag/$c -o run --output-format csv -- python -u bench.py --serial --steps 3 --warmup 0 --no-cpu-baseline --no-extra > gpurun_out/$tag/$c.log 2>&1 || { echo "pass $c failed"; tail -5 gpurun_out/$tag/$c.log; exit 1; }
   done
   python tools/pmc_traffic.py gpurun_out/$tag/FETCH_SIZE gpurun_out/$tag/WRITE_SIZE 3 gpurun_out/$tag/pmc_traffic.json > /dev/null && echo train ok || exit 1
 fi
