@@ -409,25 +409,40 @@ def decode_cached_leg(dev, rank, world, B=64, T=2048, K=32, steps=2):
                        "batch_per_gpu": B, "context": T, "new_tokens": K}}
 
 
-def mamba_leg(dev, rank, world, timer, steps=3, B=8, T=4096):
+def mamba_leg(dev, rank, world, timer, steps=3, B=8, T=4096, overlap=True, class_steps=3):
     """Config 3: models/mamba (d=1024, 10 Mamba2 layers) train step at
-    T=4096, B=8 per GPU, bf16; per-class table (SSD scan on HBM bytes)."""
+    T=4096, B=8 per GPU, bf16; per-class table (SSD scan on HBM bytes). With
+    overlap (the engine's default two-stream backward) the class table comes
+    from class_steps one-stream steps after the timed ones, as for cfg 2."""
     from midiseq.mamba import Mamba
     m = Mamba(precision="bf16").to(dev)
+    m.engine.overlap_dw = overlap
     st = TrainStep(m)
     data = iter(SyntheticMIDI(B, T, dev, rank, n_batches=2))
     for _ in range(1):
         st(*next(data))
     timer.rec.clear()
-    timer.on = True
+    timer.on = not overlap
     el = timed(lambda: st(*next(data)), steps, 0, world, dev)
     timer.on = False
-    table = timer.table(steps)
+    ncls = steps
+    if overlap:
+        m.engine.overlap_dw = False
+        ncls = max(1, class_steps)
+        timer.on = True
+        for _ in range(ncls):
+            st(*next(data))
+        torch.cuda.synchronize()
+        timer.on = False
+    table = timer.table(ncls)
+    timer.rec.clear()
     del st, m
     tok_s = world * B * T * steps / el
     fpt = 3.0 * 174e6  # SURVEY.md §8(d) cfg 3: 174 MFLOP per token forward
     out = {"value": round(tok_s, 1), "unit": "tokens/s", "ms_per_step": round(el / steps * 1e3, 3),
            "mfu": round(tok_s / world * fpt / 1e12 / PEAK_BF16_TFLOPS, 4), "classes": table,
+           "classes_source": (f"{ncls} one-stream steps after the timed ones (the timed steps run the weight-"
+                              "gradient GEMMs on a second stream)") if overlap else "the timed steps (serial)",
            "config": {"workload": "cfg 3 Mamba train step (filtered CE + Adam)", "batch_per_gpu": B, "seq_len": T}}
     if "ssd_fwd" in table:
         r = table["ssd_fwd"]
@@ -481,7 +496,7 @@ def main():
     if args.only == "mamba":
         timer = ClassTimer()
         L.TAP = timer
-        r = mamba_leg(dev, rank, world, timer, steps=args.steps)
+        r = mamba_leg(dev, rank, world, timer, steps=args.steps, overlap=not args.serial, class_steps=args.class_steps)
         L.TAP = None
         if rank == 0:
             print(json.dumps({"mamba_train": r}), flush=True)
@@ -548,7 +563,7 @@ def main():
         torch.cuda.empty_cache()
         extra["decode_cached"] = decode_cached_leg(dev, rank, world)
         torch.cuda.empty_cache()
-        extra["mamba_train"] = mamba_leg(dev, rank, world, timer)
+        extra["mamba_train"] = mamba_leg(dev, rank, world, timer, overlap=overlap, class_steps=args.class_steps)
         torch.cuda.empty_cache()
         extra["mamba_decode"] = mamba_decode_leg(dev, rank, world)
         extra["midi_decode"] = midi_decode_leg(dev, rank, world)

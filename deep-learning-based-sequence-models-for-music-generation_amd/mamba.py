@@ -171,6 +171,8 @@ class DecodeCache:
 class MambaEngine:
     # decode steps replay a captured HIP graph (MSQ_NO_STEP_GRAPH=1: eager launches)
     step_graphs = not os.environ.get("MSQ_NO_STEP_GRAPH")
+    # weight-gradient GEMMs of the backward on a second stream (see backward())
+    overlap_dw = os.environ.get("MSQ_SERIAL_DW") != "1"
 
     def __init__(self, cfg: MambaConfig, flat):
         self.cfg = cfg
@@ -330,27 +332,41 @@ class MambaEngine:
         s = stream()
         hook = self.layer_grad_ready
         dl = dlogits[:, :V]
-        ops.gemm(dlogits, A.f, ta=True, tb=True, out=G["lm_w"], epilogue=L.EPI_ACCUM)  # pad columns are 0
-        if not head_bias_done:
-            ops.colsum(dl, G["lm_b"][:V], accumulate=True)
+        # weight gradients on a second stream (ops.SideStream; the
+        # Transformer's backward does the same): the out_proj / in_proj dW
+        # GEMMs (MFMA-bound) overlap the HBM-bound gated-norm / SSD / conv
+        # backward of the main stream. Shared buffers they read: gin (gxb in
+        # bf16, else gx) and dzx, each overwritten one step later only after
+        # the side launch that reads it (before_write). MSQ_SERIAL_DW=1 or
+        # overlap_dw = False keeps one stream.
+        sd = ops.SideStream(self.device, self.overlap_dw, hook)
+
+        def lm_w():
+            ops.gemm(dlogits, A.f, ta=True, tb=True, out=G["lm_w"], epilogue=L.EPI_ACCUM)  # pad columns are 0
+            if not head_bias_done:
+                ops.colsum(dl, G["lm_b"][:V], accumulate=True)
+        sd.run("dlogits", lm_w)
         Wt = self.transposed_weights()
         dx_gemm(dlogits, W, Wt, "lm_w", Bw["df"])
         gx, gxb = Bw["gx"], Bw["gxb"]
         gx.zero_()
         ops.layernorm_bwd(gx, Bw["df"], A.xlast, A.stf[0], A.stf[1], P["lnf_w"], G["lnf_w"], G["lnf_b"],
                           seg=(T, N_META))
-        if hook is not None:
-            hook("head")
+        sd.layer_done("head")
         # per-chunk state gradients of the bf16 SSD backward (msq_mamba_ssd_bwd_workspace)
         ssd_ws = ops.workspace(L.lib().msq_mamba_ssd_bwd_workspace(Bb, Ll, H), self.device, "ssd_bwd")
+        bf = self.act == torch.bfloat16
+        gin = gxb if bf else gx
         for l in reversed(range(cfg.n_layers)):
-            gin = gxb
-            if self.act == torch.bfloat16:
+            if bf:
+                sd.before_write("gin")
                 ops.cast(gxb, gx)
-            else:
-                gin = gx
-            ops.gemm(gin, A.yn[l], ta=True, tb=True, out=G[f"{l}.out_w"], epilogue=L.EPI_ACCUM)
+
+            def out_w(l=l):
+                ops.gemm(gin, A.yn[l], ta=True, tb=True, out=G[f"{l}.out_w"], epilogue=L.EPI_ACCUM)
+            sd.run("gin", out_w)
             dx_gemm(gin, W, Wt, f"{l}.out_w", Bw["dyn"])
+            sd.before_write("dzx")
             call("msq_mamba_gnorm_bwd", ptr(Bw["dy"]), ptr(Bw["dzx"]), ptr(A.y[l]), di, ptr(A.zx[l]), cfg.d_in_proj,
                  dtc, ptr(P[f"{l}.norm_w"]), ptr(A.rstd[l]), ptr(Bw["dyn"]), di, ptr(G[f"{l}.norm_w"]), M, di, s)
             call("msq_mamba_ssd_bwd", ptr(Bw["dxc"]), cfg.conv_dim, ptr(Bw["dzx"]), ptr(Bw["dy"]), di,
@@ -360,13 +376,17 @@ class MambaEngine:
             call("msq_mamba_conv_bwd", ptr(Bw["dzx"]), ptr(Bw["dxc"]), cfg.conv_dim, ptr(A.zx[l]), cfg.d_in_proj, dtc,
                  ptr(P[f"{l}.conv_w"]), ptr(P[f"{l}.conv_b"]), ptr(G[f"{l}.conv_w"]), ptr(G[f"{l}.conv_b"]), Bb, Ll,
                  di, H, s)
-            ops.gemm(Bw["dzx"], A.xa[l], ta=True, tb=True, out=G[f"{l}.in_w"], epilogue=L.EPI_ACCUM)
+
+            def in_w(l=l):
+                ops.gemm(Bw["dzx"], A.xa[l], ta=True, tb=True, out=G[f"{l}.in_w"], epilogue=L.EPI_ACCUM)
+            sd.run("dzx", in_w)
+            if not bf:
+                sd.before_write("gin")  # gx: read by this layer's out_proj dW
             dx_gemm(Bw["dzx"], W, Wt, f"{l}.in_w", gx)
-            if hook is not None:
-                hook(l)
+            sd.layer_done(l)
         ops.embed_bwd(G["tok_emb"], G["meta_emb"], gx, idx, meta)
-        if hook is not None:
-            hook(-1)
+        sd.layer_done(-1)
+        sd.finish()
 
 
 class _MambaFn(torch.autograd.Function):

@@ -112,6 +112,66 @@ def gemm_bias_colstats(A, W, out, bias, part):
     return True
 
 
+class SideStream:
+    """Weight-gradient launches of a backward on a second stream. Weight
+    gradients (dW GEMMs, bias column sums of a bf16 branch gradient) feed only
+    the optimizer, never the next layer's backward, so they can overlap the
+    dX / normalisation / mixer chain of the main stream: each side launch
+    waits for the main stream's producer of its inputs (an event recorded at
+    the call), and the main stream waits for the side launch that reads a
+    shared buffer before it overwrites it (before_write). With enabled=False
+    every launch runs in place on the current stream (the one-stream
+    backward). `hook` (the DDP bucket callback) runs on the side stream after
+    both streams' work of the bucket (layer_done); finish() joins the streams
+    before the optimizer reads the gradients."""
+
+    _streams = {}
+
+    def __init__(self, device, enabled, hook=None):
+        self.main = torch.cuda.current_stream(device)
+        self.enabled = enabled
+        if enabled and device not in SideStream._streams:
+            SideStream._streams[device] = torch.cuda.Stream(device=device)
+        self.side = SideStream._streams[device] if enabled else self.main
+        self.hook = hook
+        self.pending = {}
+
+    def run(self, key, fn):
+        if not self.enabled:
+            fn()
+            return
+        ev = torch.cuda.Event()
+        ev.record(self.main)
+        self.side.wait_event(ev)
+        with torch.cuda.stream(self.side):
+            fn()
+        done = torch.cuda.Event()
+        done.record(self.side)
+        self.pending[key] = done
+
+    def before_write(self, key):
+        ev = self.pending.pop(key, None)
+        if ev is not None:
+            self.main.wait_event(ev)
+
+    def layer_done(self, key):
+        if self.hook is None:
+            return
+        if not self.enabled:
+            self.hook(key)
+            return
+        ev = torch.cuda.Event()
+        ev.record(self.main)
+        self.side.wait_event(ev)
+        with torch.cuda.stream(self.side):  # the bucket's event then follows both streams
+            self.hook(key)
+
+    def finish(self):
+        if self.enabled:
+            self.main.wait_stream(self.side)  # the optimizer reads every gradient
+        self.pending.clear()
+
+
 _WS = {}
 
 

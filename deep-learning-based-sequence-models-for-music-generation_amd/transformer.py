@@ -558,41 +558,8 @@ class TransformerEngine:
         # main stream waits for the side stream before it overwrites a buffer
         # the side still reads (gb / gb2 / dh / dqkv, one layer of slack).
         ov = Bw["gb2"] is not None and getattr(self, "overlap_dw", False)
-        main = torch.cuda.current_stream(self.device)
-        if ov and getattr(self, "_dw_stream", None) is None:
-            self._dw_stream = torch.cuda.Stream(device=self.device)
-        side = self._dw_stream if ov else main
-        pending = {}
-
-        def on_side(key, fn):
-            if not ov:
-                fn()
-                return
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                fn()
-            done = torch.cuda.Event()
-            done.record(side)
-            pending[key] = done
-
-        def before_write(key):
-            ev = pending.pop(key, None)
-            if ev is not None:
-                main.wait_event(ev)
-
-        def layer_done(key):
-            if hook is None:
-                return
-            if not ov:
-                hook(key)
-                return
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
-            with torch.cuda.stream(side):  # the bucket's event then follows both streams
-                hook(key)
+        sd = ops.SideStream(self.device, ov, hook)
+        on_side, before_write, layer_done = sd.run, sd.before_write, sd.layer_done
 
         # lm_head (model_transformer.py:147,161)
         def lm_w():
@@ -662,8 +629,7 @@ class TransformerEngine:
             layer_done(l)
         ops.embed_bwd(G["tok_emb"], G["meta_emb"], gres, idx, meta)
         layer_done(-1)
-        if ov:
-            main.wait_stream(side)  # the optimizer reads every gradient
+        sd.finish()
 
     def bucket_ranges(self):
         from .ddp import transformer_buckets
