@@ -1098,6 +1098,213 @@ __global__ __launch_bounds__(256) void rpass_kernel(float* __restrict__ U, const
     }
 }
 
+// ---------------------------------------------------------------- fused chunk scans
+// state + pass (forward) and uterm + rpass (backward) as one launch each: one
+// workgroup per (b, h) walks its chunks in order and keeps the running state (or
+// the running exit gradient) in the MFMA accumulator registers, so the per-chunk
+// S_c / U_c never go to HBM -- the only state traffic is the one fp32 store of
+// every chunk's entry state H_c (exit gradient dH_c) that `out` / `grad` read.
+// The next chunk's x / B (dY / C) and dt rows are loaded into registers while the
+// current chunk's product runs. Same arithmetic as state -> pass (uterm -> rpass):
+// H_{c+1} = e^{cum_last_c} H_c + S_c with S_c from the same MFMA sequence.
+__device__ __forceinline__ Chunk chunk_at(const MambaArgs& a, int64_t bh, int c) {
+    Chunk k;
+    k.b = bh / a.nheads;
+    k.h = bh % a.nheads;
+    k.c = c;
+    k.t0 = (int64_t)c * Q;
+    k.nval = (int)min<int64_t>(Q, a.L - k.t0);
+    return k;
+}
+__device__ __forceinline__ float dt_raw(const MambaArgs& a, const Chunk& k, const bf16* zx, int tid) {
+    return tid < k.nval ? (float)zx[(k.b * a.L + k.t0 + tid) * a.ldz + a.d_inner + a.conv_dim + k.h] : 0.f;
+}
+// wave 0: dt = softplus(raw + bias) (0 past nval), inclusive scan of dt A
+__device__ __forceinline__ void dt_cum_raw(const Chunk& k, float raw, float bias, float A, float* sdt, float* scum,
+                                           int tid) {
+    if (tid < 64) {
+        const float d = tid < k.nval ? softplus(raw + bias) : 0.f;
+        sdt[tid] = d;
+        float v = d * A;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const float u = __shfl_up(v, o, 64);
+            if (tid >= o) v += u;
+        }
+        scum[tid] = v;
+    }
+}
+
+// Two chunks' rows are in flight ahead of the one being multiplied (register sets
+// alternate with the chunk parity), and the LDS image / dt / cum rows are double
+// buffered, so one iteration has two barriers and no load on its critical path.
+constexpr size_t SCAN_LDS = 2 * (IMG + 512);
+__global__ __launch_bounds__(256) void scan_fwd_kernel(MambaArgs a, const bf16* __restrict__ xc,
+                                                       const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
+                                                       const float* __restrict__ A_log, float* __restrict__ states,
+                                                       float* __restrict__ clast, int nch, float* __restrict__ fin) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t bh = blockIdx.x;
+    const int64_t h = bh % a.nheads;
+    const float A = -expf(A_log[h]), bias = dt_bias[h];
+    const int rb = 32 * (w >> 1), cb = 32 * (w & 1);
+    f32x4 H[2][2];
+    zero22(H);
+    u32x4 x0[2], b0[2], x1[2], b1[2];
+    float r0 = 0.f, r1 = 0.f;
+    auto load = [&](int c, u32x4 (&xr)[2], u32x4 (&br)[2], float& raw) {
+        const Chunk k = chunk_at(a, bh, c);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            xr[u] = ld_chunk(a, k, xc, h * P, tid + 256 * u);
+            br[u] = ld_chunk(a, k, xc, a.d_inner, tid + 256 * u);
+        }
+        raw = dt_raw(a, k, zx, tid);
+    };
+    // chunk c from its register set; then that set takes chunk c + 2
+    auto body = [&](int c, u32x4 (&xr)[2], u32x4 (&br)[2], float& raw) {
+        const Chunk k = chunk_at(a, bh, c);
+        char* sXB = smem + (c & 1) * (IMG + 512);  // half 0: dt x e^{cum_last - cum_s} [s][p]; half 1: B [s][n]
+        float* sdt = (float*)(sXB + IMG);
+        float* scum = sdt + 64;
+        float* st = states + (bh * nch + c) * (int64_t)(P * N);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                *(f32x4*)(st + (rb + 16 * i + (lane & 15)) * N + cb + 16 * j + 4 * (lane >> 4)) = H[i][j];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = tid + 256 * u;
+            *(u32x4*)(sXB + offd(e >> 3, 8 + (e & 7))) = br[u];
+        }
+        dt_cum_raw(k, raw, bias, A, sdt, scum, tid);
+        __syncthreads();
+        const float cl = scum[k.nval - 1];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = tid + 256 * u, row = e >> 3;
+            const float f = row < k.nval ? sdt[row] * expf(cl - scum[row]) : 0.f;
+            float v[8];
+            unpack8(xr[u], v);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] *= f;
+            *(u32x4*)(sXB + offd(row, e & 7)) = pack8(v);
+        }
+        if (c + 2 < nch) load(c + 2, xr, br, raw);
+        __syncthreads();
+        f32x4 acc[2][2];
+        zero22(acc);
+        mm<true, true>(acc, sXB, 0, sXB, 1, rb, cb, lane);  // [p][n] = sum_s X[s][p] B[s][n]
+        const float ecl = expf(cl);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) H[i][j][r] = ecl * H[i][j][r] + acc[i][j][r];
+        if (tid == 0) clast[bh * nch + c] = cl;
+        // no trailing barrier: chunk c + 1 writes the other buffer, and chunk c + 2
+        // writes this one only after every wave has passed chunk c + 1's first barrier
+    };
+    load(0, x0, b0, r0);
+    if (nch > 1) load(1, x1, b1, r1);
+    for (int c = 0; c < nch; c += 2) {
+        body(c, x0, b0, r0);
+        if (c + 1 < nch) body(c + 1, x1, b1, r1);
+    }
+    if (fin) {
+        float* fs = fin + bh * (int64_t)(P * N);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                *(f32x4*)(fs + (rb + 16 * i + (lane & 15)) * N + cb + 16 * j + 4 * (lane >> 4)) = H[i][j];
+    }
+}
+
+// reverse: dH = 0; for c = last .. 0: U[c] = dH (exit gradient); dH = e^{cum_last_c} dH + U_c
+__global__ __launch_bounds__(256) void scan_bwd_kernel(MambaArgs a, const bf16* __restrict__ xc,
+                                                       const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
+                                                       const float* __restrict__ A_log, const float* __restrict__ dY,
+                                                       int64_t ldy, float* __restrict__ U, int nch) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t bh = blockIdx.x;
+    const int64_t h = bh % a.nheads;
+    const float A = -expf(A_log[h]), bias = dt_bias[h];
+    const int rb = 32 * (w >> 1), cb = 32 * (w & 1);
+    f32x4 D[2][2];
+    zero22(D);
+    u32x4 c0[2], c1[2];
+    f32x4 y0[2][2], y1[2][2];
+    float r0 = 0.f, r1 = 0.f;
+    auto load = [&](int c, u32x4 (&cr)[2], f32x4 (&yr)[2][2], float& raw) {
+        const Chunk k = chunk_at(a, bh, c);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
+            cr[u] = ld_chunk(a, k, xc, a.d_inner + N, e);
+            yr[u][0] = yr[u][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (row < k.nval) {
+                const float* src = dY + (k.b * a.L + k.t0 + row) * ldy + h * P + ch * 8;
+                yr[u][0] = *(const f32x4*)src;
+                yr[u][1] = *(const f32x4*)(src + 4);
+            }
+        }
+        raw = dt_raw(a, k, zx, tid);
+    };
+    auto body = [&](int c, u32x4 (&cr)[2], f32x4 (&yr)[2][2], float& raw) {
+        const Chunk k = chunk_at(a, bh, c);
+        char* sYC = smem + (c & 1) * (IMG + 512);  // half 0: e^{cum_t} dY [t][p]; half 1: C [t][n]
+        float* sdt = (float*)(sYC + IMG);
+        float* scum = sdt + 64;
+        float* dst = U + (bh * nch + c) * (int64_t)(P * N);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                *(f32x4*)(dst + (rb + 16 * i + (lane & 15)) * N + cb + 16 * j + 4 * (lane >> 4)) = D[i][j];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = tid + 256 * u;
+            *(u32x4*)(sYC + offd(e >> 3, 8 + (e & 7))) = cr[u];
+        }
+        dt_cum_raw(k, raw, bias, A, sdt, scum, tid);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
+            const float et = expf(scum[row]);
+            float v[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = yr[u][0][q] * et, v[4 + q] = yr[u][1][q] * et;
+            *(u32x4*)(sYC + offd(row, ch)) = pack8(v);
+        }
+        const float cl = scum[k.nval - 1];
+        if (c - 2 >= 0) load(c - 2, cr, yr, raw);
+        __syncthreads();
+        f32x4 acc[2][2];
+        zero22(acc);
+        mm<true, true>(acc, sYC, 0, sYC, 1, rb, cb, lane);  // [p][n] = sum_t Ys[t][p] C[t][n]
+        const float ecl = expf(cl);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) D[i][j][r] = ecl * D[i][j][r] + acc[i][j][r];
+    };
+    // chunks walk down from nch - 1; the parity of (nch - 1 - c) picks the register set
+    load(nch - 1, c0, y0, r0);
+    if (nch > 1) load(nch - 2, c1, y1, r1);
+    for (int c = nch - 1; c >= 0; c -= 2) {
+        body(c, c0, y0, r0);
+        if (c - 1 >= 0) body(c - 1, c1, y1, r1);
+    }
+}
+
 template <typename TD>
 __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* __restrict__ xc,
                                                       const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
@@ -1394,12 +1601,19 @@ extern "C" int msq_mamba_ssd_fwd_state(float* y, int64_t ldy, float* states, flo
     if (dtype == MSQ_BF16 && !getenv("MSQ_MAMBA_SSD_V1")) {
         float* clast = states + B * nheads * nch * (int64_t)(P * N);
         const dim3 gch((unsigned)(B * nheads * nch));
-        allow_lds(ssd2::state_kernel, ssd2::STATE_LDS);
         allow_lds(ssd2::out_kernel, ssd2::OUT_LDS);
-        hipLaunchKernelGGL(ssd2::state_kernel, gch, dim3(256), ssd2::STATE_LDS, s, a, (const bf16*)xc,
-                           (const bf16*)zxbcdt, dt_bias, A_log, states, clast, nch);
-        hipLaunchKernelGGL(ssd2::pass_kernel, dim3((unsigned)((B * nheads * P * N + 255) / 256)), dim3(256), 0, s,
-                           states, clast, B * nheads, nch, final_state);
+        if (getenv("MSQ_MAMBA_SSD_3K")) {  // per-chunk state kernel + separate pass (round-2 form)
+            allow_lds(ssd2::state_kernel, ssd2::STATE_LDS);
+            hipLaunchKernelGGL(ssd2::state_kernel, gch, dim3(256), ssd2::STATE_LDS, s, a, (const bf16*)xc,
+                               (const bf16*)zxbcdt, dt_bias, A_log, states, clast, nch);
+            hipLaunchKernelGGL(ssd2::pass_kernel, dim3((unsigned)((B * nheads * P * N + 255) / 256)), dim3(256), 0,
+                               s, states, clast, B * nheads, nch, final_state);
+        } else {
+            allow_lds(ssd2::scan_fwd_kernel, ssd2::SCAN_LDS);
+            hipLaunchKernelGGL(ssd2::scan_fwd_kernel, dim3((unsigned)(B * nheads)), dim3(256), ssd2::SCAN_LDS, s, a,
+                               (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, states, clast, nch,
+                               final_state);
+        }
         hipLaunchKernelGGL(ssd2::out_kernel, gch, dim3(256), ssd2::OUT_LDS, s, a, (const bf16*)xc,
                            (const bf16*)zxbcdt, dt_bias, A_log, D, y, ldy, states, nch);
         MSQ_LAUNCH_CHECK();
@@ -1484,12 +1698,18 @@ extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, cons
         float* U = (float*)workspace;
         float* dbc = U + B * nheads * nch * (int64_t)(P * N);
         const dim3 gch((unsigned)(B * nheads * nch));
-        allow_lds(ssd2::uterm_kernel, ssd2::UTERM_LDS);
         allow_lds(ssd2::grad_kernel<bf16>, ssd2::GRAD_LDS);
-        hipLaunchKernelGGL(ssd2::uterm_kernel, gch, dim3(256), ssd2::UTERM_LDS, s, a, (const bf16*)xc,
-                           (const bf16*)zxbcdt, dt_bias, A_log, dY, ldy, U, nch);
-        hipLaunchKernelGGL(ssd2::rpass_kernel, dim3((unsigned)((B * nheads * P * N + 255) / 256)), dim3(256), 0, s,
-                           U, clast, B * nheads, nch);
+        if (getenv("MSQ_MAMBA_SSD_3K")) {
+            allow_lds(ssd2::uterm_kernel, ssd2::UTERM_LDS);
+            hipLaunchKernelGGL(ssd2::uterm_kernel, gch, dim3(256), ssd2::UTERM_LDS, s, a, (const bf16*)xc,
+                               (const bf16*)zxbcdt, dt_bias, A_log, dY, ldy, U, nch);
+            hipLaunchKernelGGL(ssd2::rpass_kernel, dim3((unsigned)((B * nheads * P * N + 255) / 256)), dim3(256), 0,
+                               s, U, clast, B * nheads, nch);
+        } else {
+            allow_lds(ssd2::scan_bwd_kernel, ssd2::SCAN_LDS);
+            hipLaunchKernelGGL(ssd2::scan_bwd_kernel, dim3((unsigned)(B * nheads)), dim3(256), ssd2::SCAN_LDS, s, a,
+                               (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, dY, ldy, U, nch);
+        }
         hipLaunchKernelGGL(ssd2::grad_kernel<bf16>, gch, dim3(256), ssd2::GRAD_LDS, s, a, (const bf16*)xc,
                            (const bf16*)zxbcdt, dt_bias, A_log, D, dY, ldy, states, U, dxc, dbc, (bf16*)dzxbcdt,
                            gA_log, gD, gdt_bias, nch);

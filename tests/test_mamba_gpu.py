@@ -99,3 +99,33 @@ def test_mamba_two_stream_backward_matches_single_stream(precision):
     assert torch.isfinite(g0).all()
     err = (g0 - g1).abs().max().item()
     assert err <= 1e-6 * g0.abs().max().item(), err
+
+
+@pytest.mark.parametrize("T", [200, 700])
+def test_mamba_fused_scan_matches_three_kernel_path(T, monkeypatch):
+    """The fused chunk scans (scan_fwd: state + pass, scan_bwd: uterm + rpass,
+    one workgroup per (b, h) walking its chunks with the running state in
+    registers) give the same loss and gradients as the per-chunk kernels plus
+    the separate pass launches (MSQ_MAMBA_SSD_3K=1); T = 200 ends on a partial
+    chunk (8 rows)."""
+    from midiseq.train_parallel import TrainStep
+    rng = np.random.default_rng(11)
+    B = 2
+    w = torch.from_numpy(np.stack([grammar_tokens(rng, REAL, T + 1) for _ in range(B)])).cuda()
+    meta = torch.tensor([[519, 279, 202, 202, 202, 178], [432, 277, 202, 202, 202, 173]]).cuda()
+    grads, losses = [], []
+    for three in (True, False):
+        if three:
+            monkeypatch.setenv("MSQ_MAMBA_SSD_3K", "1")
+        else:
+            monkeypatch.delenv("MSQ_MAMBA_SSD_3K", raising=False)
+        m, _ = build(256, 2, "bf16")
+        st = TrainStep(m)
+        losses.append(float(st(w[:, :-1], w[:, 1:], meta)))
+        torch.cuda.synchronize()
+        grads.append(st.grads.clone())
+    g0, g1 = grads
+    assert torch.isfinite(g1).all()
+    assert abs(losses[0] - losses[1]) <= 1e-6 * abs(losses[0]), losses
+    err = (g0 - g1).abs().max().item()
+    assert err <= 1e-5 * g0.abs().max().item(), err

@@ -24,7 +24,10 @@ tag = sys.argv[1]
 d = json.load(open(f"gpurun_out/ab/{tag}.json"))
 c = d.get("classes", {})
 top = sorted(c.items(), key=lambda kv: -kv[1]["ms_per_step"])[:9]
-print(tag, "[" + sys.argv[2] + "]", d["ms_per_step"], d.get("loss_last"), " ".join(f"{k}={v['ms_per_step']}" for k, v in top))
+if "ms_per_step" in d:
+    print(tag, "[" + sys.argv[2] + "]", d["ms_per_step"], d.get("loss_last"), " ".join(f"{k}={v['ms_per_step']}" for k, v in top))
+else:
+    print(tag, "[" + sys.argv[2] + "]")
 for k in ("decode_cached", "mamba_train", "mamba_decode", "decode"):
     if k in d:
         e = d[k]
