@@ -1116,14 +1116,28 @@ __device__ __forceinline__ Chunk chunk_at(const MambaArgs& a, int64_t bh, int c)
     k.nval = (int)min<int64_t>(Q, a.L - k.t0);
     return k;
 }
-__device__ __forceinline__ float dt_raw(const MambaArgs& a, const Chunk& k, const bf16* zx, int tid) {
-    return tid < k.nval ? (float)zx[(k.b * a.L + k.t0 + tid) * a.ldz + a.d_inner + a.conv_dim + k.h] : 0.f;
+// raw dt bits (bf16 in the low half): converted only where dt_cum_raw uses them, so
+// the prefetch does not wait for its own load (a conversion right after the load does)
+__device__ __forceinline__ unsigned dt_raw(const MambaArgs& a, const Chunk& k, const bf16* zx, int tid) {
+    const unsigned short* zu = (const unsigned short*)zx;
+    return tid < k.nval ? (unsigned)zu[(k.b * a.L + k.t0 + tid) * a.ldz + a.d_inner + a.conv_dim + k.h] : 0u;
+}
+// unmasked forms for the scan kernels: rows past nval read the chunk's last valid
+// row (finite data; the consumer zeroes its weight), so no branch skips a load
+__device__ __forceinline__ u32x4 ld_clamped(const MambaArgs& a, const Chunk& k, const bf16* xc, int64_t col0, int e) {
+    const int row = min(e >> 3, k.nval - 1), ch = e & 7;
+    return *(const u32x4*)(xc + (k.b * a.L + k.t0 + row) * a.ldxc + col0 + ch * 8);
+}
+__device__ __forceinline__ unsigned dt_raw_clamped(const MambaArgs& a, const Chunk& k, const bf16* zx, int tid) {
+    const unsigned short* zu = (const unsigned short*)zx;
+    const int row = min(tid & 63, k.nval - 1);
+    return (unsigned)zu[(k.b * a.L + k.t0 + row) * a.ldz + a.d_inner + a.conv_dim + k.h];
 }
 // wave 0: dt = softplus(raw + bias) (0 past nval), inclusive scan of dt A
-__device__ __forceinline__ void dt_cum_raw(const Chunk& k, float raw, float bias, float A, float* sdt, float* scum,
-                                           int tid) {
+__device__ __forceinline__ void dt_cum_raw(const Chunk& k, unsigned raw, float bias, float A, float* sdt,
+                                           float* scum, int tid) {
     if (tid < 64) {
-        const float d = tid < k.nval ? softplus(raw + bias) : 0.f;
+        const float d = tid < k.nval ? softplus(__uint_as_float(raw << 16) + bias) : 0.f;
         sdt[tid] = d;
         float v = d * A;
 #pragma unroll
@@ -1152,28 +1166,33 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(MambaArgs a, const bf16* 
     f32x4 H[2][2];
     zero22(H);
     u32x4 x0[2], b0[2], x1[2], b1[2];
-    float r0 = 0.f, r1 = 0.f;
-    auto load = [&](int c, u32x4 (&xr)[2], u32x4 (&br)[2], float& raw) {
-        const Chunk k = chunk_at(a, bh, c);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            xr[u] = ld_chunk(a, k, xc, h * P, tid + 256 * u);
-            br[u] = ld_chunk(a, k, xc, a.d_inner, tid + 256 * u);
-        }
-        raw = dt_raw(a, k, zx, tid);
-    };
-    // chunk c from its register set; then that set takes chunk c + 2
-    auto body = [&](int c, u32x4 (&xr)[2], u32x4 (&br)[2], float& raw) {
-        const Chunk k = chunk_at(a, bh, c);
-        char* sXB = smem + (c & 1) * (IMG + 512);  // half 0: dt x e^{cum_last - cum_s} [s][p]; half 1: B [s][n]
-        float* sdt = (float*)(sXB + IMG);
-        float* scum = sdt + 64;
-        float* st = states + (bh * nch + c) * (int64_t)(P * N);
+    unsigned r0 = 0u, r1 = 0u;
+    auto store_state = [&](float* st) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
                 *(f32x4*)(st + (rb + 16 * i + (lane & 15)) * N + cb + 16 * j + 4 * (lane >> 4)) = H[i][j];
+    };
+    auto load = [&](int c, u32x4 (&xr)[2], u32x4 (&br)[2], unsigned& raw) {
+        const Chunk k = chunk_at(a, bh, c);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            xr[u] = ld_clamped(a, k, xc, h * P, tid + 256 * u);
+            br[u] = ld_clamped(a, k, xc, a.d_inner, tid + 256 * u);
+        }
+        raw = dt_raw_clamped(a, k, zx, tid);
+    };
+    // chunk c from its register set; then that set takes chunk c + 2
+    // c == nch (the odd tail of the unrolled pair) repeats chunk nch - 1 without
+    // updating H: every trip runs both bodies, so no branch skips a load or store
+    auto body = [&](int c0, u32x4 (&xr)[2], u32x4 (&br)[2], unsigned& raw) {
+        const bool valid = c0 < nch;
+        const int c = min(c0, nch - 1);
+        const Chunk k = chunk_at(a, bh, c);
+        char* sXB = smem + (c & 1) * (IMG + 512);  // half 0: dt x e^{cum_last - cum_s} [s][p]; half 1: B [s][n]
+        float* sdt = (float*)(sXB + IMG);
+        float* scum = sdt + 64;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int e = tid + 256 * u;
@@ -1192,7 +1211,7 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(MambaArgs a, const bf16* 
             for (int q = 0; q < 8; ++q) v[q] *= f;
             *(u32x4*)(sXB + offd(row, e & 7)) = pack8(v);
         }
-        if (c + 2 < nch) load(c + 2, xr, br, raw);
+        load(min(c + 2, nch - 1), xr, br, raw);  // unconditional: the wait counts stay static
         __syncthreads();
         f32x4 acc[2][2];
         zero22(acc);
@@ -1203,24 +1222,21 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(MambaArgs a, const bf16* 
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) H[i][j][r] = ecl * H[i][j][r] + acc[i][j][r];
-        if (tid == 0) clast[bh * nch + c] = cl;
+                for (int r = 0; r < 4; ++r) H[i][j][r] = valid ? ecl * H[i][j][r] + acc[i][j][r] : H[i][j][r];
+        // the entry state of chunk c + 1 (or the final state) is stored right after
+        // the update: H is next overwritten one chunk later, so the wait the store's
+        // source registers need does not also wait for the next loads
+        store_state(c + 1 < nch ? states + (bh * nch + c + 1) * (int64_t)(P * N) : fin + bh * (int64_t)(P * N));
+        clast[bh * nch + c] = cl;  // every lane, same value: no divergent branch around a store
         // no trailing barrier: chunk c + 1 writes the other buffer, and chunk c + 2
         // writes this one only after every wave has passed chunk c + 1's first barrier
     };
+    store_state(states + bh * nch * (int64_t)(P * N));  // H_0 = 0
     load(0, x0, b0, r0);
-    if (nch > 1) load(1, x1, b1, r1);
+    load(min(1, nch - 1), x1, b1, r1);
     for (int c = 0; c < nch; c += 2) {
         body(c, x0, b0, r0);
-        if (c + 1 < nch) body(c + 1, x1, b1, r1);
-    }
-    if (fin) {
-        float* fs = fin + bh * (int64_t)(P * N);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-                *(f32x4*)(fs + (rb + 16 * i + (lane & 15)) * N + cb + 16 * j + 4 * (lane >> 4)) = H[i][j];
+        body(c + 1, x1, b1, r1);
     }
 }
 
@@ -1228,7 +1244,8 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(MambaArgs a, const bf16* 
 __global__ __launch_bounds__(256) void scan_bwd_kernel(MambaArgs a, const bf16* __restrict__ xc,
                                                        const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
                                                        const float* __restrict__ A_log, const float* __restrict__ dY,
-                                                       int64_t ldy, float* __restrict__ U, int nch) {
+                                                       int64_t ldy, float* __restrict__ U, int nch,
+                                                       float* __restrict__ dh0) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t bh = blockIdx.x;
@@ -1239,33 +1256,33 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(MambaArgs a, const bf16* 
     zero22(D);
     u32x4 c0[2], c1[2];
     f32x4 y0[2][2], y1[2][2];
-    float r0 = 0.f, r1 = 0.f;
-    auto load = [&](int c, u32x4 (&cr)[2], f32x4 (&yr)[2][2], float& raw) {
-        const Chunk k = chunk_at(a, bh, c);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
-            cr[u] = ld_chunk(a, k, xc, a.d_inner + N, e);
-            yr[u][0] = yr[u][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-            if (row < k.nval) {
-                const float* src = dY + (k.b * a.L + k.t0 + row) * ldy + h * P + ch * 8;
-                yr[u][0] = *(const f32x4*)src;
-                yr[u][1] = *(const f32x4*)(src + 4);
-            }
-        }
-        raw = dt_raw(a, k, zx, tid);
-    };
-    auto body = [&](int c, u32x4 (&cr)[2], f32x4 (&yr)[2][2], float& raw) {
-        const Chunk k = chunk_at(a, bh, c);
-        char* sYC = smem + (c & 1) * (IMG + 512);  // half 0: e^{cum_t} dY [t][p]; half 1: C [t][n]
-        float* sdt = (float*)(sYC + IMG);
-        float* scum = sdt + 64;
-        float* dst = U + (bh * nch + c) * (int64_t)(P * N);
+    unsigned r0 = 0u, r1 = 0u;
+    auto store_d = [&](float* dst) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
                 *(f32x4*)(dst + (rb + 16 * i + (lane & 15)) * N + cb + 16 * j + 4 * (lane >> 4)) = D[i][j];
+    };
+    auto load = [&](int c, u32x4 (&cr)[2], f32x4 (&yr)[2][2], unsigned& raw) {
+        const Chunk k = chunk_at(a, bh, c);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
+            cr[u] = ld_clamped(a, k, xc, a.d_inner + N, e);
+            const float* src = dY + (k.b * a.L + k.t0 + min(row, k.nval - 1)) * ldy + h * P + ch * 8;
+            yr[u][0] = *(const f32x4*)src;  // rows past nval: zeroed where used
+            yr[u][1] = *(const f32x4*)(src + 4);
+        }
+        raw = dt_raw_clamped(a, k, zx, tid);
+    };
+    auto body = [&](int c0, u32x4 (&cr)[2], f32x4 (&yr)[2][2], unsigned& raw) {
+        const bool valid = c0 >= 0;  // c0 == -1: the odd tail, chunk 0 again without an update
+        const int c = max(c0, 0);
+        const Chunk k = chunk_at(a, bh, c);
+        char* sYC = smem + (c & 1) * (IMG + 512);  // half 0: e^{cum_t} dY [t][p]; half 1: C [t][n]
+        float* sdt = (float*)(sYC + IMG);
+        float* scum = sdt + 64;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int e = tid + 256 * u;
@@ -1276,14 +1293,14 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(MambaArgs a, const bf16* 
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
-            const float et = expf(scum[row]);
+            const float et = row < k.nval ? expf(scum[row]) : 0.f;
             float v[8];
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = yr[u][0][q] * et, v[4 + q] = yr[u][1][q] * et;
             *(u32x4*)(sYC + offd(row, ch)) = pack8(v);
         }
         const float cl = scum[k.nval - 1];
-        if (c - 2 >= 0) load(c - 2, cr, yr, raw);
+        load(max(c - 2, 0), cr, yr, raw);  // unconditional: the wait counts stay static
         __syncthreads();
         f32x4 acc[2][2];
         zero22(acc);
@@ -1294,14 +1311,17 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(MambaArgs a, const bf16* 
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) D[i][j][r] = ecl * D[i][j][r] + acc[i][j][r];
+                for (int r = 0; r < 4; ++r) D[i][j][r] = valid ? ecl * D[i][j][r] + acc[i][j][r] : D[i][j][r];
+        // exit gradient of chunk c - 1 (chunk 0's entry gradient goes to the scratch dh0)
+        store_d(c > 0 ? U + (bh * nch + c - 1) * (int64_t)(P * N) : dh0 + bh * (int64_t)(P * N));
     };
     // chunks walk down from nch - 1; the parity of (nch - 1 - c) picks the register set
+    store_d(U + (bh * nch + nch - 1) * (int64_t)(P * N));  // the last chunk's exit gradient is 0
     load(nch - 1, c0, y0, r0);
-    if (nch > 1) load(nch - 2, c1, y1, r1);
+    load(max(nch - 2, 0), c1, y1, r1);
     for (int c = nch - 1; c >= 0; c -= 2) {
         body(c, c0, y0, r0);
-        if (c - 1 >= 0) body(c - 1, c1, y1, r1);
+        body(c - 1, c1, y1, r1);
     }
 }
 
@@ -1569,8 +1589,9 @@ constexpr size_t STATE_LDS = IMG + 512, OUT_LDS = 3 * IMG + 512;
 
 extern "C" size_t msq_mamba_states_size(int64_t B, int64_t L, int64_t nheads) {
     // chunk-entry states [B][H][nch][P][N] + per-chunk decay sums cum_last [B][H][nch]
+    // + [B][H][P][N] final state written when the caller passes none
     const int64_t nch = (L + Q - 1) / Q;
-    return (size_t)B * nheads * nch * (P * N + 1) * sizeof(float);
+    return (size_t)B * nheads * (nch * (P * N + 1) + P * N) * sizeof(float);
 }
 
 #define MAMBA_CHECK()                                                                                         \
@@ -1610,6 +1631,7 @@ extern "C" int msq_mamba_ssd_fwd_state(float* y, int64_t ldy, float* states, flo
                                s, states, clast, B * nheads, nch, final_state);
         } else {
             allow_lds(ssd2::scan_fwd_kernel, ssd2::SCAN_LDS);
+            if (!final_state) final_state = clast + B * nheads * nch;  // scratch past cum_last
             hipLaunchKernelGGL(ssd2::scan_fwd_kernel, dim3((unsigned)(B * nheads)), dim3(256), ssd2::SCAN_LDS, s, a,
                                (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, states, clast, nch,
                                final_state);
@@ -1678,7 +1700,9 @@ extern "C" int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const float* y, int
 
 extern "C" size_t msq_mamba_ssd_bwd_workspace(int64_t B, int64_t L, int64_t nheads) {
     // per-chunk state gradients [B][H][nch][P][N] | per-head dB, dC rows [B*L][H][2N]
-    return (size_t)B * nheads * ((L + Q - 1) / Q) * P * N * sizeof(float) + (size_t)B * L * nheads * 2 * N * sizeof(float);
+    // + [B][H][P][N] scratch for the scan's gradient of the initial state
+    return (size_t)B * nheads * ((L + Q - 1) / Q) * P * N * sizeof(float) + (size_t)B * L * nheads * 2 * N * sizeof(float) +
+           (size_t)B * nheads * P * N * sizeof(float);
 }
 
 extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, const float* dY, int64_t ldy,
@@ -1708,7 +1732,8 @@ extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, cons
         } else {
             allow_lds(ssd2::scan_bwd_kernel, ssd2::SCAN_LDS);
             hipLaunchKernelGGL(ssd2::scan_bwd_kernel, dim3((unsigned)(B * nheads)), dim3(256), ssd2::SCAN_LDS, s, a,
-                               (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, dY, ldy, U, nch);
+                               (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, dY, ldy, U, nch,
+                               dbc + B * L * nheads * 2 * N);
         }
         hipLaunchKernelGGL(ssd2::grad_kernel<bf16>, gch, dim3(256), ssd2::GRAD_LDS, s, a, (const bf16*)xc,
                            (const bf16*)zxbcdt, dt_bias, A_log, D, dY, ldy, states, U, dxc, dbc, (bf16*)dzxbcdt,
