@@ -446,7 +446,7 @@ def mamba_leg(dev, rank, world, timer, steps=3, B=8, T=4096, overlap=True, class
            "config": {"workload": "cfg 3 Mamba train step (filtered CE + Adam)", "batch_per_gpu": B, "seq_len": T}}
     if "ssd_fwd" in table:
         r = table["ssd_fwd"]
-        out["roofline"] = {"kernel": "SSD scan forward (msq_mamba_ssd_fwd_state: state + pass + out kernels)",
+        out["roofline"] = {"kernel": "SSD scan forward (msq_mamba_ssd_fwd_state: fused chunk scan + out kernels)",
                            "bound": "hbm", "achieved": r["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
                            "frac": r["frac"], "traffic": pmc_traffic("ssd_fwd", "pmc_mamba_traffic.json"),
                            "avg_launch_ms": r["avg_launch_ms"], "algorithmic_bytes": int(r["work_per_launch"]),

@@ -959,7 +959,7 @@ __global__ __launch_bounds__(256) void out_kernel(MambaArgs a, const bf16* __res
                                                   const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
                                                   const float* __restrict__ A_log, const float* __restrict__ Dp,
                                                   float* __restrict__ y, int64_t ldy, const float* __restrict__ states,
-                                                  int nch) {
+                                                  int nch, float* __restrict__ clast) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sCB = smem;           // half 0: C [t][n];     half 1: B [s][n]
     char* sXH = smem + IMG;     // half 0: dt x [s][p];  half 1: H [p][n]
@@ -983,6 +983,7 @@ __global__ __launch_bounds__(256) void out_kernel(MambaArgs a, const bf16* __res
     }
     dt_cum(a, k, zx, dt_bias, A, sdt, scum, tid);
     __syncthreads();
+    if (tid == 0) clast[(k.b * a.nheads + k.h) * nch + k.c] = scum[k.nval - 1];  // for rpass
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         const int e = tid + 256 * u, row = e >> 3;
@@ -1227,7 +1228,6 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(MambaArgs a, const bf16* 
         // the update: H is next overwritten one chunk later, so the wait the store's
         // source registers need does not also wait for the next loads
         store_state(c + 1 < nch ? states + (bh * nch + c + 1) * (int64_t)(P * N) : fin + bh * (int64_t)(P * N));
-        clast[bh * nch + c] = cl;  // every lane, same value: no divergent branch around a store
         // no trailing barrier: chunk c + 1 writes the other buffer, and chunk c + 2
         // writes this one only after every wave has passed chunk c + 1's first barrier
     };
@@ -1637,7 +1637,7 @@ extern "C" int msq_mamba_ssd_fwd_state(float* y, int64_t ldy, float* states, flo
                                final_state);
         }
         hipLaunchKernelGGL(ssd2::out_kernel, gch, dim3(256), ssd2::OUT_LDS, s, a, (const bf16*)xc,
-                           (const bf16*)zxbcdt, dt_bias, A_log, D, y, ldy, states, nch);
+                           (const bf16*)zxbcdt, dt_bias, A_log, D, y, ldy, states, nch, clast);
         MSQ_LAUNCH_CHECK();
         return MSQ_OK;
     }
