@@ -368,6 +368,9 @@ def midi_decode_leg(dev, rank, world, B=64, L=4048, iters=50, cpu_rows=4):
     return out
 
 
+FULL_LEN = 2000  # cfg 5: scripts/generate.py --length 2000
+
+
 def decode_cached_leg(dev, rank, world, B=64, T=2048, K=32, steps=2):
     """Config 5, cached mode (a documented approximation, midiseq/generate.py):
     B=64 prompts of 2048 tokens per GPU (replicas), prefill = one exact
@@ -383,6 +386,9 @@ def decode_cached_leg(dev, rank, world, B=64, T=2048, K=32, steps=2):
                              mode="cached", return_tensor=True, group=_group(world))
     el_pre = timed(lambda: run(1), steps, 1, world, dev)
     el_all = timed(lambda: run(1 + K), steps, 1, world, dev)
+    # cfg 5's own length (scripts/generate.py --length 2000): one whole run,
+    # prefill included, so the window slides over every ring block
+    el_full = timed(lambda: run(FULL_LEN), 1, 0, world, dev)
     cfg = m.cfg
     del m
     ms_step = (el_all - el_pre) / (steps * K) * 1e3
@@ -405,6 +411,8 @@ def decode_cached_leg(dev, rank, world, B=64, T=2048, K=32, steps=2):
                          "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
                          "algorithmic_bytes_per_step": int(nbytes),
                          "bytes_model": "K/V ring L*B*(T+6)*d*2*2 + bf16 weights + incremental ring LSE (~30 B per (b, v)) + new row"},
+            "full_length": {"new_tokens": FULL_LEN, "s": round(el_full, 3),
+                            "new_tokens_per_s": round(world * B * FULL_LEN / el_full, 1)},
             "config": {"workload": "cfg 5 Transformer cached decode (KV ring, approximation of the exact window)",
                        "batch_per_gpu": B, "context": T, "new_tokens": K}}
 
