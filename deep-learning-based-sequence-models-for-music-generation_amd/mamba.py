@@ -23,6 +23,12 @@ from .transformer import TransformerEngine, _align, _select, dx_gemm
 D_STATE, D_CONV, HEADDIM = 64, 4, 64
 
 
+def _keep_casts():
+    """MSQ_MAMBA_CASTS=1: fp32 layer outputs / input gradients plus a cast
+    launch (the round-2 form; A/B switch)."""
+    return os.environ.get("MSQ_MAMBA_CASTS") == "1"
+
+
 @dataclass
 class MambaConfig:
     d_model: int = 1024
@@ -256,11 +262,18 @@ class MambaEngine:
                 cache.conv[l].copy_(zx.view(B, Ll, cfg.d_in_proj)[:, Ll - (D_CONV - 1):, di:di + cfg.conv_dim])
             call("msq_mamba_gnorm_fwd", ptr(yn), di, ptr(A.rstd[k]), ptr(y), di, ptr(zx), cfg.d_in_proj, dtc,
                  ptr(P[f"{l}.norm_w"]), M, di, float(cfg.norm_eps), s)
-            xo = A.xlast if l == cfg.n_layers - 1 else A.x[(l + 1) % 2]
-            ops.gemm(yn, W[f"{l}.out_w"], out=xo)
-            if l < cfg.n_layers - 1:
+            if l == cfg.n_layers - 1:
+                ops.gemm(yn, W[f"{l}.out_w"], out=A.xlast)
+            else:
                 xa = A.xa[l + 1] if save else A.xa[(l + 1) % 2]
-                ops.cast(xa, xo)
+                if xa.dtype != torch.float32 and not _keep_casts():
+                    # the next layer's bf16 input straight from the GEMM's fp32
+                    # accumulator: the same rounding as an fp32 row + cast
+                    ops.gemm(yn, W[f"{l}.out_w"], out=xa)
+                else:
+                    xo = A.x[(l + 1) % 2]
+                    ops.gemm(yn, W[f"{l}.out_w"], out=xo)
+                    ops.cast(xa, xo)
         ops.layernorm_fwd(A.xlast, P["lnf_w"], P["lnf_b"], out=A.f, mean=A.stf[0], rstd=A.stf[1], seg=(T, N_META))
         V = cfg.vocab_size
         # full V_pad rows (pad rows of lm_w / lm_b are zero): 16-B aligned rows, 256-tile eligible
@@ -357,10 +370,10 @@ class MambaEngine:
         ssd_ws = ops.workspace(L.lib().msq_mamba_ssd_bwd_workspace(Bb, Ll, H), self.device, "ssd_bwd")
         bf = self.act == torch.bfloat16
         gin = gxb if bf else gx
+        if bf:
+            sd.before_write("gin")
+            ops.cast(gxb, gx)
         for l in reversed(range(cfg.n_layers)):
-            if bf:
-                sd.before_write("gin")
-                ops.cast(gxb, gx)
 
             def out_w(l=l):
                 ops.gemm(gin, A.yn[l], ta=True, tb=True, out=G[f"{l}.out_w"], epilogue=L.EPI_ACCUM)
@@ -380,9 +393,14 @@ class MambaEngine:
             def in_w(l=l):
                 ops.gemm(Bw["dzx"], A.xa[l], ta=True, tb=True, out=G[f"{l}.in_w"], epilogue=L.EPI_ACCUM)
             sd.run("dzx", in_w)
-            if not bf:
-                sd.before_write("gin")  # gx: read by this layer's out_proj dW
-            dx_gemm(Bw["dzx"], W, Wt, f"{l}.in_w", gx)
+            sd.before_write("gin")  # gin: read by this layer's out_proj dW
+            # below layer 0 the next layer down reads only the bf16 copy: the dX
+            # GEMM rounds its fp32 accumulator straight into it (as gx + cast would)
+            direct = bf and l > 0 and not _keep_casts()
+            dx_gemm(Bw["dzx"], W, Wt, f"{l}.in_w", gxb if direct else gx)
+            if bf and l > 0 and not direct:
+                sd.before_write("gin")
+                ops.cast(gxb, gx)
             sd.layer_done(l)
         ops.embed_bwd(G["tok_emb"], G["meta_emb"], gx, idx, meta)
         sd.layer_done(-1)

@@ -129,3 +129,29 @@ def test_mamba_fused_scan_matches_three_kernel_path(T, monkeypatch):
     assert abs(losses[0] - losses[1]) <= 1e-6 * abs(losses[0]), losses
     err = (g0 - g1).abs().max().item()
     assert err <= 1e-5 * g0.abs().max().item(), err
+
+
+def test_mamba_direct_bf16_outputs_match_cast_path(monkeypatch):
+    """The out_proj forward and the in_proj input-gradient GEMMs round their
+    fp32 accumulators straight into the next layer's bf16 buffers; the
+    MSQ_MAMBA_CASTS=1 path writes fp32 and casts. Same rounding, so the loss
+    and gradients agree bit for bit (up to the per-head parameter atomics)."""
+    from midiseq.train_parallel import TrainStep
+    rng = np.random.default_rng(12)
+    B, T = 2, 300
+    w = torch.from_numpy(np.stack([grammar_tokens(rng, REAL, T + 1) for _ in range(B)])).cuda()
+    meta = torch.tensor([[519, 279, 202, 202, 202, 178], [432, 277, 202, 202, 202, 173]]).cuda()
+    grads, losses = [], []
+    for keep in (True, False):
+        if keep:
+            monkeypatch.setenv("MSQ_MAMBA_CASTS", "1")
+        else:
+            monkeypatch.delenv("MSQ_MAMBA_CASTS", raising=False)
+        m, _ = build(256, 3, "bf16")
+        st = TrainStep(m)
+        losses.append(float(st(w[:, :-1], w[:, 1:], meta)))
+        torch.cuda.synchronize()
+        grads.append(st.grads.clone())
+    assert losses[0] == losses[1], losses
+    err = (grads[0] - grads[1]).abs().max().item()
+    assert err <= 1e-6 * grads[0].abs().max().item(), err
