@@ -39,6 +39,7 @@ __device__ __forceinline__ float softplus(float x) { return x > 20.f ? x : log1p
 // block: 64 channels (lanes) x 4 waves, each wave a contiguous segment of CONV_SEG
 // steps with a sliding 4-tap window (one load per input element)
 constexpr int CONV_SEG = 64;
+constexpr int CONV_U = 8;
 template <typename T, typename TO>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(MambaArgs a, const T* __restrict__ zx, const float* __restrict__ w,
                                                        const float* __restrict__ bias, TO* __restrict__ out) {
@@ -58,14 +59,22 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(MambaArgs a, const T* __r
         const int64_t tt = t0 - 3 + k;
         win[k + 1] = tt >= 0 ? (float)src[tt * a.ldz] : 0.f;
     }
-    for (int64_t t = t0; t < t1; ++t) {
+    // CONV_U steps per batch: their loads are issued together (clamped to the
+    // segment, so no branch skips one), then the sliding window runs over them
+    for (int64_t tb = t0; tb < t1; tb += CONV_U) {
+        T xin[CONV_U];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) win[k] = win[k + 1];
-        win[3] = (float)src[t * a.ldz];
-        float acc = bc;
+        for (int u = 0; u < CONV_U; ++u) xin[u] = src[min(tb + u, t1 - 1) * a.ldz];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) acc += wk[k] * win[k];
-        dst[t * a.ldxc] = (TO)silu(acc);
+        for (int u = 0; u < CONV_U; ++u) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) win[k] = win[k + 1];
+            win[3] = (float)xin[u];
+            float acc = bc;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc += wk[k] * win[k];
+            if (tb + u < t1) dst[(tb + u) * a.ldxc] = (TO)silu(acc);
+        }
     }
 }
 
@@ -99,17 +108,31 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(MambaArgs a, const T* __r
             win[k + 1] = tt >= 0 ? (float)src[tt * a.ldz] : 0.f;
         }
         const int64_t tend = min(a.L, t1 + 3);
-        for (int64_t tau = t0; tau < t1 + 3; ++tau) {
+        // CONV_U steps per batch, their input / dout loads issued together
+        // (clamped to tend - 1: no branch skips a load)
+        for (int64_t tb = t0; tb < t1 + 3; tb += CONV_U) {
+        T xin[CONV_U];
+        float dyin[CONV_U];
+#pragma unroll
+        for (int u = 0; u < CONV_U; ++u) {
+            const int64_t tl = min(tb + u, tend - 1);
+            xin[u] = src[tl * a.ldz];
+            dyin[u] = dsrc[tl * ldd];
+        }
+#pragma unroll
+        for (int u = 0; u < CONV_U; ++u) {
+            const int64_t tau = tb + u;
+            if (tau >= t1 + 3) break;
 #pragma unroll
             for (int k = 0; k < 3; ++k) win[k] = win[k + 1], dp[k] = dp[k + 1];
             float d = 0.f;
             if (tau < tend) {
-                win[3] = (float)src[tau * a.ldz];
+                win[3] = (float)xin[u];
                 float pre = bc;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) pre += wk[k] * win[k];
                 const float sg = sigm(pre);
-                d = dsrc[tau * ldd] * sg * (1.f + pre * (1.f - sg));
+                d = dyin[u] * sg * (1.f + pre * (1.f - sg));
                 if (tau < t1) {
                     gb += d;
 #pragma unroll
@@ -127,6 +150,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(MambaArgs a, const T* __r
                 for (int k = 0; k < 4; ++k) di += wk[k] * dp[3 - k];
                 dzx[(b * a.L + t) * a.ldz + a.d_inner + c] = (TD)di;
             }
+        }
         }
     }
 #pragma unroll
