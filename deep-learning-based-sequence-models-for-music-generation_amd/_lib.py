@@ -68,6 +68,7 @@ SIGNATURES = {
     "msq_transpose_bf16": (_i, [_p, _i64, _p, _i64, _i64, _i64, _p]),
     "msq_gemm_colstats_bytes": (_sz, [_i64, _i64]),
     "msq_gemm_bias_colstats": (_i, [_i, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _p]),
+    "msq_gemm_bias_colstats_applies": (_i, [_i, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _i64]),
     "msq_filtered_ce_bias_part": (_i, [_p, _p, _i64, _p, _p, _i, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
                                        _i64, _i64, _f, _p, _p, _i64, _i64, _p, _p]),
     "msq_gemm_set_route": (_i, [_i]),

@@ -55,6 +55,10 @@ int flash_bwd_kv3(const AttnArgs& a, const float* lse, const float* Dv, const bf
 // wave per SIMD; -1 if unsupported (ldr < S + 128, n_meta > 8, > 4 GB)
 int flash_bwd_kv4(const AttnArgs& a, const float* lse, const float* Dv, const bf16* dout, int64_t ldo, bf16* dqkv,
                   int64_t ldd, bf16* dqr, bf16* dsj, int64_t ldr, float* meta_ds, hipStream_t s);
+// v5 key/value pass (attn_bwd5.hip): software-pipelined v4; dsj == nullptr
+// writes dS only r-indexed (dqr); -1 if unsupported
+int flash_bwd_kv5(const AttnArgs& a, const float* lse, const float* Dv, const bf16* dout, int64_t ldo, bf16* dqkv,
+                  int64_t ldd, bf16* dqr, bf16* dsj, int64_t ldr, hipStream_t s);
 // dq = dSj.K + dQR.R into the q columns of dqkv (attn_dq.hip)
 void flash_bwd_dq(const AttnArgs& a, const bf16* dsj, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd,
                   hipStream_t s);

@@ -1,0 +1,565 @@
+// Relative-position flash attention backward, key/value-major pass, v5
+// (model_transformer.py:54-90 differentiated; P recomputed from the forward's
+// row log-sum-exp):
+//   P_ij  = exp(scale (q_i.k_j + q_i.R[S-1-i+j]) - lse_i)
+//   dS_ij = P_ij (dO_i.v_j m_ij ks - D_i) scale,   D_i = dO_i.O_i
+//   dV_j  = ks sum_i P_ij m_ij dO_i,  dK_j = sum_i dS_ij q_i   (accumulated here)
+//   (m_ij the dropout keep bit, ks = 1/(1-p); m = 1, ks = 1 without dropout)
+//   dS written r-indexed, dQR[h][b][i][r = S-1-i+j] (the dq kernel reads its
+//   j-view, the dR product its r-view), and with DSJ also j-indexed (dSj).
+//   The metadata-block entries j > i (i < j < n_meta: keys every query sees)
+//   are masked here like the rest of the upper triangle; flash_bwd_meta_kernel
+//   adds their dK / dV / dq / dR terms.
+//
+// Geometry as v4 (attn_bwd4.hip): one workgroup = 4 waves, one per SIMD, =
+// 128 keys of one (b, h); a wave owns 32 keys on the lanes of
+// v_mfma_f32_32x32x16; K / V rows stay in AGPRs as the B operands of S = Q.K^T
+// and dP = dO.V^T, whose accumulators (key on the lane) are the B operands of
+// dV^T += dO^T.P and dK^T += Q^T.dS; the relative term is a 64-row R window
+// per wave and 32-query tile, skewed onto the keys by one ds_bpermute per
+// register; Q / dO / R arrive by LDS-DMA in chunk-major images.
+//
+// What is new: a one-wave-per-SIMD kernel has nothing to hide its VALU behind
+// but its own MFMAs, and v4 ran the score products, the skew + softmax and the
+// dV / dK products one after the other (~5,400 cycles per wave-tile against
+// 1,536 of MFMA). v5 software-pipelines the query tiles. Iteration t:
+//   * barrier (tile t+1 landed; tile t-1's buffers free), then the 32 MFMAs
+//     of A(t+1) = S / QR / dP of tile t+1, with the skew + softmax of tile t
+//     (whose accumulators A(t) finished one iteration earlier) cut into 32
+//     snippets, one per MFMA gap, and the staging DMA of tile t+1+DEPTH and
+//     the row stores of dS(t-1) in the first gaps;
+//   * the 16 MFMAs of C(t) = dV / dK of tile t beside the dS(t) staging writes.
+// Two accumulator sets ping-pong (the loop is unrolled twice so their
+// registers are fixed); each (MFMA, snippet) pair is fenced by a sched_barrier.
+#include <type_traits>
+#include <utility>
+
+#include "attn_tiles.h"
+
+namespace {
+using namespace attn;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int NT = 256;
+constexpr int DEPTH = 2;          // tiles in flight beyond the one A(t+1) reads
+constexpr int NB = DEPTH + 2;     // Q / dO / row-constant buffers
+constexpr int KB = 128, QT = 32;  // keys per workgroup, queries per tile
+constexpr int NCH = 5 + DEPTH;    // R ring (32-row chunks)
+constexpr int TILE = QT * 256;    // 32 rows x 128 bf16
+constexpr int O_Q = 0, O_O = NB * TILE, O_R = 2 * NB * TILE;
+constexpr int O_L = O_R + NCH * TILE;       // lse log2(e), D scale: NB tiles x 2 x 64 floats
+constexpr int O_D = O_L + NB * 2 * 64 * 4;  // dropout keep words of the 128 keys, NB tiles
+constexpr int T_PITCH = 272, T_BYTES = QT * T_PITCH;  // dS staging: 32 rows x 128 keys bf16
+constexpr int O_T = O_D + NB * KB * 4;
+constexpr int LDS_BYTES = O_T + 2 * T_BYTES;
+// vector memory ops per wave and iteration: NDMA staging pieces (Q 2, dO 2,
+// one 4-byte piece: lse / D on waves 0-1, keep words or a dummy on waves 2-3,
+// R 2), then the dS row stores (2, or 4 with the j-indexed copy)
+constexpr int NDMA = 7;
+constexpr uint32_t OOB = 0xFFFF0000u;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void* p = (void*)(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* dst_wave, uint32_t vo) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_char*)dst_wave, 16, vo, 0, 0, 0);
+}
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rs, char* dst_wave, uint32_t vo) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_char*)dst_wave, 4, vo, 0, 0, 0);
+}
+__device__ __forceinline__ void bar() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+#ifndef KV5_NOSB
+#define SB() __builtin_amdgcn_sched_barrier(0)
+#else
+#define SB() ((void)0)
+#endif
+
+// MFMAs as asm statements so the register classes stay fixed (AGPRs: dK^T /
+// dV^T and the K / V operands; VGPRs: the per-tile S, dP, QR accumulators that
+// the softmax reads). Hazards hipcc does not pad inside asm
+// (cdna_hip_programming.md §5.7 item 2): an operand may be a fresh VALU result
+// (s_nop 1 first); a D register is read by VALU only a whole pipeline stage
+// (>= 16 MFMAs) after its last MFMA, or after drain4.
+__device__ __forceinline__ void mfma_acc_a(f32x16& acc, bf16x8 a, bf16x8 b) {  // D = C in AGPRs
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_first_va(f32x16& acc, bf16x8 a, const bf16x8& b) {  // D = A.B (B in AGPRs)
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "a"(b));
+}
+__device__ __forceinline__ void mfma_acc_va(f32x16& acc, bf16x8 a, const bf16x8& b) {
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b));
+}
+__device__ __forceinline__ void mfma_first_vv(f32x16& acc, bf16x8 a, bf16x8 b) {
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_acc_vv(f32x16& acc, bf16x8 a, bf16x8 b) {
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void drain4(f32x16& a, f32x16& b, f32x16& c, f32x16& d) {
+    asm volatile("s_nop 15\n\ts_nop 7" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+__device__ __forceinline__ void drain_a(f32x16 (&x)[4], f32x16 (&y)[4]) {
+    asm volatile("s_nop 15\n\ts_nop 7" : "+a"(x[0]), "+a"(x[1]), "+a"(x[2]), "+a"(x[3]), "+a"(y[0]), "+a"(y[1]),
+                 "+a"(y[2]), "+a"(y[3]));
+}
+// query row of accumulator register e in lane half hh (32x32 C/D map)
+__device__ __forceinline__ int acc_row(int e, int hh) { return (e & 3) + 8 * (e >> 2) + 4 * hh; }
+__device__ __forceinline__ float and_f(float x, int m) { return __int_as_float(__float_as_int(x) & m); }
+
+struct Acc {
+    f32x16 s, dp, q0, q1;  // S = Q.K^T, dP = dO.V^T, QR window blocks 0 / 1 (query rows x keys)
+};
+
+// l2 = lse * log2(e), dsc = D * scale (per query row, flash_bwd_pre_vec_kernel)
+template <bool DROP, bool DSJ>
+__global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const float* __restrict__ lse,
+                                                              const float* __restrict__ Dv,
+                                                              const bf16* __restrict__ dout, int64_t ldo,
+                                                              bf16* __restrict__ dqkv, int64_t ldd,
+                                                              bf16* __restrict__ dqr, bf16* __restrict__ dsj,
+                                                              int64_t ldr) {
+    constexpr int NST = DSJ ? 4 : 2;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* sR = smem + O_R;
+    const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, c32 = lane & 31;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int S = (int)a.S, H = (int)a.H;
+    const int64_t ldq = a.ldq;
+    const Blk3 blk = xcd_blk3(a.xcd);
+    const int kb = blk.x;  // 0 = keys 0..127 (the heaviest block)
+    const int h = blk.y, b = blk.z;
+    const int j0 = kb * KB, jw0 = j0 + 32 * w, jk = jw0 + c32;  // this lane's key
+    const bf16* qkv_b = (const bf16*)a.qkv + (int64_t)b * S * ldq;
+    const bf16* dout_b = dout + (int64_t)b * S * ldo;
+    const __amdgpu_buffer_rsrc_t rq = make_rsrc(qkv_b, (uint32_t)((int64_t)S * ldq * 2));
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(dout_b, (uint32_t)((int64_t)S * ldo * 2));
+    const __amdgpu_buffer_rsrc_t rr = make_rsrc((const bf16*)a.R + (int64_t)h * a.S_max * HS, (uint32_t)(S * HS * 2));
+    const float* Lp = lse + ((int64_t)b * H + h) * S;
+    const float* Dp = Dv + ((int64_t)b * H + h) * S;
+    const __amdgpu_buffer_rsrc_t rl = make_rsrc(Lp, (uint32_t)(S * 4));
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc(Dp, (uint32_t)(S * 4));
+    bf16* qr_rows = dqr + ((int64_t)h * a.B + b) * S * ldr;
+    bf16* sj_rows = DSJ ? dsj + ((int64_t)h * a.B + b) * S * ldr : nullptr;
+    const float c2 = a.scale * LOG2E;
+    // dS = P (dP m ks - D) scale = P fma(dP m, ks scale, -D scale)
+    const float ks_scale = (DROP ? a.keep_scale : 1.f) * a.scale;
+
+    // key-side B operands: lane (key c32, half hh) holds K[key][16 ks + 8 hh + 0..7]
+    bf16x8 kf[8], vf[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+        if (jk < S) {
+            kf[ks] = *(const bf16x8*)(qkv_b + (int64_t)jk * ldq + (H + h) * HS + ks * 16 + hh * 8);
+            vf[ks] = *(const bf16x8*)(qkv_b + (int64_t)jk * ldq + (2 * H + h) * HS + ks * 16 + hh * 8);
+        } else {
+            kf[ks] = vf[ks] = (bf16x8){};
+        }
+        // pinned to AGPRs for the whole kernel (else the allocator keeps them in
+        // VGPRs and copies them into AGPRs at every use)
+        asm volatile("" : "+a"(kf[ks]), "+a"(vf[ks]));
+    }
+    f32x16 dk[4], dv[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) dk[n][e] = dv[n][e] = 0.f;
+
+    // mutable copies of the lane constants the loop uses (made opaque per iteration)
+    int ltid = tid, lhh = hh, lc32 = c32, ljk = jk, lhh7 = hh << 7, lz0 = c32 + 4 * hh, lbpb0 = (c32 - 4 * hh - 1) * 4;
+    // query tiles i0 = j0 + 32 t (causal: i >= j0; block 0 also the metadata rows)
+    const int it0 = j0;
+    const int nqt = (S - it0 + QT - 1) / QT;
+    // R window: chunk c = rows S + 96 - 32 c + [0, 32); wave w of tile T reads
+    // chunks T + 4 - w (window block 0) and T + 3 - w (block 1)
+    const int rw0 = S - QT;
+
+    // DMA: wave-instruction k (0, 1) of wave w fills chunks 4w + 2k + hh (a
+    // 1-KB run of the chunk-major image: 16-B chunk ch of row r at
+    // ch*512 + (16 r ^ 64 (ch & 3))); lane c32 of half hh lands in slot c32,
+    // which holds row c32 ^ 4 (2k + hh)
+    int lrow[2];
+    uint32_t offQ[2], offO[2], offR[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int ch = 4 * w + 2 * k + hh;
+        lrow[k] = c32 ^ ((2 * k + hh) << 2);
+        offQ[k] = (uint32_t)((lrow[k] * ldq + (int64_t)h * HS + ch * 8) * 2);
+        offO[k] = (uint32_t)((lrow[k] * ldo + (int64_t)h * HS + ch * 8) * 2);
+        offR[k] = (uint32_t)((lrow[k] * HS + ch * 8) * 2);
+    }
+    const int64_t mld = a.mask_ld;
+    const __amdgpu_buffer_rsrc_t rm =
+        make_rsrc(DROP ? (const void*)(a.colmask + (int64_t)(b * H + h) * (mask_bh_bytes(mld) / 4)) : (const void*)a.R,
+                  DROP ? (uint32_t)mask_bh_bytes(mld) : 0u);
+    // staging piece p (0..6) of query tile T (R chunk T + 4): Q 0-1, dO 2-3,
+    // row constants 4 (lse / D on waves 0-1, keep words colmask[b,h,j][i0/32]
+    // of the block's keys on waves 2-3, a zero-filling dummy without dropout),
+    // R 5-6. Every piece is issued by every wave (out-of-range rows: dropped
+    // offset), so the per-iteration vmcnt arithmetic is exact.
+    auto dma_piece = [&](int p, int T) {
+        const int i0 = it0 + QT * T, buf = T % NB;
+        if (p < 4) {
+            const int k = p & 1;
+            const bool ok = i0 + lrow[k] < S;
+            if (p < 2)
+                dma16(rq, smem + O_Q + buf * TILE + w * 2048 + k * 1024,
+                      ok ? offQ[k] + (uint32_t)i0 * (uint32_t)(ldq * 2) : OOB);
+            else
+                dma16(ro, smem + O_O + buf * TILE + w * 2048 + k * 1024,
+                      ok ? offO[k] + (uint32_t)i0 * (uint32_t)(ldo * 2) : OOB);
+        } else if (p == 4) {
+            const int ln = ltid & 63;
+            if (w < 2) {
+                const bool okl = i0 + ln < S;
+                dma4(w == 0 ? rl : rd, smem + O_L + (buf * 2 + w) * 256, okl ? (uint32_t)((i0 + ln) * 4) : OOB);
+            } else {
+                const int key = j0 + 64 * (w - 2) + ln;
+                dma4(rm, smem + O_D + buf * KB * 4 + (w - 2) * 256,
+                     DROP && key < S && i0 < S ? (uint32_t)(mask_word(mld, key, i0) * 4) : OOB);
+            }
+        } else {
+            const int k = p - 5, c = T + 4, r0 = rw0 + 128 - 32 * c, rg = r0 + lrow[k];
+            dma16(rr, sR + (c % NCH) * TILE + w * 2048 + k * 1024,
+                  (rg >= 0 && rg < S) ? offR[k] + (uint32_t)(r0 * HS * 2) : OOB);
+        }
+    };
+
+    // row reads (Q / dO A operands, R B operands): chunk 2 ks + hh of row c32 =
+    // rof[ks & 1] + 1024 ks
+    int rof[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) rof[k] = hh * 512 + ((c32 * 16) ^ ((2 * k + hh) << 6));
+    // transposed quads (dV^T / dK^T A operands): lane 4q+p of 16-lane group G
+    // reads rows 16 s + 8 u + 4 (G>>1) + q, columns 32 db + 16 (G&1) + 4p .. +3,
+    // i.e. tb[u] + 2048 db + 256 s
+    int tb[2];
+    {
+        const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, x = 2 * (G & 1) + (p >> 1);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) tb[u] = x * 512 + ((128 * u + 64 * (G >> 1) + 16 * q) ^ (x << 6)) + (p & 1) * 8;
+    }
+    auto tr_frag = [&](const char* img, int s2, int db) {
+        return cat8(tr_read(img, tb[0] + 2048 * db + 256 * s2), tr_read(img, tb[1] + 2048 * db + 256 * s2));
+    };
+
+    // dS row stores of the staged tile ip (NST / 2 per row half): thread t
+    // stores 8 keys of query rows t/16 and 16 + t/16, r-indexed at
+    // r = S-1-i+j (2-byte aligned rows, unaligned 16-B stores; entries j > i
+    // land at r >= S, in the row padding) and with DSJ j-indexed. Rows past the
+    // sequence end and the slot before tile 0 use the dropped offset, so every
+    // wave issues exactly NST stores per iteration.
+    const uint32_t ds_bytes = (uint32_t)min<int64_t>((int64_t)S * ldr * 2, OOB - 1);
+    const int ldr2 = (int)(ldr * 2);
+    auto store_piece = [&](int k, int ip, int sbuf, bool valid) {
+        // descriptors rebuilt per use from readfirstlane'd halves (kept live
+        // across the loop they would sit in VGPRs: a waterfall loop per store)
+        const int row = (ltid >> 4) + 16 * k, ch = ltid & 15;
+        const u32x4 v = *(const u32x4*)(smem + O_T + sbuf * T_BYTES + row * T_PITCH + ch * 16);
+        const int i = ip + row, j = j0 + 8 * ch;
+        const bool in = valid && i < S;
+        // 32-bit offsets (S * ldr * 2 < 4 GB, checked at launch)
+        const uint32_t rowb = (uint32_t)i * (uint32_t)ldr2;
+        const __amdgpu_buffer_rsrc_t rqr = make_rsrc(qr_rows, ds_bytes);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rqr, in ? rowb + (uint32_t)(S - 1 - i + j) * 2u : OOB, 0, 0);
+        if (DSJ) {
+            const __amdgpu_buffer_rsrc_t rsj = make_rsrc(sj_rows, ds_bytes);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rsj, in ? rowb + (uint32_t)j * 2u : OOB, 0, 0);
+        }
+    };
+
+    // skew: register e of lane c32 takes the window value from lane
+    // (c32 - row(e) - 1) mod 32 of the same half; the source selects block 0
+    // when c32 + row(e) >= 31 (z = c32 + 4 hh against 31 - (e&3) - 8 (e>>2))
+
+    // pipeline state carried between iterations: one set of accumulators
+    // (VGPRs; the AGPRs hold dK^T / dV^T and K / V) and the skewed relative
+    // term bp of the tile the next iteration's softmax reads
+    Acc acc;
+    float bp[16];
+
+    // ---- skew of tile T (its q0 / q1 final, >= 16 MFMAs old) into bp, with
+    // the causal / sequence-end mask folded in as -inf (p = exp2(-inf) = 0,
+    // dS = 0 * finite = 0); snippet `e` (one element per C-phase gap)
+    int sk_z = 0, sk_bpb = 0;
+    uint32_t sk_vm = 0u;
+    auto skew_setup = [&](int T) {
+        const int i0 = it0 + QT * T;
+        // per-tile lane constants made opaque (hoisted, the 16 masks and 16
+        // addresses would pin registers for the whole kernel)
+        sk_z = lz0;
+        sk_bpb = lbpb0;
+        asm volatile("" : "+v"(sk_z), "+v"(sk_bpb));
+        // rows k + 4hh valid: jk <= i0 + k + 4hh <= S - 1 (all ones in full tiles);
+        // the metadata tile's j > i entries are left to flash_bwd_meta_kernel
+        const int lo = ljk - i0 - 4 * lhh, hi = S - 1 - i0 - 4 * lhh;
+        const uint32_t up = hi >= 31 ? 0xffffffffu : (hi < 0 ? 0u : (2u << hi) - 1u);
+        const uint32_t dn = lo <= 0 ? 0xffffffffu : (lo >= 32 ? 0u : (0xffffffffu << lo));
+        sk_vm = up & dn;
+    };
+    auto skew = [&](auto E) {
+        constexpr int e = decltype(E)::value, k = (e & 3) + 8 * (e >> 2);
+        const float sel = (sk_z >= 31 - k) ? acc.q0[e] : acc.q1[e];
+        const int adr = ((sk_bpb - 4 * k) & 124) | lhh7;
+        const int v = __builtin_amdgcn_ds_bpermute(adr, __float_as_int(sel));
+        const int m = __builtin_amdgcn_sbfe((int)sk_vm, k, 1);
+        float b = __int_as_float((v & m) | ((int)0xff800000 & ~m));  // v_bfi: valid ? v : -inf
+        // keep the carried value float-typed: as an i32 loop phi (what
+        // instcombine makes of the bit ops) the allocator moved ~100 values
+        // into the AGPR file and spilled
+        asm volatile("" : "+v"(b));
+        bp[e] = b;
+    };
+
+    // ---- one iteration (t): with DO_A, A(t+1) runs beside it.
+    //  phase 1 (16 MFMAs: QR window of t+1 into q0 / q1) | softmax stage a of
+    //           tile t (p from s + bp), the staging DMA of tile t+1+DEPTH,
+    //           the dS(t-1) row stores
+    //  phase 2 (16 MFMAs: S of t+1, then dP of t+1, into the registers tile
+    //           t's s / dp just left) | softmax stage b (dS from dp), dS(t)
+    //           staging writes
+    //  phase 3 (16 MFMAs: C(t) = dV / dK of tile t) | skew of tile t+1
+    auto iter = [&](auto DOA, int t) {
+        constexpr bool DO_A = decltype(DOA)::value;
+        const int i0 = it0 + QT * t, buf = t % NB, sb = t & 1, T = t + 1;
+        // the lane constants are re-declared opaque every iteration: the
+        // unrolled gaps derive dozens of per-lane addresses from them, and
+        // hoisted out of the loop those pinned (and spilled) ~100 VGPRs
+        asm volatile("" : "+v"(lrow[0]), "+v"(lrow[1]), "+v"(offQ[0]), "+v"(offQ[1]), "+v"(offO[0]), "+v"(offO[1]),
+                     "+v"(offR[0]), "+v"(offR[1]));
+        asm volatile("" : "+v"(rof[0]), "+v"(rof[1]), "+v"(tb[0]), "+v"(tb[1]), "+v"(ltid), "+v"(ljk), "+v"(lhh),
+                     "+v"(lc32));
+        asm volatile("" : "+v"(lhh7), "+v"(lz0), "+v"(lbpb0));
+        // tile t+1's data: issued DEPTH iterations ago
+        if (t >= DEPTH) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST + (NDMA + NST) * (DEPTH - 1)) : "memory");
+        bar();  // tile t+1 landed everywhere; tile t-1's buffers and dS(t-1) staging published
+        const float* cL = (const float*)(smem + O_L + buf * 512);
+        const float* cD = cL + 64;
+        float pv[16];
+        uint32_t mk = 0u;
+        bf16x8 pa[2], da[2];
+        // stage a: p = exp2((s + bp) c2 - lse log2e); the dropped P for dV
+        auto stage_a = [&](auto E) {
+            constexpr int e = decltype(E)::value, k = (e & 3) + 8 * (e >> 2);
+            const float p = __builtin_amdgcn_exp2f(fmaf(acc.s[e] + bp[e], c2, -cL[acc_row(e, 0) + 4 * lhh]));
+            pv[e] = p;
+            pa[e >> 3][e & 7] = (bf16)(DROP ? and_f(p, __builtin_amdgcn_sbfe((int)mk, k, 1)) : p);
+        };
+        // stage b: dS = p fma(dP m, ks scale, -D scale)
+        auto stage_b = [&](auto E) {
+            constexpr int e = decltype(E)::value, k = (e & 3) + 8 * (e >> 2);
+            float dpv = acc.dp[e];
+            if (DROP) dpv = and_f(dpv, __builtin_amdgcn_sbfe((int)mk, k, 1));
+            da[e >> 3][e & 7] = (bf16)(pv[e] * fmaf(dpv, ks_scale, -cD[acc_row(e, 0) + 4 * lhh]));
+        };
+        const char* cQn = smem + O_Q + (T % NB) * TILE;
+        const char* cOn = smem + O_O + (T % NB) * TILE;
+        const char* rb0 = sR + ((T + 4 - w) % NCH) * TILE;
+        const char* rb1 = sR + ((T + 3 - w) % NCH) * TILE;
+        bf16x8 fq[2], fx[2], fy[2];
+        auto ldqr = [&](int ks, int n) {
+            const int off = rof[ks & 1] + 1024 * ks;
+            fq[n] = *(const bf16x8*)(cQn + off);
+            fx[n] = *(const bf16x8*)(rb0 + off);
+            fy[n] = *(const bf16x8*)(rb1 + off);
+        };
+        // ---- phase 1
+        if (DO_A) ldqr(0, 0);
+        static_for<16>([&](auto G) {
+            constexpr int g = decltype(G)::value, ks = g >> 1, c = ks & 1;
+            if (DO_A) {
+                if ((g & 1) == 0) {
+                    if (ks + 1 < 8) ldqr(ks + 1, c ^ 1);
+                    if (ks == 0) mfma_first_vv(acc.q0, fq[c], fx[c]);
+                    else mfma_acc_vv(acc.q0, fq[c], fx[c]);
+                } else {
+                    if (ks == 0) mfma_first_vv(acc.q1, fq[c], fy[c]);
+                    else mfma_acc_vv(acc.q1, fq[c], fy[c]);
+                }
+            }
+            if constexpr (g < NDMA) dma_piece(g, t + 1 + DEPTH);
+            if constexpr (g == NDMA || g == NDMA + 1) store_piece(g - NDMA, i0 - QT, sb ^ 1, t >= 1);
+            if constexpr (g == 0) {
+                // keep word of this lane's key over the tile's 32 queries; bit
+                // k of mk = query row k + 4 hh
+                if (DROP) mk = ((const uint32_t*)(smem + O_D + buf * KB * 4))[32 * w + lc32] >> (4 * lhh);
+            }
+            if constexpr (g >= 2) stage_a(std::integral_constant<int, g - 2>{});
+            if constexpr (g >= 14) stage_a(std::integral_constant<int, g>{});
+            if constexpr (g >= 6) stage_b(std::integral_constant<int, g - 6>{});
+            SB();
+        });
+        // ---- phase 2: S chain (tile t's s is dead), then dP chain (its dp
+        // dies at the stage b of gap 7)
+        bf16x8 fa[2];
+        auto lds1 = [&](int ks, int n, bool q) {
+            const int off = rof[ks & 1] + 1024 * ks;
+            fa[n] = *(const bf16x8*)((q ? cQn : cOn) + off);
+        };
+        char* st = smem + O_T + sb * T_BYTES + 4 * lhh * T_PITCH + (32 * w + lc32) * 2;
+        if (DO_A) lds1(0, 0, true);
+        static_for<16>([&](auto G) {
+            constexpr int g = decltype(G)::value, ks = g & 7, c = g & 1;
+            if (DO_A) {
+                if (g + 1 < 16) lds1((g + 1) & 7, c ^ 1, g + 1 < 8);
+                if (g < 8) {
+                    if (ks == 0) mfma_first_va(acc.s, fa[c], kf[ks]);
+                    else mfma_acc_va(acc.s, fa[c], kf[ks]);
+                } else {
+                    if (ks == 0) mfma_first_va(acc.dp, fa[c], vf[ks]);
+                    else mfma_acc_va(acc.dp, fa[c], vf[ks]);
+                }
+            }
+            if constexpr (g < 6) stage_b(std::integral_constant<int, 10 + g>{});
+            if constexpr (g >= 8) {  // dS(t) staging for the next iteration's row stores
+                constexpr int e0 = 2 * (g - 8);
+                *(bf16*)(st + acc_row(e0, 0) * T_PITCH) = da[e0 >> 3][e0 & 7];
+                *(bf16*)(st + acc_row(e0 + 1, 0) * T_PITCH) = da[(e0 + 1) >> 3][(e0 + 1) & 7];
+            }
+            SB();
+        });
+        // ---- phase 3: C(t): dV^T[d][j] += dO^T[d][i] P[i][j], dK^T[d][j] +=
+        // Q^T[d][i] dS[i][j] (16 MFMAs) | skew of tile t+1
+        const char* cQ = smem + O_Q + buf * TILE;
+        const char* cO = smem + O_O + buf * TILE;
+        bf16x8 fo[2], fqq[2];
+        fo[0] = tr_frag(cO, 0, 0);
+        fqq[0] = tr_frag(cQ, 0, 0);
+        if (DO_A) skew_setup(T);
+        static_for<16>([&](auto G) {
+            constexpr int g = decltype(G)::value, n = g >> 1, c = n & 1, db = n >> 1, s2 = n & 1;
+            if ((g & 1) == 0) {
+                if (n + 1 < 8) {
+                    fo[c ^ 1] = tr_frag(cO, (n + 1) & 1, (n + 1) >> 1);
+                    fqq[c ^ 1] = tr_frag(cQ, (n + 1) & 1, (n + 1) >> 1);
+                }
+                mfma_acc_a(dv[db], fo[c], pa[s2]);
+            } else {
+                mfma_acc_a(dk[db], fqq[c], da[s2]);
+            }
+            if (DO_A) skew(std::integral_constant<int, g>{});
+            SB();
+        });
+    };
+
+    // prologue: tiles 0..DEPTH and the R chunks of their windows, A(0), skew(0)
+#pragma unroll
+    for (int d = 0; d <= DEPTH; ++d)
+#pragma unroll
+        for (int p = 0; p < NDMA; ++p) dma_piece(p, d);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {  // chunks 0..3 (dma_piece covers chunk T + 4 of tile T)
+        const int r0 = rw0 + 128 - 32 * c;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int rg = r0 + lrow[k];
+            dma16(rr, sR + (c % NCH) * TILE + w * 2048 + k * 1024,
+                  (rg >= 0 && rg < S) ? offR[k] + (uint32_t)(r0 * HS * 2) : OOB);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    {
+        const char* cQ = smem + O_Q;
+        const char* cO = smem + O_O;
+        const char* rb0 = sR + ((4 - w) % NCH) * TILE;
+        const char* rb1 = sR + ((3 - w) % NCH) * TILE;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            const int off = rof[ks & 1] + 1024 * ks;
+            const bf16x8 fq = *(const bf16x8*)(cQ + off), fo = *(const bf16x8*)(cO + off);
+            const bf16x8 fx = *(const bf16x8*)(rb0 + off), fy = *(const bf16x8*)(rb1 + off);
+            if (ks == 0) {
+                mfma_first_vv(acc.q0, fq, fx);
+                mfma_first_vv(acc.q1, fq, fy);
+                mfma_first_va(acc.s, fq, kf[0]);
+                mfma_first_va(acc.dp, fo, vf[0]);
+            } else {
+                mfma_acc_vv(acc.q0, fq, fx);
+                mfma_acc_vv(acc.q1, fq, fy);
+                mfma_acc_va(acc.s, fq, kf[ks]);
+                mfma_acc_va(acc.dp, fo, vf[ks]);
+            }
+        }
+        drain4(acc.s, acc.dp, acc.s, acc.dp);
+        asm volatile("s_nop 15\n\ts_nop 7" : "+v"(acc.q0), "+v"(acc.q1));
+        skew_setup(0);
+        static_for<16>([&](auto E) { skew(E); });
+    }
+    for (int t = 0; t + 1 < nqt; ++t) iter(std::true_type{}, t);
+    iter(std::false_type{}, nqt - 1);
+    // the last tile's dS rows
+    bar();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) store_piece(k, it0 + QT * (nqt - 1), (nqt - 1) & 1, true);
+
+    // lane holds dK^T / dV^T [d = 32 db + acc_row(e)][key c32]
+    drain_a(dk, dv);
+    if (jk < S) {
+        const float vs = DROP ? a.keep_scale : 1.f;
+        bf16* dkp = dqkv + ((int64_t)b * S + jk) * ldd + (H + h) * HS;
+        bf16* dvp = dkp + H * HS;
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+#pragma unroll
+            for (int e4 = 0; e4 < 4; ++e4) {
+                const int d = 32 * db + 8 * e4 + 4 * hh;
+                store4(dkp + d, (f32x4){dk[db][4 * e4], dk[db][4 * e4 + 1], dk[db][4 * e4 + 2], dk[db][4 * e4 + 3]});
+                store4(dvp + d, (f32x4){dv[db][4 * e4] * vs, dv[db][4 * e4 + 1] * vs, dv[db][4 * e4 + 2] * vs,
+                                        dv[db][4 * e4 + 3] * vs});
+            }
+    }
+}
+
+}  // namespace
+
+int flash_bwd_kv5(const AttnArgs& a, const float* lse, const float* Dv, const bf16* dout, int64_t ldo, bf16* dqkv,
+                  int64_t ldd, bf16* dqr, bf16* dsj, int64_t ldr, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)flash_bwd_kv5_kernel<false, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)flash_bwd_kv5_kernel<true, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)flash_bwd_kv5_kernel<false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)flash_bwd_kv5_kernel<true, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        attr = true;
+    }
+    if (a.S * a.ldq * 2 >= (int64_t)OOB || a.S * ldo * 2 >= (int64_t)OOB || a.n_meta > 8) return -1;
+    if (a.colmask && mask_bh_bytes(a.mask_ld) >= (int64_t)OOB) return -1;
+    if (ldr < a.S + 128) return -1;
+    const dim3 grid((unsigned)((a.S + KB - 1) / KB), (unsigned)a.H, (unsigned)a.B);
+    const bool drop = a.colmask != nullptr, sj = dsj != nullptr;
+#define KV5_LAUNCH(D, J)                                                                                          \
+    hipLaunchKernelGGL((flash_bwd_kv5_kernel<D, J>), grid, dim3(NT), LDS_BYTES, s, a, lse, Dv, dout, ldo, dqkv, ldd, \
+                       dqr, dsj, ldr)
+    if (drop) {
+        if (sj) KV5_LAUNCH(true, true);
+        else KV5_LAUNCH(true, false);
+    } else {
+        if (sj) KV5_LAUNCH(false, true);
+        else KV5_LAUNCH(false, false);
+    }
+#undef KV5_LAUNCH
+    return 0;
+}

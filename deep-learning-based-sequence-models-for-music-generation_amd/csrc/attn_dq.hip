@@ -16,7 +16,6 @@
 // from a (row>>1)&7 chunk-swizzled image; B (K / R rows = [k][d], d contiguous)
 // with ds_read_b64_tr_b16 from a 2*g(k) chunk-swizzled image (T10).
 #include "attn.h"
-#include <cstdlib>
 
 namespace {
 
@@ -58,14 +57,43 @@ __device__ __forceinline__ bf16x8 frag_mn(const char* s, int rb, int ks, int lan
     return u.v;
 }
 
-// BK 64: 64 KB of LDS, two workgroups per CU; BK 32: 32 KB, four
-template <int BK>
-__global__ __launch_bounds__(NT, BK == 64 ? 2 : 4) void flash_bwd_dq_kernel(AttnArgs a, const bf16* __restrict__ dsj,
-                                                                          const bf16* __restrict__ dqr, int64_t ldr,
-                                                                          bf16* __restrict__ dqkv, int64_t ldd) {
+// bf16 elements [s, s + 8) of the 32-byte window lo:hi (s wave-uniform, 0..7):
+// four v_alignbyte over the dword pairs the window straddles
+__device__ __forceinline__ u32x4 funnel8(u32x4 lo, u32x4 hi, int s) {
+    const uint32_t bs = (uint32_t)(s & 1) * 2u;
+    auto ab = [&](uint32_t h, uint32_t l) { return __builtin_amdgcn_alignbyte(h, l, bs); };
+    switch (s >> 1) {
+        case 0: return (u32x4){ab(lo[1], lo[0]), ab(lo[2], lo[1]), ab(lo[3], lo[2]), ab(hi[0], lo[3])};
+        case 1: return (u32x4){ab(lo[2], lo[1]), ab(lo[3], lo[2]), ab(hi[0], lo[3]), ab(hi[1], hi[0])};
+        case 2: return (u32x4){ab(lo[3], lo[2]), ab(hi[0], lo[3]), ab(hi[1], hi[0]), ab(hi[2], hi[1])};
+        default: return (u32x4){ab(hi[0], lo[3]), ab(hi[1], hi[0]), ab(hi[2], hi[1]), ab(hi[3], hi[2])};
+    }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dq_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void* p = (void*)(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// 64 KB of LDS, two workgroups per CU. DS1 (dS stored once, r-indexed): the
+// dS.K term reads the j-view of dQR, row i's run starting at key j being the
+// dQR run starting at r = S-1-i+j. That start is 2-byte aligned, so each
+// 16-B chunk is cut from two ALIGNED chunk loads by a funnel shift; the shift
+// (S-1-i) mod 8 depends on the row only through i mod 8, so each A-operand
+// load instruction covers 8 rows of one residue class (rows 64 rb + r8 + 8 m,
+// one per 8 lanes) and its shift is wave-uniform. The entries past the
+// diagonal read the row's stored zeros (j > i inside a 128-key block) or its
+// padding (never written, zeroed once per workspace: ldr >= S + 200).
+template <bool DS1>
+__global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const bf16* __restrict__ dsj,
+                                                             const bf16* __restrict__ dqr, int64_t ldr,
+                                                             bf16* __restrict__ dqkv, int64_t ldd) {
+    constexpr int BK = 64;
     constexpr int A_BYTES = BM * BK * 2, B_BYTES = BK * HSZ * 2, STAGE = A_BYTES + B_BYTES;
     constexpr int NU = BK / 16;  // 16-B chunks per thread per operand and stage
-    constexpr int CPR = BK / 8;  // chunks per A row
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int64_t S = a.S, H = a.H, ldq = a.ldq;
@@ -75,32 +103,48 @@ __global__ __launch_bounds__(NT, BK == 64 ? 2 : 4) void flash_bwd_dq_kernel(Attn
     const int64_t h = blk.y, b = blk.z;
     const int64_t i0 = (int64_t)qt * BM, ilast = min<int64_t>(S - 1, i0 + BM - 1);
     const int64_t rows = ((h * a.B + b) * S) * ldr;
-    const bf16* A0 = dsj + rows;
-    const bf16* A1 = dqr + rows;
+    const uint32_t slab = (uint32_t)(S * ldr * 2);
+    const __amdgpu_buffer_rsrc_t rR = dq_rsrc(dqr + rows, slab);
+    const __amdgpu_buffer_rsrc_t rJ = dq_rsrc((DS1 ? dqr : dsj) + rows, slab);
     const bf16* B0 = (const bf16*)a.qkv + b * S * ldq + (H + h) * HSZ;
     const bf16* B1 = (const bf16*)a.R + h * a.S_max * HSZ;
     const int64_t ke0 = min<int64_t>(S, i0 + BM);        // j range [0, ke0)
     const int64_t kb1 = (S - 1 - ilast) / BK * BK;       // r range [kb1, S)
     const int n0 = (int)((ke0 + BK - 1) / BK), nt = n0 + (int)((S - kb1 + BK - 1) / BK);
+    // A-operand load u of this wave: rows 64 rb + r8 + 8 m (m = lane / 8), chunk lane % 8
+    const int m8 = lane >> 3, ch8 = lane & 7;
+    int arow[NU], ashift[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int cls = wid * NU + u, r8 = cls & 7, rb = cls >> 3;
+        arow[u] = 64 * rb + r8 + 8 * m8;
+        ashift[u] = __builtin_amdgcn_readfirstlane((int)((S - 1 - r8) & 7));  // i0, k0: multiples of 8
+    }
 
     u32x4 ra[NU], rb[NU];
     auto load = [&](int t) {
         const bool s1 = t >= n0;
         const int64_t k0 = s1 ? kb1 + (int64_t)(t - n0) * BK : (int64_t)t * BK;
         const int64_t kend = s1 ? S : ke0;
-        const bf16* A = s1 ? A1 : A0;
         const bf16* B = s1 ? B1 : B0;
         const int64_t ldb = s1 ? HSZ : ldq;
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
-            const int c = tid + NT * u;
             {  // A [128 rows][BK k]
-                const int row = c / CPR, ch = c % CPR;
-                const int64_t gi = i0 + row, gk = k0 + ch * 8;
-                const int valid = gi < S ? (int)min<int64_t>(8, kend - gk) : 0;
-                ra[u] = load_chunk(A + gi * ldr + gk, valid);
+                const int64_t gi = i0 + arow[u];
+                if (DS1 && !s1) {  // j-view of dQR: r = S-1-gi+k0+8ch .. +7
+                    const int64_t r = S - 1 - gi + k0 + 8 * ch8;
+                    const uint32_t off = gi < S ? (uint32_t)((gi * ldr + (r & ~(int64_t)7)) * 2) : 0xFFFF0000u;
+                    const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(rJ, off, 0, 0);
+                    const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(rJ, off + 16u, 0, 0);
+                    ra[u] = funnel8(lo, hi, ashift[u]);
+                } else {
+                    const uint32_t off = gi < S ? (uint32_t)((gi * ldr + k0 + 8 * ch8) * 2) : 0xFFFF0000u;
+                    ra[u] = __builtin_amdgcn_raw_buffer_load_b128(s1 ? rR : rJ, off, 0, 0);
+                }
             }
             {  // B [BK k][128 d]
+                const int c = tid + NT * u;
                 const int kr = c >> 4, ch = c & 15;
                 const int64_t gk = k0 + kr;
                 rb[u] = load_chunk(B + gk * ldb + ch * 8, gk < kend ? 8 : 0);
@@ -112,9 +156,9 @@ __global__ __launch_bounds__(NT, BK == 64 ? 2 : 4) void flash_bwd_dq_kernel(Attn
         char* sb = sa + A_BYTES;
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
+            const int row = arow[u];
+            *(u32x4*)(sa + row * (BK * 2) + swz_k<BK>(row, ch8) * 16) = ra[u];
             const int c = tid + NT * u;
-            const int row = c / CPR, ch = c % CPR;
-            *(u32x4*)(sa + row * (BK * 2) + swz_k<BK>(row, ch) * 16) = ra[u];
             const int kr = c >> 4, chb = c & 15;
             *(u32x4*)(sb + kr * 256 + swz_mn(kr, chb) * 16) = rb[u];
         }
@@ -140,7 +184,7 @@ __global__ __launch_bounds__(NT, BK == 64 ? 2 : 4) void flash_bwd_dq_kernel(Attn
         for (int ks = 0; ks < BK / 32; ++ks) {
             bf16x8 af[4], bfr[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) af[i] = frag_k<BK>(sa, wm + i * 16, ks, lane);
+            for (int i = 0; i < 4; ++i) af[i] = frag_k<64>(sa, wm + i * 16, ks, lane);
 #pragma unroll
             for (int j = 0; j < 4; ++j) bfr[j] = frag_mn(sb, wn + j * 16, ks, lane);
 #pragma unroll
@@ -168,11 +212,7 @@ __global__ __launch_bounds__(NT, BK == 64 ? 2 : 4) void flash_bwd_dq_kernel(Attn
 
 void flash_bwd_dq(const AttnArgs& a, const bf16* dsj, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd,
                   hipStream_t s) {
-    static const int bk = [] {
-        const char* e = getenv("MSQ_ATTN_DQ_BK");
-        return e && atoi(e) == 32 ? 32 : 64;
-    }();
     const dim3 grid((unsigned)((a.S + BM - 1) / BM), (unsigned)a.H, (unsigned)a.B);
-    if (bk == 32) hipLaunchKernelGGL(flash_bwd_dq_kernel<32>, grid, dim3(NT), 0, s, a, dsj, dqr, ldr, dqkv, ldd);
-    else hipLaunchKernelGGL(flash_bwd_dq_kernel<64>, grid, dim3(NT), 0, s, a, dsj, dqr, ldr, dqkv, ldd);
+    if (dsj) hipLaunchKernelGGL(flash_bwd_dq_kernel<false>, grid, dim3(NT), 0, s, a, dsj, dqr, ldr, dqkv, ldd);
+    else hipLaunchKernelGGL(flash_bwd_dq_kernel<true>, grid, dim3(NT), 0, s, a, dsj, dqr, ldr, dqkv, ldd);
 }

@@ -182,24 +182,14 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(AttnArgs a, bf16* __re
 
 // ------------------------------------------------------------ backward: pre
 // D[b,h,i] = sum_d dO[i,d] O[i,d]
-__global__ void flash_bwd_pre_kernel(AttnArgs a, const bf16* __restrict__ dout, int64_t ldo,
-                                     const bf16* __restrict__ out, float* __restrict__ Dv) {
-    const int64_t row = blockIdx.x * 4LL + (threadIdx.x >> 6);  // over B*S*H
-    const int lane = threadIdx.x & 63;
-    if (row >= a.B * a.S * a.H) return;
-    const int64_t h = row % a.H, bi = row / a.H;
-    const int64_t b = bi / a.S, i = bi % a.S;
-    const f32x2 x = (f32x2){(float)dout[bi * ldo + h * HS + 2 * lane], (float)dout[bi * ldo + h * HS + 2 * lane + 1]};
-    const f32x2 y = (f32x2){(float)out[bi * ldo + h * HS + 2 * lane], (float)out[bi * ldo + h * HS + 2 * lane + 1]};
-    const float s = wave_sum(x[0] * y[0] + x[1] * y[1]);
-    if (lane == 0) Dv[(b * a.H + h) * a.S + i] = s;
-}
-
 // same, 16 lanes x 8 elements (one 16-B load of dO and of O each) per
-// (row, head): 4 head-rows per wave
+// (row, head): 4 head-rows per wave; also the key/value pass v5's row
+// constants l2 = lse * log2(e) and dsc = D * scale
 __global__ __launch_bounds__(256) void flash_bwd_pre_vec_kernel(AttnArgs a, const bf16* __restrict__ dout,
                                                                 int64_t ldo, const bf16* __restrict__ out,
-                                                                float* __restrict__ Dv) {
+                                                                const float* __restrict__ lse,
+                                                                float* __restrict__ Dv, float* __restrict__ l2,
+                                                                float* __restrict__ dsc) {
     const int64_t row = blockIdx.x * 16LL + (threadIdx.x >> 4);  // over B*S*H
     const int l = threadIdx.x & 15;
     const bool ok = row < a.B * a.S * a.H;
@@ -213,8 +203,10 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_vec_kernel(AttnArgs a, cons
 #pragma unroll
     for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     if (ok && l == 0) {
-        const int64_t b = bi / a.S, i = bi % a.S;
-        Dv[(b * a.H + h) * a.S + i] = s;
+        const int64_t b = bi / a.S, i = bi % a.S, k = (b * a.H + h) * a.S + i;
+        Dv[k] = s;
+        dsc[k] = s * a.scale;
+        l2[k] = lse[k] * LOG2E;
     }
 }
 
@@ -247,6 +239,81 @@ __global__ void flash_bwd_meta_kernel(AttnArgs a, const float* __restrict__ meta
         }
         bf16* p = dqkv + (b * S + i + 1) * ldd + h * HS + d;
         *p = (bf16)((float)*p + gq);
+    }
+}
+
+// metadata prefix, v5 form: the key/value pass v5 masks the entries j > i
+// inside the metadata prefix (i < j < n_meta, keys every query sees) like the
+// rest of the upper triangle, so this kernel owns them whole: per (b, h) and
+// pair (i, j)
+//   s    = scale (q_i.k_j + [j >= i+2] q_{i+1}.R[j-i-2]),  p = exp(s - lse_i)
+//   dS   = p (dO_i.v_j m_ij ks - D_i) scale
+//   dV_j += p m_ij ks dO_i,  dK_j += dS q_i,  dq_i += dS k_j
+//   j >= i+2: dq_{i+1} += dS R[j-i-2],  dR[j-i-2] += dS q_{i+1}
+// (model_transformer.py:70-90 with the _rel_shift wrap of :84-90 for j > i)
+__global__ __launch_bounds__(HS) void flash_bwd_meta5_kernel(AttnArgs a, const float* __restrict__ lse,
+                                                             const float* __restrict__ Dv,
+                                                             const bf16* __restrict__ dout, int64_t ldo,
+                                                             bf16* __restrict__ dqkv, int64_t ldd,
+                                                             float* __restrict__ dR) {
+    __shared__ float red[3][2];
+    const int64_t h = blockIdx.y, b = blockIdx.z;
+    const int d = threadIdx.x, lane = d & 63, wv = d >> 6;  // 128 threads, one per dim
+    const int64_t S = a.S, H = a.H, ldq = a.ldq, bh = b * H + h;
+    const bf16* qkv = (const bf16*)a.qkv + b * S * ldq;
+    const bf16* Rp = (const bf16*)a.R + h * a.S_max * HS;
+    const bf16* dob = dout + b * S * ldo;
+    const int nm = (int)min<int64_t>(a.n_meta, S);
+    float gq[8], gk[8], gv[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) gq[r] = gk[r] = gv[r] = 0.f;
+    auto q = [&](int i) { return (float)qkv[i * ldq + h * HS + d]; };
+    auto k = [&](int j) { return (float)qkv[j * ldq + (H + h) * HS + d]; };
+    auto v = [&](int j) { return (float)qkv[j * ldq + (2 * H + h) * HS + d]; };
+    auto sum3 = [&](float x, float y, float z) {
+        x = wave_sum(x);
+        y = wave_sum(y);
+        z = wave_sum(z);
+        __syncthreads();
+        if (lane == 0) {
+            red[0][wv] = x;
+            red[1][wv] = y;
+            red[2][wv] = z;
+        }
+        __syncthreads();
+    };
+#pragma unroll 1
+    for (int i = 0; i + 1 < nm; ++i) {
+#pragma unroll 1
+        for (int j = i + 1; j < nm; ++j) {
+            const bool far = j >= i + 2;
+            const float rr = far ? (float)Rp[(j - i - 2) * HS + d] : 0.f;
+            const float q1 = far ? q(i + 1) : 0.f;
+            sum3(q(i) * k(j), q1 * rr, (float)dob[i * ldo + h * HS + d] * v(j));
+            const float sc = (red[0][0] + red[0][1] + red[1][0] + red[1][1]) * a.scale;
+            const float dp = red[2][0] + red[2][1];
+            const float p = expf(sc - lse[bh * S + i]);
+            const float m = a.rowmask ? keep_bit(a, bh, i, j) : 1.f;  // ks or 0 with dropout
+            const float ds = p * (dp * m - Dv[bh * S + i]) * a.scale;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                if (r == j) {
+                    gv[r] += p * m * (float)dob[i * ldo + h * HS + d];
+                    gk[r] += ds * q(i);
+                }
+                if (r == i) gq[r] += ds * k(j);
+                if (far && r == i + 1) gq[r] += ds * rr;
+            }
+            if (far) atomicAdd(dR + (h * a.S_max + (j - i - 2)) * HS + d, ds * q1);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        if (r >= nm) break;
+        bf16* row = dqkv + (b * S + r) * ldd;
+        row[h * HS + d] = (bf16)((float)row[h * HS + d] + gq[r]);
+        row[(H + h) * HS + d] = (bf16)((float)row[(H + h) * HS + d] + gk[r]);
+        row[(2 * H + h) * HS + d] = (bf16)((float)row[(2 * H + h) * HS + d] + gv[r]);
     }
 }
 
@@ -284,10 +351,13 @@ __global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, bf16* __restrict__ 
 
 // dQR / dSj row pitch: >= S + 128 so that the key/value pass's whole-row dS
 // stores of a 128-key block never reach the next row (dQR entries j > i fall
-// at r = S-1-i+j in [S, S+127): padding no reader touches)
-int64_t flash_dqr_ld(int64_t S) { return (S + 128 + 7) / 8 * 8; }
+// at r = S-1-i+j in [S, S+127)), and >= S + 200 for the dq kernel's j-view of
+// dQR (dS-once: row i's K range ends below i0 + 192, i.e. r < S + 191, plus
+// the funnel shift's second chunk): padding, zeroed once per workspace
+int64_t flash_dqr_ld(int64_t S) { return (S + 200 + 7) / 8 * 8; }
 
 // workspace: dQR bf16 [H][B][S][ldr] | dSj bf16 [H][B][S][ldr] | D f32 [B][H][S] | meta_ds f32 [B][H][8][8]
+//            | l2 f32 [B][H][S] | dsc f32 [B][H][S]
 //            | dR split-K partials f32 [ksplit][H][S][HS]
 static size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 static size_t dr_ws_bytes(int64_t B, int64_t S, int64_t H) {
@@ -296,7 +366,7 @@ static size_t dr_ws_bytes(int64_t B, int64_t S, int64_t H) {
 
 size_t flash_bwd_workspace(int64_t B, int64_t S, int64_t H) {
     const int64_t ldr = flash_dqr_ld(S);
-    return 2 * align256((size_t)H * B * S * ldr * 2) + align256((size_t)B * H * S * 4) +
+    return 2 * align256((size_t)H * B * S * ldr * 2) + 3 * align256((size_t)B * H * S * 4) +
            align256((size_t)B * H * 64 * 4) + align256(dr_ws_bytes(B, S, H));
 }
 
@@ -319,6 +389,10 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     float* meta_ds = (float*)p;
     p += align256((size_t)B * H * 64 * 4);
     float* dr_ws = (float*)p;
+    p += align256(dr_ws_bytes(B, S, H));
+    float* l2 = (float*)p;
+    p += align256((size_t)B * H * S * 4);
+    float* dsc = (float*)p;
 
     // the band and row pads are never written non-zero by the passes below
     // (their dS entries there are 0 by the mask), so a workspace that already
@@ -327,24 +401,26 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
         hipLaunchKernelGGL(dqr_band_zero_kernel, dim3((unsigned)((H * B * S + 3) / 4)), dim3(256), 0, s, dqr, dsj, ldr,
                            S, H * B * S);
     hipMemsetAsync(meta_ds, 0, (size_t)B * H * 64 * 4, s);
-    if (ldo % 8 == 0 && ((uintptr_t)dout % 16) == 0 && ((uintptr_t)out % 16) == 0)
-        hipLaunchKernelGGL(flash_bwd_pre_vec_kernel, dim3((unsigned)((B * S * H + 15) / 16)), dim3(256), 0, s, a, dout,
-                           ldo, out, Dv);
-    else
-        hipLaunchKernelGGL(flash_bwd_pre_kernel, dim3((unsigned)((B * S * H + 3) / 4)), dim3(256), 0, s, a, dout, ldo,
-                           out, Dv);
+    if (ldo % 8 || ((uintptr_t)dout % 16) || ((uintptr_t)out % 16))
+        return msq_set_error(MSQ_ERR_ARG, "flash_bwd: dout / out need 16-B aligned rows");
+    hipLaunchKernelGGL(flash_bwd_pre_vec_kernel, dim3((unsigned)((B * S * H + 15) / 16)), dim3(256), 0, s, a, dout, ldo,
+                       out, lse, Dv, l2, dsc);
     // key/value pass: dK, dV, and dS in both layouts (v4; MSQ_ATTN_BWD_KV=3
     // selects the v3 pass, kept for A/B measurements)
-    static const bool use_v3 = [] {
+    // MSQ_ATTN_BWD_KV: 5 (default) the v5 pass storing dS once; 50 v5 also
+    // storing the j-indexed copy; 4 / 3 the older passes (both copies)
+    static const int kv_ver = [] {
         const char* e = getenv("MSQ_ATTN_BWD_KV");
-        return e && e[0] == '3';
+        return e ? atoi(e) : 5;
     }();
-    const int kv_rc = use_v3 ? flash_bwd_kv3(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s)
-                             : flash_bwd_kv4(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s);
+    const bool ds1 = kv_ver == 5;
+    const int kv_rc = kv_ver == 3   ? flash_bwd_kv3(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s)
+                      : kv_ver == 4 ? flash_bwd_kv4(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s)
+                                    : flash_bwd_kv5(a, l2, dsc, dout, ldo, dqkv, ldd, dqr, ds1 ? nullptr : dsj, ldr, s);
     if (kv_rc)
         return msq_set_error(MSQ_ERR_UNSUPPORTED, "flash_bwd: shape outside the key/value pass (n_meta > 8 or > 4 GB)");
     // dq (bf16, q columns of dqkv) = dSj . K + dQR . R
-    flash_bwd_dq(a, dsj, dqr, ldr, dqkv, ldd, s);
+    flash_bwd_dq(a, ds1 ? nullptr : dsj, dqr, ldr, dqkv, ldd, s);
     // dR[h][r] += sum_{b,i} dQR[h][b,i][r] q_{b,i}   (batched over heads; per batch
     // segment only i >= S-1-r contributes: tri 2, split over segments)
     // (a strided-batched hipBLASLt product over the whole K range, 2x the
@@ -352,7 +428,11 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     int rc = gemm_bf16_tri(2, S, 1, 1, S, HS, B * S, dqr, ldr, B * S * ldr, a.qkv, a.ldq, HS, dR, MSQ_F32, HS,
                            a.S_max * HS, H, MSQ_EPI_ACCUM, nullptr, MSQ_F32, 0, 0, s, dr_ws, dr_ws_bytes(B, S, H));
     if (rc) return msq_set_error(MSQ_ERR_ARG, "flash_bwd: dR product");
-    hipLaunchKernelGGL(flash_bwd_meta_kernel, dim3(1, (unsigned)H, (unsigned)B), dim3(HS), 0, s, a, meta_ds, dqkv, ldd,
-                       dR);
+    if (kv_ver == 3 || kv_ver == 4)
+        hipLaunchKernelGGL(flash_bwd_meta_kernel, dim3(1, (unsigned)H, (unsigned)B), dim3(HS), 0, s, a, meta_ds, dqkv,
+                           ldd, dR);
+    else
+        hipLaunchKernelGGL(flash_bwd_meta5_kernel, dim3(1, (unsigned)H, (unsigned)B), dim3(HS), 0, s, a, lse, Dv, dout,
+                           ldo, dqkv, ldd, dR);
     return 0;
 }

@@ -129,6 +129,7 @@ bool gemm256p_colsum_launch(GemmArgs g, int ta, int tb, int epi, int aux_dtype, 
 // persistent tile, bias epilogue + column (max, sum exp) partials of the stored bf16
 // C per (256-row tile, wave-row) p: part[2p][n] = max, part[2p+1][n] = sum (row stride
 // pld); false when it does not apply
+bool gemm256p_colstats_applies(GemmArgs g, int tb, const float* part, int64_t pld);
 bool gemm256p_colstats_launch(GemmArgs g, int ta, int tb, float* part, int64_t pld, hipStream_t s);
 // skinny-M weight-streaming kernel of the decode steps (gemm_skinny.hip):
 // false when the problem is not M <= 64 / ta = tb = 0 / a forward epilogue

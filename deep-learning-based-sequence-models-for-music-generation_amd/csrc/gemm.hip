@@ -755,22 +755,44 @@ extern "C" size_t msq_gemm_colstats_bytes(int64_t M, int64_t N) {
     return (size_t)((M + 255) / 256) * 4 * ((N + 3) / 4 * 4) * 4;
 }
 
-extern "C" int msq_gemm_bias_colstats(int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
-                                      const void* B, int64_t ldb, void* C, int64_t ldc, const float* bias, float* part,
-                                      int64_t pld, void* stream) {
-    MSQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && part && pld >= N && pld % 4 == 0 && M % 256 == 0,
-                  "msq_gemm_bias_colstats: sizes (M %% 256 == 0, pld >= N, pld %% 4 == 0)");
-    MSQ_CHECK_ARG(lda >= K && ldb >= (tb ? N : K) && ldc >= N && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0 &&
-                      ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0 && ((uintptr_t)C % 16) == 0,
-                  "msq_gemm_bias_colstats: leading dims / alignment (ld %% 8 == 0, 16-B aligned)");
-    GemmArgs g{};
+static bool colstats_args(GemmArgs& g, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                          const void* B, int64_t ldb, const void* C, int64_t ldc, const float* bias, const float* part,
+                          int64_t pld) {
+    if (!(M > 0 && N > 0 && K > 0 && part && pld >= N && pld % 4 == 0 && M % 256 == 0)) return false;
+    if (!(lda >= K && ldb >= (tb ? N : K) && ldc >= N && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0 &&
+          ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0 && ((uintptr_t)C % 16) == 0))
+        return false;
+    g = GemmArgs{};
     g.M = M; g.N = N; g.K = K;
     g.A = A; g.lda = lda;
     g.B = B; g.ldb = ldb;
-    g.C = C; g.ldc = ldc;
+    g.C = (void*)C; g.ldc = ldc;
     g.bias = bias;
     g.batch = 1;
     g.vec = 1;
+    return true;
+}
+
+extern "C" int msq_gemm_bias_colstats_applies(int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                                              const void* B, int64_t ldb, const void* C, int64_t ldc,
+                                              const float* bias, const float* part, int64_t pld) {
+    GemmArgs g;
+    // the other GEMM routes move the large products to another kernel family:
+    // the caller then runs the plain bias GEMM on that route
+    if (gemm_route() != MSQ_ROUTE_DEFAULT) return 0;
+    if (!colstats_args(g, tb, M, N, K, A, lda, B, ldb, C, ldc, bias, part, pld)) return 0;
+    return gemm256p_colstats_applies(g, tb, part, pld) ? 1 : 0;
+}
+
+extern "C" int msq_gemm_bias_colstats(int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                                      const void* B, int64_t ldb, void* C, int64_t ldc, const float* bias, float* part,
+                                      int64_t pld, void* stream) {
+    GemmArgs g;
+    MSQ_CHECK_ARG(colstats_args(g, tb, M, N, K, A, lda, B, ldb, C, ldc, bias, part, pld),
+                  "msq_gemm_bias_colstats: sizes / leading dims / alignment (M %% 256 == 0, pld >= N, pld %% 4 == 0, "
+                  "ld %% 8 == 0, 16-B aligned)");
+    if (gemm_route() != MSQ_ROUTE_DEFAULT)
+        return msq_set_error(MSQ_ERR_UNSUPPORTED, "msq_gemm_bias_colstats: only on the default GEMM route");
     if (!gemm256p_colstats_launch(g, 0, tb, part, pld, (hipStream_t)stream))
         return msq_set_error(MSQ_ERR_UNSUPPORTED, "msq_gemm_bias_colstats: shape outside the persistent 256 tile");
     MSQ_LAUNCH_CHECK();

@@ -511,10 +511,18 @@ bool gemm256p_colsum_launch(GemmArgs g, int ta, int tb, int epi, int aux_dtype, 
 // bias epilogue + per-(M-tile, wave-row) column (max, sum exp) partials of the
 // stored bf16 values into part (row stride pld): the lm_head forward feeding
 // the time-axis logsumexp of the filtered loss (train.py:133-138)
-bool gemm256p_colstats_launch(GemmArgs g, int ta, int tb, float* part, int64_t pld, hipStream_t s) {
+static bool colstats_prepare(GemmArgs& g, int ta, int tb, const float* part, int64_t pld) {
     if (ta != 0 || g.aux) return false;
     if (!p_prepare(g, ta, tb, MSQ_EPI_BIAS, MSQ_BF16, MSQ_F32)) return false;
-    if (pld < g.N || pld % 4 || ((uintptr_t)part % 16) || (int64_t)g.tiles_m * 4 * pld * 4 >= (int64_t)OOB) return false;
+    return !(pld < g.N || pld % 4 || ((uintptr_t)part % 16) || (int64_t)g.tiles_m * 4 * pld * 4 >= (int64_t)OOB);
+}
+
+bool gemm256p_colstats_applies(GemmArgs g, int tb, const float* part, int64_t pld) {
+    return colstats_prepare(g, 0, tb, part, pld);
+}
+
+bool gemm256p_colstats_launch(GemmArgs g, int ta, int tb, float* part, int64_t pld, hipStream_t s) {
+    if (!colstats_prepare(g, ta, tb, part, pld)) return false;
     g.cs_ws = part;
     g.ldx = pld;
     if (tb == 0) launch_p<0, 0, MSQ_EPI_BIAS, bf16, float, 2>(g, s);

@@ -171,7 +171,17 @@ class DecodeCache:
         self.length = 0  # positions absorbed (metadata excluded)
         # the step as one HIP graph (captured on the second step; the first
         # runs eagerly and allocates the step's workspaces)
-        self.graph, self.graph_tok, self.eager_steps = None, None, 0
+        self.graph, self.tok_buf, self.eager_steps = None, None, 0
+
+    def stage_tok(self, tok):
+        """the step graph's token buffer (int64 [B]) holding tok; a new buffer
+        (shape change) drops the captured graph"""
+        if self.tok_buf is None or self.tok_buf.shape != tok.shape or self.tok_buf.device != tok.device:
+            self.tok_buf = torch.empty(tok.shape, dtype=torch.int64, device=tok.device)
+            self.graph = None
+        if tok.data_ptr() != self.tok_buf.data_ptr():
+            self.tok_buf.copy_(tok)
+        return self.tok_buf
 
 
 class MambaEngine:
@@ -293,13 +303,17 @@ class MambaEngine:
         # every launch of a step has fixed pointers and sizes (the recurrent
         # state lives in the cache): replay one captured HIP graph instead of
         # ~7 launches per layer from the host
-        if self.step_graphs and tok.data_ptr() == cache.graph_tok and cache.graph is not None:
+        # (the graph reads the token from the cache's staging buffer: a fresh
+        # token tensor per step costs a device copy, not a re-capture)
+        if self.step_graphs and cache.graph is not None:
+            cache.stage_tok(tok)
             cache.graph.replay()
-        elif self.step_graphs and cache.eager_steps >= 1 and tok.is_contiguous():
+        elif self.step_graphs and cache.eager_steps >= 1:
+            tb = cache.stage_tok(tok)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self._step_body(tok, cache)
-            cache.graph, cache.graph_tok = g, tok.data_ptr()
+                self._step_body(tb, cache)
+            cache.graph = g
             g.replay()
         else:
             self._step_body(tok, cache)

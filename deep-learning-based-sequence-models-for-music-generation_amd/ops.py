@@ -103,9 +103,12 @@ def gemm_bias_colstats(A, W, out, bias, part):
     shape is outside the kernel (the caller runs the plain GEMM)."""
     M, K = A.shape
     N = W.shape[0]
-    # the persistent 256 tile's preconditions (gemm256_plan: >= 128 tiles, K % 8)
-    if A.dtype != torch.bfloat16 or M % 256 or N % 8 or K % 8 or out.shape != (M, N) or \
-            (M // 256) * ((N + 255) // 256) < 128:
+    if A.dtype != torch.bfloat16 or out.shape != (M, N):
+        return False
+    # the kernel's own preconditions (persistent 256 tile, descriptor extents of
+    # C and of the partials, 16-B alignment, GEMM route), asked without a launch
+    if not L.lib().msq_gemm_bias_colstats_applies(0, M, N, K, ptr(A), A.stride(0), ptr(W), W.stride(0), ptr(out),
+                                                   out.stride(0), ptr(bias), ptr(part), part.stride(-2)):
         return False
     call("msq_gemm_bias_colstats", 0, M, N, K, ptr(A), A.stride(0), ptr(W), W.stride(0), ptr(out), out.stride(0),
          ptr(bias), ptr(part), part.stride(-2), stream())

@@ -250,7 +250,17 @@ class TransformerDecodeCache:
         # the step before it goes into the ring, and the captured graph
         self.pos_dev = torch.zeros(1, device=device, dtype=torch.int64)
         self.row_buf = e(B, cfg.v_pad)
-        self.graph, self.graph_tok, self.graph_gen = None, None, None
+        self.graph, self.graph_gen, self.tok_buf = None, None, None
+
+    def stage_tok(self, tok):
+        """the step graph's token buffer (int64 [B]) holding tok; a new buffer
+        (shape change) drops the captured graph"""
+        if self.tok_buf is None or self.tok_buf.shape != tok.shape or self.tok_buf.device != tok.device:
+            self.tok_buf = torch.empty(tok.shape, dtype=torch.int64, device=tok.device)
+            self.graph = None
+        if tok.data_ptr() != self.tok_buf.data_ptr():
+            self.tok_buf.copy_(tok)
+        return self.tok_buf
 
 
 def dx_gemm(dy, W, Wt, name, out):
@@ -447,12 +457,16 @@ class TransformerEngine:
         if not tok.is_cuda:
             raise RuntimeError("the MI355X engine runs on the GPU only (no CPU fallback)")
         self.refresh_shadow()
-        if self.step_graphs and cache.part_valid and tok.is_contiguous() and cache.length >= 1:
-            if cache.graph is None or cache.graph_tok != tok.data_ptr() or cache.graph_gen != self._wgen_now():
+        if self.step_graphs and cache.part_valid and cache.length >= 1:
+            # the graph reads the token from the cache's staging buffer, so a
+            # caller handing a fresh tensor every step costs a device copy,
+            # not a re-capture
+            tb = cache.stage_tok(tok)
+            if cache.graph is None or cache.graph_gen != self._wgen_now():
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    self._step_dev(tok, cache)
-                cache.graph, cache.graph_tok, cache.graph_gen = g, tok.data_ptr(), self._wgen_now()
+                    self._step_dev(tb, cache)
+                cache.graph, cache.graph_gen = g, self._wgen_now()
             cache.graph.replay()
             cache.length += 1
             cache.logits = cache.row_buf

@@ -162,8 +162,14 @@ int msq_gemm_colsum(int ta, int tb, int64_t M, int64_t N, int64_t K, const void*
  * ordered (b, t) with T % 256 == 0: pass part, T / 128 and pld to
  * msq_filtered_ce_bias_part. M % 256 == 0; part holds
  * msq_gemm_colstats_bytes(M, N) bytes at pld = N rounded up to 4. Returns
- * MSQ_ERR_UNSUPPORTED for shapes outside the persistent 256 tile. */
+ * MSQ_ERR_UNSUPPORTED for shapes outside the persistent 256 tile (or with a
+ * GEMM route other than MSQ_ROUTE_DEFAULT); msq_gemm_bias_colstats_applies
+ * answers that for the same arguments without launching (1 / 0; host only,
+ * no device needed): a caller then runs the plain bias GEMM instead. */
 size_t msq_gemm_colstats_bytes(int64_t M, int64_t N);
+int msq_gemm_bias_colstats_applies(int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
+                                   int64_t ldb, const void* C, int64_t ldc, const float* bias, const float* part,
+                                   int64_t pld);
 int msq_gemm_bias_colstats(int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
                            int64_t ldb, void* C, int64_t ldc, const float* bias, float* part, int64_t pld,
                            void* stream);
