@@ -44,14 +44,8 @@ int exact_bwd(const AttnArgs& a, const float* lse, const float* dout, int64_t ld
 // bf16 flash path (attn_flash.hip), hs == 128
 int64_t flash_dqr_ld(int64_t S);
 size_t flash_bwd_workspace(int64_t B, int64_t S, int64_t H);
-int flash_fwd(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s);
-// v2 forward (attn_fwd.hip): 128-query blocks, LDS-DMA K/V/R-ring pipeline; -1 if unsupported
-int flash_fwd2(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s);
-// v3 key/value-major backward pass (attn_bwd3.hip): dK, dV, dQR; -1 if unsupported
-// dS goes to dqr (r-indexed) and dsj (j-indexed), both [H][B][S][ldr]
-int flash_bwd_kv3(const AttnArgs& a, const float* lse, const float* Dv, const bf16* dout, int64_t ldo, bf16* dqkv,
-                  int64_t ldd, bf16* dqr, bf16* dsj, int64_t ldr, float* meta_ds, hipStream_t s);
-// v4 key/value pass (attn_bwd4.hip): same outputs as v3; 32x32x16 MFMAs, one
+// v4 key/value pass (attn_bwd4.hip): dS to dqr (r-indexed) and dsj (j-indexed),
+// both [H][B][S][ldr]; 32x32x16 MFMAs, one
 // wave per SIMD; -1 if unsupported (ldr < S + 128, n_meta > 8, > 4 GB)
 int flash_bwd_kv4(const AttnArgs& a, const float* lse, const float* Dv, const bf16* dout, int64_t ldo, bf16* dqkv,
                   int64_t ldd, bf16* dqr, bf16* dsj, int64_t ldr, float* meta_ds, hipStream_t s);

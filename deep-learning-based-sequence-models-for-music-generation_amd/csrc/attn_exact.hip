@@ -233,14 +233,9 @@ static int relattn_fwd(int dtype, void* out, int64_t ld_out, float* lse, const A
         exact_fwd(a, (float*)out, ld_out, lse, s);
     } else {
         MSQ_CHECK_ARG(a.hs == 128 && a.ldq % 8 == 0 && ld_out % 4 == 0, "msq_relattn_fwd: bf16 path needs hs == 128");
-        // MSQ_ATTN_FWD=1|2|3 selects a kernel generation for A/B runs (default 3)
-        const char* v = getenv("MSQ_ATTN_FWD");
-        const int ver = a.rowmask ? 3 : (v ? atoi(v) : 3);
-        int rc = -1;
-        if (ver >= 3) rc = flash_fwd3(a, (bf16*)out, ld_out, lse, s);
-        if (rc && a.rowmask) return msq_set_error(MSQ_ERR_UNSUPPORTED, "msq_relattn_fwd: dropout needs the v3 kernel");
-        if (rc && ver >= 2) rc = flash_fwd2(a, (bf16*)out, ld_out, lse, s);
-        if (rc) flash_fwd(a, (bf16*)out, ld_out, lse, s);
+        if (flash_fwd3(a, (bf16*)out, ld_out, lse, s))
+            return msq_set_error(MSQ_ERR_UNSUPPORTED,
+                                 "msq_relattn_fwd: shape outside the flash kernel (n_meta > 8 or a > 4 GB operand)");
     }
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;

@@ -1,26 +1,14 @@
-// Relative-position flash attention, bf16 MFMA path (hs = 128).
-//
-// Forward (one workgroup = 4 waves = 64 query rows of one (b, h); each wave
-// owns 16 queries; key tiles of 64):
-//   * scores are computed "swapped" (S^T = K.Q^T) so each lane owns ONE query
-//     row (lane & 15) and 16 of the tile's keys: row max / sum need only two
-//     cross-lane steps, P is already the B operand of the next MFMA and the
-//     output accumulator O^T keeps the query on the lane too (no shuffles);
-//   * the relative term BD(i,j) = q_i . R[S-1-i+j] (model_transformer.py:70-75,
-//     84-90) is a GEMM against a 80-row window of R per wave (R tile staged per
-//     key tile), followed by a per-wave skew through LDS: QR[i][w] -> BD[i][j]
-//     with w = j - i + 15;
-//   * online softmax in the exp2 domain, mask j <= i || j < n_meta implicit;
-//   * the meta-block terms BD(i, j >= i+2) = q_{i+1}.R[j-i-2] (only i < 5) are
-//     added by the single wave that sees tile (0, 0).
-// Backward (flash_bwd below):
-//   pre : D_i = sum_d dO.O
-//   kv  : per 128-key block (attn_bwd3.hip): recompute S, P; dP = dO.V^T;
+// Relative-position flash attention backward, bf16 MFMA path (hs = 128):
+// the host side of the pass sequence and its small kernels
+// (model_transformer.py:54-90 differentiated):
+//   pre : D_i = sum_d dO.O (and the v5 row constants lse log2(e), D scale)
+//   kv  : per 128-key block (attn_bwd5.hip): recompute S, P; dP = dO.V^T;
 //         dS = P (dP - D) scale; dK, dV accumulated in registers; dS written
-//         r-indexed dQR[h][b][i][r = S-1-i+j] and j-indexed dSj[h][b][i][j];
-//   dq  : dq = dSj . K + dQR . R (attn_dq.hip);
+//         once, r-indexed: dQR[h][b][i][r = S-1-i+j];
+//   dq  : dq = dS . K (the j-view of dQR) + dQR . R (attn_dq.hip);
 //   GEMM: dR += dQR^T . Q (batched over heads, split-K partials);
-//   fix : meta-block terms (j > i inside the metadata prefix).
+//   meta: the metadata-prefix entries j > i (flash_bwd_meta5_kernel).
+// The forward is attn_fwd3.hip.
 #include "attn_tiles.h"
 #include "gemm.h"
 #include <cstdlib>
@@ -30,155 +18,6 @@ namespace {
 
 using namespace attn;
 constexpr int NT = 256;
-
-// copy `rows` rows of 128 bf16 (row r from src + r*ld, zero if !valid) into an image
-template <int MODE>  // 0 row, 1 pairs, 2 quads
-__device__ __forceinline__ void stage_rows(char* dst, const bf16* src, int64_t ld, int rows, int64_t first,
-                                           int64_t lo, int64_t hi, int tid) {
-    for (int c = tid; c < rows * 16; c += NT) {
-        const int row = c >> 4, ch = c & 15;
-        const int64_t gr = first + row;
-        u32x4 v = (u32x4){0u, 0u, 0u, 0u};
-        if (gr >= lo && gr < hi) v = *(const u32x4*)(src + gr * ld + ch * 8);
-        const int off = MODE == 0 ? off_row(row, ch) : (MODE == 1 ? off_pairs(row, ch) : off_quads(row, ch));
-        *(u32x4*)(dst + off) = v;
-    }
-}
-
-// --------------------------------------------------------------------- forward
-constexpr int F_QB = 64, F_KB = 64, F_RW = 128, F_SCR = 84;
-constexpr int F_LDS_K = F_KB * 256, F_LDS_R = F_RW * 256, F_LDS_S = 4 * 16 * F_SCR * 4;
-
-__global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(AttnArgs a, bf16* __restrict__ out, int64_t ldo,
-                                                          float* __restrict__ lse) {
-    __shared__ __attribute__((aligned(16))) char smem[F_LDS_K + F_LDS_R + F_LDS_S];
-    char* sK = smem;
-    char* sR = smem + F_LDS_K;  // R window; V overlays it after the QR products
-    float* scr = (float*)(smem + F_LDS_K + F_LDS_R);
-
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, il = lane & 15;
-    const int64_t S = a.S;
-    const int nqb = (int)((S + F_QB - 1) / F_QB);
-    const int qb = nqb - 1 - (int)blockIdx.x;  // heaviest blocks first
-    const int64_t h = blockIdx.y, b = blockIdx.z;
-    const int64_t i0 = (int64_t)qb * F_QB + 16 * w;
-    const int64_t iq = i0 + il;  // this lane's query row
-    const int64_t ldq = a.ldq;
-    const bf16* qkv = (const bf16*)a.qkv;
-    const bf16* Qp = qkv + b * S * ldq + h * HS;
-    const bf16* Kp = Qp + a.H * HS;
-    const bf16* Vp = Kp + a.H * HS;
-    const bf16* Rp = (const bf16*)a.R + h * a.S_max * HS;
-    float* scw = scr + w * 16 * F_SCR;
-
-    // Q fragments (Y operand): Q[iq][32ks + 8g .. +7]
-    bf16x8 qf[4];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-        if (iq < S) qf[ks] = *(const bf16x8*)(Qp + iq * ldq + ks * 32 + g * 8);
-        else qf[ks] = (bf16x8){};
-    }
-
-    f32x4 oacc[8];
-#pragma unroll
-    for (int n = 0; n < 8; ++n) oacc[n] = zero4();
-    float m_run = -INFINITY, l_part = 0.f;
-    const float c2 = a.scale * LOG2E;
-
-    const int64_t last_q = min<int64_t>((int64_t)qb * F_QB + F_QB - 1, S - 1);
-    const int nkt = (int)(last_q / F_KB) + 1;
-    for (int kt = 0; kt < nkt; ++kt) {
-        const int64_t j0 = (int64_t)kt * F_KB;
-        const int64_t rbase = S - F_QB - (int64_t)qb * F_QB + j0;  // R row of window row 0
-        __syncthreads();
-        stage_rows<0>(sK, Kp, ldq, F_KB, j0, 0, S, tid);
-        stage_rows<0>(sR, Rp, HS, F_RW, rbase, 0, S, tid);
-        __syncthreads();
-
-        // S^T tile: sacc[nt][r] = S_ac[key 16nt+4g+r][query il]
-        f32x4 sacc[4];
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-            sacc[nt] = zero4();
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) sacc[nt] = mfma(frag_row(sK, nt * 16, ks, lane), qf[ks], sacc[nt]);
-        }
-        // QR window of this wave: rows wb .. wb+79 of the R tile
-        const int wb = 48 - 16 * w;
-        f32x4 qacc[5];
-#pragma unroll
-        for (int t = 0; t < 5; ++t) {
-            qacc[t] = zero4();
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) qacc[t] = mfma(frag_row(sR, wb + t * 16, ks, lane), qf[ks], qacc[t]);
-        }
-        __syncthreads();  // every wave is done with the R tile
-        stage_rows<2>(sR, Vp, ldq, F_KB, j0, 0, S, tid);
-
-        // skew QR[i][w] -> BD[i][j] through this wave's scratch
-#pragma unroll
-        for (int t = 0; t < 5; ++t) *(f32x4*)(scw + il * F_SCR + t * 16 + 4 * g) = qacc[t];
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_wave_barrier();
-        float sv[4][4];
-        float mx = -INFINITY;
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int jl = nt * 16 + 4 * g + r;
-                const int64_t j = j0 + jl;
-                float s = sacc[nt][r] + scw[il * F_SCR + jl - il + 15];
-                const bool ok = (j < S) && (j <= iq || j < a.n_meta);
-                if (ok && j >= iq + 2) {  // meta block, BD = q_{i+1}.R[j-i-2]
-                    const bf16* q1 = Qp + (iq + 1) * ldq;
-                    const bf16* rr = Rp + (j - iq - 2) * HS;
-                    float acc = 0.f;
-                    for (int d = 0; d < HS; ++d) acc += (float)q1[d] * (float)rr[d];
-                    s += acc;
-                }
-                s = ok ? s * c2 : -INFINITY;
-                sv[nt][r] = s;
-                mx = fmaxf(mx, s);
-            }
-        }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float m_new = fmaxf(m_run, mx);
-        const float alpha = exp2f(m_run - m_new);
-        m_run = m_new;
-        float ps = 0.f;
-        bf16x8 pf[2];
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float p = exp2f(sv[nt][r] - m_new);
-                ps += p;
-                pf[nt >> 1][(nt & 1) * 4 + r] = (bf16)p;
-            }
-        }
-        l_part = l_part * alpha + ps;
-#pragma unroll
-        for (int n = 0; n < 8; ++n) oacc[n] *= alpha;
-        __syncthreads();  // V staged
-        // O^T[d][i] += V^T[d][key] P^T[key][i]
-#pragma unroll
-        for (int n = 0; n < 8; ++n) {
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) oacc[n] = mfma(frag_quads(sR, ks * 32, n * 16, lane), pf[ks], oacc[n]);
-        }
-    }
-    float l = l_part + __shfl_xor(l_part, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    if (iq < S) {
-        const float inv = 1.f / l;
-        bf16* op = out + (b * S + iq) * ldo + h * HS;
-#pragma unroll
-        for (int n = 0; n < 8; ++n) store4(op + n * 16 + 4 * g, oacc[n] * inv);
-        if (g == 0) lse[(b * a.H + h) * S + iq] = (m_run + log2f(l)) / LOG2E;
-    }
-}
 
 // ------------------------------------------------------------ backward: pre
 // D[b,h,i] = sum_d dO[i,d] O[i,d]
@@ -370,12 +209,6 @@ size_t flash_bwd_workspace(int64_t B, int64_t S, int64_t H) {
            align256((size_t)B * H * 64 * 4) + align256(dr_ws_bytes(B, S, H));
 }
 
-int flash_fwd(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s) {
-    const dim3 grid((unsigned)((a.S + F_QB - 1) / F_QB), (unsigned)a.H, (unsigned)a.B);
-    hipLaunchKernelGGL(flash_fwd_kernel, grid, dim3(NT), 0, s, a, out, ldo, lse);
-    return 0;
-}
-
 int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo, const bf16* out, bf16* dqkv,
               int64_t ldd, float* dR, void* ws, bool ws_ready, hipStream_t s) {
     const int64_t B = a.B, S = a.S, H = a.H, ldr = flash_dqr_ld(S);
@@ -408,14 +241,13 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     // key/value pass: dK, dV, and dS in both layouts (v4; MSQ_ATTN_BWD_KV=3
     // selects the v3 pass, kept for A/B measurements)
     // MSQ_ATTN_BWD_KV: 5 (default) the v5 pass storing dS once; 50 v5 also
-    // storing the j-indexed copy; 4 / 3 the older passes (both copies)
+    // storing the j-indexed copy; 4 the older pass (both copies)
     static const int kv_ver = [] {
         const char* e = getenv("MSQ_ATTN_BWD_KV");
         return e ? atoi(e) : 5;
     }();
     const bool ds1 = kv_ver == 5;
-    const int kv_rc = kv_ver == 3   ? flash_bwd_kv3(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s)
-                      : kv_ver == 4 ? flash_bwd_kv4(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s)
+    const int kv_rc = kv_ver == 4 ? flash_bwd_kv4(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s)
                                     : flash_bwd_kv5(a, l2, dsc, dout, ldo, dqkv, ldd, dqr, ds1 ? nullptr : dsj, ldr, s);
     if (kv_rc)
         return msq_set_error(MSQ_ERR_UNSUPPORTED, "flash_bwd: shape outside the key/value pass (n_meta > 8 or > 4 GB)");
@@ -428,7 +260,7 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     int rc = gemm_bf16_tri(2, S, 1, 1, S, HS, B * S, dqr, ldr, B * S * ldr, a.qkv, a.ldq, HS, dR, MSQ_F32, HS,
                            a.S_max * HS, H, MSQ_EPI_ACCUM, nullptr, MSQ_F32, 0, 0, s, dr_ws, dr_ws_bytes(B, S, H));
     if (rc) return msq_set_error(MSQ_ERR_ARG, "flash_bwd: dR product");
-    if (kv_ver == 3 || kv_ver == 4)
+    if (kv_ver == 4)
         hipLaunchKernelGGL(flash_bwd_meta_kernel, dim3(1, (unsigned)H, (unsigned)B), dim3(HS), 0, s, a, meta_ds, dqkv,
                            ldd, dR);
     else

@@ -613,7 +613,7 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
     plan128_ksplit(g, dtype, epilogue);
     g.ws = (float*)ws;
     hipStream_t s = (hipStream_t)stream;
-    if (dtype == MSQ_BF16 && M <= 64 && !getenv("MSQ_GEMM_NOSKINNY") &&
+    if (dtype == MSQ_BF16 && M <= 64 &&
         gemm_skinny_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, (size_t)ws_bytes, s)) {
         MSQ_LAUNCH_CHECK();
         return MSQ_OK;
@@ -631,13 +631,10 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
         // tiles alone would take one more full round of the 256 tile on a few
         // CUs. Run the whole 256-row tiles there and the tail rows with the 128
         // tile. The persistent kernel takes the partial tiles itself (measured
-        // 0.6 ms per step faster than this split at cfg 2; MSQ_GEMM_TAIL=1
-        // splits anyway).
+        // 0.6 ms per step faster than this split at cfg 2).
         GemmArgs p = g;
         const bool split = batch == 1 && epilogue != MSQ_EPI_ACCUM && M % 256 != 0 && M > 256 &&
-                           !getenv("MSQ_GEMM_NOTAIL") &&
-                           (nop || getenv("MSQ_GEMM_TAIL") ||
-                            !gemm256p_applies(g, ta, tb, epilogue, c_dtype, aux_dtype)) &&
+                           (nop || !gemm256p_applies(g, ta, tb, epilogue, c_dtype, aux_dtype)) &&
                            gemm256_plan(p, ta, tb, epilogue) &&
                            (int64_t)p.tiles_m * p.tiles_n % 256 != 0 &&
                            (int64_t)p.tiles_m * p.tiles_n % 256 <= p.tiles_n;

@@ -365,11 +365,7 @@ bool gemm256_colsum_launch(GemmArgs g, int ta, int tb, int epi, int aux_dtype, f
     if (g.N % 4 || g.batch != 1 || ws_bytes < gemm256_colsum_ws_bytes(g.M, g.N) || !gemm256_plan(g, ta, tb, epi))
         return false;
     g.cs_ws = ws;
-    static const bool no_p = [] {
-        const char* e = getenv("MSQ_GEMM_CS_NOP");
-        return e && e[0] == '1';
-    }();
-    if (!no_p && gemm256p_colsum_launch(g, ta, tb, epi, aux_dtype, s)) {
+    if (gemm256p_colsum_launch(g, ta, tb, epi, aux_dtype, s)) {
         hipLaunchKernelGGL(colsum_partials_kernel, dim3((unsigned)((g.N + 63) / 64)), dim3(1024), 0, s, ws,
                            (int64_t)g.tiles_m * 2, g.N, dbias, accumulate);
         return true;

@@ -185,7 +185,7 @@ void launch_plain(const GemmArgs& g, int mt, int ks, hipStream_t s) {
 template <int EPI, typename TC, typename TX>
 void launch_mt(GemmArgs g, size_t ws_bytes, hipStream_t s) {
     const int mt = (int)((g.M + 15) / 16);
-    if (g.K <= SK_WAVES * 2 * 32 && !getenv("MSQ_SKINNY_NOPK")) {
+    if (g.K <= SK_WAVES * 2 * 32) {
         if (mt == 1) launch_pk<EPI, TC, TX, 1>(g, s);
         else if (mt == 2) launch_pk<EPI, TC, TX, 2>(g, s);
         else if (mt == 3) launch_pk<EPI, TC, TX, 3>(g, s);
@@ -226,7 +226,7 @@ bool launch_epi(const GemmArgs& g, int epi, int aux_dtype, size_t wsb, hipStream
 int skinny_ksplit(int64_t M, int64_t N, int64_t K, int64_t* kper) {
     const int64_t ntiles = (N + 15) / 16;
     *kper = K;
-    if (M > 64 || K <= SK_WAVES * 2 * 32 || ntiles >= 128 || N % 4 || getenv("MSQ_SKINNY_NOSPLIT")) return 1;
+    if (M > 64 || K <= SK_WAVES * 2 * 32 || ntiles >= 128 || N % 4) return 1;
     const int64_t want = std::min<int64_t>((256 + ntiles - 1) / ntiles, K / 1024);
     if (want <= 1) return 1;
     const int64_t q = SK_WAVES * 32;  // whole k-steps for every wave of a slice

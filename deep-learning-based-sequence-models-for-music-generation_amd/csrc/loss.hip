@@ -982,7 +982,7 @@ static int filtered_ce_impl(float* loss, void* dlogits, int64_t ldd, float* dbia
     float* part2 = (float*)(ws + (size_t)B * TSPLIT * 2 * V * 4 + (size_t)B * V * 4 + (size_t)B * T * 4 * 2 + 256);
     const bool bfl = dtype == MSQ_BF16;
     const bool stream2 = dlogits && ld % 8 == 0 && ldd % 8 == 0 && ((uintptr_t)logits % 16) == 0 &&
-                         ((uintptr_t)dlogits % 16) == 0 && !getenv("MSQ_CE_V1");
+                         ((uintptr_t)dlogits % 16) == 0;
     if (!stream2) {
         if (bfl) colstats_launch<bf16>(a, col_lse, part, s);
         else colstats_launch<float>(a, col_lse, part, s);

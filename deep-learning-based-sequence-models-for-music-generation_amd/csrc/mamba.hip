@@ -1643,7 +1643,7 @@ extern "C" int msq_mamba_ssd_fwd_state(float* y, int64_t ldy, float* states, flo
     const MambaArgs a = mk(B, L, d_inner, nheads, ldz, ldxc);
     hipStream_t s = (hipStream_t)stream;
     const int nch = (int)((L + Q - 1) / Q);
-    if (dtype == MSQ_BF16 && !getenv("MSQ_MAMBA_SSD_V1")) {
+    if (dtype == MSQ_BF16) {
         float* clast = states + B * nheads * nch * (int64_t)(P * N);
         const dim3 gch((unsigned)(B * nheads * nch));
         allow_lds(ssd2::out_kernel, ssd2::OUT_LDS);
@@ -1739,7 +1739,7 @@ extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, cons
     const MambaArgs a = mk(B, L, d_inner, nheads, ldz, ldxc);
     hipStream_t s = (hipStream_t)stream;
     // dB / dC columns are accumulated with atomics across heads
-    if (dtype == MSQ_BF16 && !getenv("MSQ_MAMBA_SSD_V1")) {
+    if (dtype == MSQ_BF16) {
         MSQ_CHECK_ARG(workspace, "msq_mamba_ssd_bwd: the bf16 path needs msq_mamba_ssd_bwd_workspace() bytes");
         const int nch = (int)((L + Q - 1) / Q);
         const float* clast = states + B * nheads * nch * (int64_t)(P * N);

@@ -399,16 +399,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(TY* __restrict__ y, float* 
 // persistent grid of the LayerNorm backward (4 rows in flight per block); the
 // partial-sum workspace is sized for the largest grid. 768 = 3 waves per SIMD,
 // the kernel's VGPR-bound occupancy: 3.57 ms per cfg-2 step against 4.43 at
-// 512 and 4.72 at 1024 (same box). MSQ_LNB_BLOCKS: A/B switch.
+// 512 and 4.72 at 1024 (same box, round 2).
 constexpr int LN_BWD_MAX_BLOCKS = 1024;
-static int ln_bwd_blocks() {
-    static const int nb = [] {
-        const char* e = getenv("MSQ_LNB_BLOCKS");
-        const int v = e ? atoi(e) : 768;
-        return v < 64 ? 64 : (v > LN_BWD_MAX_BLOCKS ? LN_BWD_MAX_BLOCKS : v);
-    }();
-    return nb;
-}
+static int ln_bwd_blocks() { return 768; }
 
 // dropout keep mask applied to the copy (the gradient into the dropped branch)
 struct CopyDrop {
@@ -423,7 +416,7 @@ struct CopyDrop {
 // residual branch that produced this LayerNorm's input (model_transformer.py
 // :51,101 proj / FFN output biases), which would otherwise be a separate
 // column-sum pass over the same rows
-template <typename TD, typename TO, int MAXC, bool BIAS, bool PF = false>
+template <typename TD, typename TO, int MAXC, bool BIAS>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO* __restrict__ dcopy,
                                                      float* __restrict__ part, const TD* __restrict__ dy,
                                                      const float* __restrict__ x, const float* __restrict__ mean,
@@ -436,17 +429,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
     for (int64_t row = blockIdx.x * 4LL + wid; row < rows; row += (int64_t)gridDim.x * 4) {
         const float mu = mean[row], rs = rstd[row];
         const int64_t xrow = map_row(row, seg, skip);
-        f32x4 xh[MAXC], g[MAXC], acc[MAXC];
+        f32x4 xh[MAXC], g[MAXC];
         float s1 = 0.f, s2 = 0.f;
-        // PF: the accumulated gradient row is read with x and dy (one memory
-        // latency per row instead of two)
-        if (PF) {
-#pragma unroll
-            for (int c = 0; c < MAXC; ++c) {
-                const int col = (c * 64 + lane) * 4;
-                if (col < d) acc[c] = *(const f32x4*)(dxa + xrow * d + col);
-            }
-        }
 #pragma unroll
         for (int c = 0; c < MAXC; ++c) {
             const int col = (c * 64 + lane) * 4;
@@ -473,7 +457,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
             const int col = (c * 64 + lane) * 4;
             if (col < d) {
                 float* dp = dxa + xrow * d + col;
-                f32x4 o = PF ? acc[c] : *(f32x4*)dp;
+                f32x4 o = *(f32x4*)dp;
 #pragma unroll
                 for (int t = 0; t < 4; ++t) o[t] += rs * (g[c][t] - m1 - xh[c][t] * m2);
                 *(f32x4*)dp = o;
@@ -586,11 +570,7 @@ static void ln_bwd_launch_b(float* dxa, TO* dcopy, float* part, const TD* dy, co
                             CopyDrop cd, hipStream_t s) {
     const dim3 grid(ln_bwd_blocks());
     if (d <= 256) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 1, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
-    else if (d <= 1024) {
-        static const bool pf = getenv("MSQ_LNB_PF") != nullptr;  // A/B switch: dx_acc read with x and dy
-        if (pf) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4, BIAS, true>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
-        else hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
-    }
+    else if (d <= 1024) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
     else hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 8, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
 }
 template <typename TD, typename TO>
