@@ -15,15 +15,39 @@ import torch.distributed as dist
 
 
 class GradBuckets:
-    def __init__(self, grads: torch.Tensor, ranges, group=None):
+    def __init__(self, grads: torch.Tensor, ranges, group=None, on_reduced=None):
         """ranges: dict key -> (start, end) slices of ``grads``; keys are the
-        notification ids passed to ``ready``."""
+        notification ids passed to ``ready``. on_reduced(start, end, scale):
+        called on the all-reduce side stream as soon as a bucket's SUM is in
+        (the per-bucket optimizer: train_parallel.TrainStep runs the fused Adam
+        over that slice there, so the last buckets' updates no longer queue
+        behind one global Adam after the backward)."""
         self.grads = grads
         self.ranges = dict(ranges)
         self.group = group
+        self.on_reduced = on_reduced
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.handles = []
         self.side = torch.cuda.Stream(device=grads.device) if grads.is_cuda else None
+
+    def uncovered(self):
+        """(start, end) slices of ``grads`` that no bucket covers"""
+        out, pos = [], 0
+        for s, e in sorted(self.ranges.values()):
+            if s > pos:
+                out.append((pos, s))
+            pos = max(pos, e)
+        if pos < self.grads.numel():
+            out.append((pos, self.grads.numel()))
+        return out
+
+    def _reduce(self, buf, s, e):
+        h = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        if self.on_reduced is None:
+            self.handles.append(h)
+            return
+        h.wait()  # the current (side) stream waits for the collective, the host does not (RCCL)
+        self.on_reduced(s, e, 1.0 / self.world)
 
     def ready(self, key):
         if self.world == 1 or key not in self.ranges:
@@ -35,12 +59,13 @@ class GradBuckets:
             ev.record(torch.cuda.current_stream(self.grads.device))
             with torch.cuda.stream(self.side):
                 self.side.wait_event(ev)
-                self.handles.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+                self._reduce(buf, s, e)
         else:
-            self.handles.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+            self._reduce(buf, s, e)
 
     def finish(self):
-        """Blocks the current stream (not the host) until every bucket is reduced."""
+        """Blocks the current stream (not the host) until every bucket is
+        reduced (and, with on_reduced, updated)."""
         for h in self.handles:
             h.wait()
         self.handles.clear()

@@ -40,13 +40,25 @@ class TrainStep:
         if hasattr(self.eng, "head_stats"):  # the loss's column statistics from the lm_head epilogue
             self.eng.head_stats = os.environ.get("MSQ_NO_HEAD_STATS") != "1"
         self.buckets = None
+        # with world > 1 the fused Adam runs per bucket, on the all-reduce side
+        # stream, as each bucket's SUM arrives (MSQ_GLOBAL_ADAM=1: one Adam over
+        # the whole buffer after the backward); slices of an elementwise
+        # update, so the parameters are bitwise those of the global step
+        self.bucket_adam = os.environ.get("MSQ_GLOBAL_ADAM") != "1"
         if dist.is_initialized() and dist.get_world_size(group) > 1:
-            self.buckets = GradBuckets(self.grads, self.eng.bucket_ranges(), group)
+            self.buckets = GradBuckets(self.grads, self.eng.bucket_ranges(), group,
+                                       on_reduced=self._adam_slice if self.bucket_adam else None)
             self.buckets.broadcast_params(flat)
             self.eng.refresh_shadow(force=True)
             self.eng.layer_grad_ready = self.buckets.ready
         else:
             self.eng.layer_grad_ready = None
+
+    def _adam_slice(self, s, e, scale):
+        sh = self.eng.shadow
+        ops.adam_step(self.model.flat.data[s:e], self.grads[s:e], self.m[s:e], self.v[s:e], self.step_no, self.lr,
+                      self.betas[0], self.betas[1], self.eps, shadow=sh[s:e] if sh is not None else None,
+                      grad_scale=scale)
 
     def __call__(self, src, trg, meta):
         eng, cfg = self.eng, self.eng.cfg
@@ -59,11 +71,16 @@ class TrainStep:
         loss, _ = ce_forward_backward(src, A.logits.view(B, T, cfg.v_pad), trg, cfg.vocab_size, self.grammar,
                                       dlogits=dl.view(B, T, cfg.v_pad), dbias=self.lm_bias_grad,
                                       colpart=A.colpart if getattr(A, "colpart_valid", False) else None)
+        self.step_no += 1  # (the per-bucket Adam inside the backward uses it)
         eng.backward(dl, self.grads, head_bias_done=True)
-        scale = self.buckets.finish() if self.buckets is not None else 1.0
-        self.step_no += 1
-        ops.adam_step(self.model.flat.data, self.grads, self.m, self.v, self.step_no, self.lr, self.betas[0],
-                      self.betas[1], self.eps, shadow=eng.shadow, grad_scale=scale)
+        if self.buckets is not None and self.bucket_adam:
+            scale = self.buckets.finish()
+            for s, e in self.buckets.uncovered():
+                self._adam_slice(s, e, scale)
+        else:
+            scale = self.buckets.finish() if self.buckets is not None else 1.0
+            ops.adam_step(self.model.flat.data, self.grads, self.m, self.v, self.step_no, self.lr, self.betas[0],
+                          self.betas[1], self.eps, shadow=eng.shadow, grad_scale=scale)
         eng.mark_shadow_fresh()
         return loss
 

@@ -57,13 +57,24 @@ def _worker(rank, world, port, q):
     src, trg, meta = _batch()
     sl = slice(rank * 2, rank * 2 + 2)
     flat, lay = _flat(_grads(src[sl], trg[sl], meta[sl]))
-    gb = GradBuckets(flat, transformer_buckets(lay))
+    # per-bucket update as TrainStep runs it (on_reduced after each bucket's
+    # SUM): an elementwise step over the reduced slice; it must see every
+    # bucket exactly once, after its reduction, with the 1/world scale
+    param = torch.zeros_like(flat)
+    seen = []
+
+    def update(s, e, scale):
+        seen.append((s, e))
+        param[s:e] -= 0.5 * flat[s:e] * scale
+
+    gb = GradBuckets(flat, transformer_buckets(lay), on_reduced=update)
     # same notification order as the backward engine: head, layers L-1..0, embeddings
     for key in ["head"] + list(reversed(range(HP["n_layer"]))) + [-1]:
         gb.ready(key)
     scale = gb.finish()
+    assert not gb.uncovered() and sorted(seen) == sorted(gb.ranges.values())
     if rank == 0:
-        q.put((flat * scale).numpy())
+        q.put(((flat * scale).numpy(), (-2.0 * param).numpy()))
     dist.destroy_process_group()
 
 
@@ -77,13 +88,14 @@ def test_two_rank_average_equals_full_batch():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = q.get(timeout=240)
+    got, upd = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     src, trg, meta = _batch()
     full, lay = _flat(_grads(src, trg, meta))
     np.testing.assert_allclose(got, full.numpy(), rtol=1e-4, atol=1e-7)
+    np.testing.assert_array_equal(upd, got)  # the per-bucket update saw the averaged gradient
 
 
 def test_bucket_ranges_cover_layout_exactly():

@@ -28,14 +28,15 @@ pytestmark = pytest.mark.gpu
 HERE = Path(__file__).parent
 
 
-def _run_world2(kind, mode, tmp_path):
+def _run_world2(kind, mode, tmp_path, env=None):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    out = tmp_path / f"{kind}_{mode}.npz"
+    out = tmp_path / f"{kind}_{mode}_{len(env or {})}.npz"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", str(HERE / "ddp_worker.py"), kind, mode, str(out)]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=dict(os.environ, OMP_NUM_THREADS="4"))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, OMP_NUM_THREADS="4", **(env or {})))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return np.load(out)
 
@@ -76,3 +77,15 @@ def test_world2_split_batch_averages_gradients(kind, tmp_path):
     nr = np.linalg.norm(a - b) / np.linalg.norm(b)
     cos = float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
     assert nr < 2e-2 and cos > 0.9995, (nr, cos)
+
+
+@pytest.mark.parametrize("kind", ["transformer", "mamba"])
+def test_world2_per_bucket_adam_equals_global_adam(kind, tmp_path):
+    """The per-bucket Adam (run on the all-reduce side stream as each bucket's
+    SUM arrives, TrainStep default) gives the parameters of one global Adam
+    after the backward (MSQ_GLOBAL_ADAM=1) bit for bit: the update is
+    elementwise and the buckets tile the flat buffer."""
+    a = _run_world2(kind, "split", tmp_path)
+    b = _run_world2(kind, "split", tmp_path, env={"MSQ_GLOBAL_ADAM": "1"})
+    assert np.array_equal(a["grads"], b["grads"])
+    assert np.array_equal(a["flat"], b["flat"])
