@@ -221,3 +221,43 @@ def test_two_stream_backward_matches_single_stream():
     # the embedding backward is the sorted (fixed-order) segment sum: no entries excluded
     err = (g0 - g1).abs().max().item()
     assert err <= 1e-6 * g0.abs().max().item(), err
+
+
+def test_cfg1_shape_fp32_against_oracle():
+    """BASELINE cfg 1's model (2 layers, d_model 128, 8 heads, T 256, B 2 — the
+    reference's CPU-runnable train.py case) through the build's exact fp32
+    path against the oracle (model_transformer.py / train.py restated, pinned
+    by G3): logits 1e-4, loss 1e-4 relative, every gradient within 2e-3 of its
+    max; then one TrainStep (Adam) stays finite and lowers nothing it should not."""
+    vocab, mv = REAL, 568
+    hp = dict(n_embd=128, n_heads=8, n_layer=2, block_len=256)
+    m, p = build(vocab, mv, hp, "fp32")
+    rng = np.random.default_rng(11)
+    B, T = 2, 256
+    w = np.stack([grammar_tokens(rng, vocab, T + 1) for _ in range(B)])
+    src, trg = torch.from_numpy(w[:, :-1].copy()), torch.from_numpy(w[:, 1:].copy())
+    meta = torch.tensor([[519, 279, 202, 202, 202, 178], [452, 272, 202, 202, 202, 184]])
+    logits = m(src.to(dev), meta.to(dev))
+    loss = filtered_cross_entropy(src.to(dev), logits, trg.to(dev), grammar_for(vocab))
+    loss.backward()
+    pr = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    ref_logits = otr.forward(pr, src, meta, hp["n_layer"], hp["n_heads"])
+    ref_loss = oloss.loss(src, trg, ref_logits, vocab)
+    ref_loss.backward()
+    np.testing.assert_allclose(logits.detach().cpu().numpy(), ref_logits.detach().numpy(), rtol=1e-4, atol=1e-4)
+    assert abs(loss.item() - ref_loss.item()) < 1e-4 * abs(ref_loss.item())
+    gd = m.grad_dict()
+    gmax = gd["lm_head.weight"].abs().max().item()
+    for k, g in gd.items():
+        g = g.cpu()
+        if k in ("ln_f.bias", "lm_head.bias"):
+            assert g.abs().max().item() < 1e-3 * gmax, k  # analytically zero (shift invariance)
+            continue
+        r = pr[k].grad
+        assert (g - r).abs().max().item() <= 2e-3 * r.abs().max().item() + 1e-7, k
+    from midiseq.train_parallel import TrainStep
+    m.zero_grad()
+    step = TrainStep(m, grammar=grammar_for(vocab))
+    l1 = step(src.to(dev), trg.to(dev), meta.to(dev))
+    assert abs(l1.item() - ref_loss.item()) < 1e-4 * abs(ref_loss.item())
+    assert torch.isfinite(m.flat.data).all().item()
