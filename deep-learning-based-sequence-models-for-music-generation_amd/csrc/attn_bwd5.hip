@@ -510,6 +510,9 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
     bar();
 #pragma unroll
     for (int k = 0; k < 2; ++k) store_piece(k, it0 + QT * (nqt - 1), (nqt - 1) & 1, true);
+    // the staging DMA issued for tiles past the end (zero-filled) lands before
+    // the workgroup gives its LDS back
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // lane holds dK^T / dV^T [d = 32 db + acc_row(e)][key c32]
     drain_a(dk, dv);
