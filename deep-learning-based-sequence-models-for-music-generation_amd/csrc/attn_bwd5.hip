@@ -499,8 +499,10 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
                 mfma_acc_va(acc.dp, fo, vf[ks]);
             }
         }
-        drain4(acc.s, acc.dp, acc.s, acc.dp);
-        asm volatile("s_nop 15\n\ts_nop 7" : "+v"(acc.q0), "+v"(acc.q1));
+        // (four distinct operands: an asm naming one tuple twice made the
+        // compiler copy it ahead of the wait states, reading the last MFMAs'
+        // results too early)
+        drain4(acc.s, acc.dp, acc.q0, acc.q1);
         skew_setup(0);
         static_for<16>([&](auto E) { skew(E); });
     }

@@ -108,3 +108,7 @@ for h in range(H):
         mx = ref.abs().max()
         bad = (e > 2e-2 * mx).nonzero()
         print(f"  dS h{h} b{b}: max err {e.max() / mx:.3e}; bad entries {len(bad)}: {bad[:12].tolist()}")
+        if h == 0 and b == 0:
+            torch.set_printoptions(precision=4, linewidth=160)
+            print("  got dS[0:7, 0:7]\n", got[:7, :7])
+            print("  ref dS[0:7, 0:7]\n", ref[:7, :7])
