@@ -294,39 +294,49 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
     // (VGPRs; the AGPRs hold dK^T / dV^T and K / V) and the skewed relative
     // term bp of the tile the next iteration's softmax reads
     Acc acc;
-    float bp[16];
+    float bp[16];            // raw window values (the mask applies in stage a)
+    f32x4 Lr[4], Dr[4];      // row constants of the carried tile: lse log2(e), D scale
+    uint32_t vm = 0u, mk = 0u;  // its causal / sequence-end mask and dropout keep word
 
-    // ---- skew of tile T (its q0 / q1 final, >= 16 MFMAs old) into bp, with
-    // the causal / sequence-end mask folded in as -inf (p = exp2(-inf) = 0,
-    // dS = 0 * finite = 0); snippet `e` (one element per C-phase gap)
+    // ---- skew of tile T (its q0 / q1 final, >= 16 MFMAs old) into bp, and
+    // the tile's row constants and masks, all for the NEXT iteration's
+    // softmax: nothing here is read before that iteration's barrier, whose
+    // lgkmcnt(0) retires these LDS reads (the bpermute is an asm statement so
+    // the compiler places no wait behind it; its float-typed result also keeps
+    // the carried value out of an i32 loop phi, which made the allocator move
+    // ~100 values into the AGPR file and spill)
     int sk_z = 0, sk_bpb = 0;
-    uint32_t sk_vm = 0u;
     auto skew_setup = [&](int T) {
-        const int i0 = it0 + QT * T;
+        const int i0 = it0 + QT * T, buf = T % NB;
         // per-tile lane constants made opaque (hoisted, the 16 masks and 16
         // addresses would pin registers for the whole kernel)
         sk_z = lz0;
         sk_bpb = lbpb0;
         asm volatile("" : "+v"(sk_z), "+v"(sk_bpb));
-        // rows k + 4hh valid: jk <= i0 + k + 4hh <= S - 1 (all ones in full tiles);
-        // the metadata tile's j > i entries are left to flash_bwd_meta_kernel
+        // rows k + 4hh valid: jk <= i0 + k + 4hh <= S - 1 (all ones in full
+        // tiles); the metadata tile's j > i entries are left to
+        // flash_bwd_meta5_kernel
         const int lo = ljk - i0 - 4 * lhh, hi = S - 1 - i0 - 4 * lhh;
         const uint32_t up = hi >= 31 ? 0xffffffffu : (hi < 0 ? 0u : (2u << hi) - 1u);
         const uint32_t dn = lo <= 0 ? 0xffffffffu : (lo >= 32 ? 0u : (0xffffffffu << lo));
-        sk_vm = up & dn;
+        vm = up & dn;
+        const float* cL = (const float*)(smem + O_L + buf * 512);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            Lr[g] = *(const f32x4*)(cL + 8 * g + 4 * lhh);
+            Dr[g] = *(const f32x4*)(cL + 64 + 8 * g + 4 * lhh);
+        }
+        // keep word of this lane's key over the tile's 32 queries; bit k of
+        // mk = query row k + 4 hh
+        if (DROP) mk = ((const uint32_t*)(smem + O_D + buf * KB * 4))[32 * w + lc32] >> (4 * lhh);
     };
     auto skew = [&](auto E) {
         constexpr int e = decltype(E)::value, k = (e & 3) + 8 * (e >> 2);
         const float sel = (sk_z >= 31 - k) ? acc.q0[e] : acc.q1[e];
         const int adr = ((sk_bpb - 4 * k) & 124) | lhh7;
-        const int v = __builtin_amdgcn_ds_bpermute(adr, __float_as_int(sel));
-        const int m = __builtin_amdgcn_sbfe((int)sk_vm, k, 1);
-        float b = __int_as_float((v & m) | ((int)0xff800000 & ~m));  // v_bfi: valid ? v : -inf
-        // keep the carried value float-typed: as an i32 loop phi (what
-        // instcombine makes of the bit ops) the allocator moved ~100 values
-        // into the AGPR file and spilled
-        asm volatile("" : "+v"(b));
-        bp[e] = b;
+        float r;
+        asm volatile("ds_bpermute_b32 %0, %1, %2" : "=v"(r) : "v"(adr), "v"(sel));
+        bp[e] = r;
     };
 
     // ---- one iteration (t): with DO_A, A(t+1) runs beside it.
@@ -351,15 +361,15 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
         // tile t+1's data: issued DEPTH iterations ago
         if (t >= DEPTH) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST + (NDMA + NST) * (DEPTH - 1)) : "memory");
         bar();  // tile t+1 landed everywhere; tile t-1's buffers and dS(t-1) staging published
-        const float* cL = (const float*)(smem + O_L + buf * 512);
-        const float* cD = cL + 64;
         float pv[16];
-        uint32_t mk = 0u;
         bf16x8 pa[2], da[2];
-        // stage a: p = exp2((s + bp) c2 - lse log2e); the dropped P for dV
+        // stage a: p = exp2((s + bp) c2 - lse log2e), bp = -inf where masked
+        // (v_bfi); the dropped P for dV
         auto stage_a = [&](auto E) {
             constexpr int e = decltype(E)::value, k = (e & 3) + 8 * (e >> 2);
-            const float p = __builtin_amdgcn_exp2f(fmaf(acc.s[e] + bp[e], c2, -cL[acc_row(e, 0) + 4 * lhh]));
+            const int m = __builtin_amdgcn_sbfe((int)vm, k, 1);
+            const float b = __int_as_float((__float_as_int(bp[e]) & m) | ((int)0xff800000 & ~m));
+            const float p = __builtin_amdgcn_exp2f(fmaf(acc.s[e] + b, c2, -Lr[e >> 2][e & 3]));
             pv[e] = p;
             pa[e >> 3][e & 7] = (bf16)(DROP ? and_f(p, __builtin_amdgcn_sbfe((int)mk, k, 1)) : p);
         };
@@ -368,7 +378,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
             constexpr int e = decltype(E)::value, k = (e & 3) + 8 * (e >> 2);
             float dpv = acc.dp[e];
             if (DROP) dpv = and_f(dpv, __builtin_amdgcn_sbfe((int)mk, k, 1));
-            da[e >> 3][e & 7] = (bf16)(pv[e] * fmaf(dpv, ks_scale, -cD[acc_row(e, 0) + 4 * lhh]));
+            da[e >> 3][e & 7] = (bf16)(pv[e] * fmaf(dpv, ks_scale, -Dr[e >> 2][e & 3]));
         };
         const char* cQn = smem + O_Q + (T % NB) * TILE;
         const char* cOn = smem + O_O + (T % NB) * TILE;
@@ -397,11 +407,6 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
             }
             if constexpr (g < NDMA) dma_piece(g, t + 1 + DEPTH);
             if constexpr (g == NDMA || g == NDMA + 1) store_piece(g - NDMA, i0 - QT, sb ^ 1, t >= 1);
-            if constexpr (g == 0) {
-                // keep word of this lane's key over the tile's 32 queries; bit
-                // k of mk = query row k + 4 hh
-                if (DROP) mk = ((const uint32_t*)(smem + O_D + buf * KB * 4))[32 * w + lc32] >> (4 * lhh);
-            }
             if constexpr (g >= 2) stage_a(std::integral_constant<int, g - 2>{});
             if constexpr (g >= 14) stage_a(std::integral_constant<int, g>{});
             if constexpr (g >= 6) stage_b(std::integral_constant<int, g - 6>{});
