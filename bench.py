@@ -109,9 +109,9 @@ CLASSIFY = {
     # conv fwd: xBC bf16 in, xc bf16 out; bwd: dxc f32 + xBC bf16 in, dxBC bf16 out
     "msq_mamba_conv_fwd": lambda a: ("mamba_conv", None, float(a[7] * a[8]) * 4 * (a[9] + 128)),
     "msq_mamba_conv_bwd": lambda a: ("mamba_conv", None, float(a[10] * a[11]) * 8 * (a[12] + 128)),
-    # gated RMSNorm fwd: y f32 + z bf16 in, yn bf16 + rstd out; bwd: y f32, z, dyn f32 in, dy f32, dz out
-    "msq_mamba_gnorm_fwd": lambda a: ("mamba_gnorm", None, float(a[9]) * (4 * a[10] + 2 * a[10] + 2 * a[10] + 4)),
-    "msq_mamba_gnorm_bwd": lambda a: ("mamba_gnorm", None, float(a[12]) * (4 + 2 + 4 + 4 + 2) * a[13]),
+    # gated RMSNorm fwd: y bf16 + z bf16 in, yn bf16 + rstd out; bwd: y bf16, z, dyn f32 in, dy f32, dz out
+    "msq_mamba_gnorm_fwd": lambda a: ("mamba_gnorm", None, float(a[9]) * (2 * a[10] + 2 * a[10] + 2 * a[10] + 4)),
+    "msq_mamba_gnorm_bwd": lambda a: ("mamba_gnorm", None, float(a[12]) * (2 + 2 + 4 + 4 + 2) * a[13]),
 }
 
 

@@ -56,6 +56,9 @@ int flash_bwd_kv5(const AttnArgs& a, const float* lse, const float* Dv, const bf
 // dq = dSj.K + dQR.R into the q columns of dqkv (attn_dq.hip)
 void flash_bwd_dq(const AttnArgs& a, const bf16* dsj, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd,
                   hipStream_t s);
+// dq v3 (attn_dq3.hip): 256-row tiles, LDS-DMA pipeline over dSj and dQR; -1 if unsupported
+int flash_bwd_dq3(const AttnArgs& a, const bf16* dsj, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd,
+                  hipStream_t s);
 // v3 forward (attn_fwd3.hip): 8 waves x 32 queries, 32-key tiles; -1 if unsupported
 int flash_fwd3(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s);
 int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo, const bf16* out, bf16* dqkv,

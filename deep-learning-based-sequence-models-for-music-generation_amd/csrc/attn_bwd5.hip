@@ -77,10 +77,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
     return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* dst_wave, uint32_t vo) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_char*)dst_wave, 16, vo, 0, 0, 0);
+    lds_dma16(rs, dst_wave, vo);
 }
 __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rs, char* dst_wave, uint32_t vo) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_char*)dst_wave, 4, vo, 0, 0, 0);
+    lds_dma4(rs, dst_wave, vo);
 }
 __device__ __forceinline__ void bar() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -215,31 +215,27 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
     // of the block's keys on waves 2-3, a zero-filling dummy without dropout),
     // R 5-6. Every piece is issued by every wave (out-of-range rows: dropped
     // offset), so the per-iteration vmcnt arithmetic is exact.
+    // Out-of-range rows need no select: every descriptor's num_records ends at
+    // the sequence end, so rows past it (and the R rows before 0, whose offsets
+    // wrap to just below 2^32) read as zeros (launch check: S + 128 rows < 4 GB).
     auto dma_piece = [&](int p, int T) {
         const int i0 = it0 + QT * T, buf = T % NB;
         if (p < 4) {
             const int k = p & 1;
-            const bool ok = i0 + lrow[k] < S;
-            if (p < 2)
-                dma16(rq, smem + O_Q + buf * TILE + w * 2048 + k * 1024,
-                      ok ? offQ[k] + (uint32_t)i0 * (uint32_t)(ldq * 2) : OOB);
-            else
-                dma16(ro, smem + O_O + buf * TILE + w * 2048 + k * 1024,
-                      ok ? offO[k] + (uint32_t)i0 * (uint32_t)(ldo * 2) : OOB);
+            if (p < 2) dma16(rq, smem + O_Q + buf * TILE + w * 2048 + k * 1024, offQ[k] + (uint32_t)i0 * (uint32_t)(ldq * 2));
+            else dma16(ro, smem + O_O + buf * TILE + w * 2048 + k * 1024, offO[k] + (uint32_t)i0 * (uint32_t)(ldo * 2));
         } else if (p == 4) {
             const int ln = ltid & 63;
             if (w < 2) {
-                const bool okl = i0 + ln < S;
-                dma4(w == 0 ? rl : rd, smem + O_L + (buf * 2 + w) * 256, okl ? (uint32_t)((i0 + ln) * 4) : OOB);
+                dma4(w == 0 ? rl : rd, smem + O_L + (buf * 2 + w) * 256, (uint32_t)((i0 + ln) * 4));
             } else {
                 const int key = j0 + 64 * (w - 2) + ln;
                 dma4(rm, smem + O_D + buf * KB * 4 + (w - 2) * 256,
-                     DROP && key < S && i0 < S ? (uint32_t)(mask_word(mld, key, i0) * 4) : OOB);
+                     DROP && i0 < S ? (uint32_t)(mask_word(mld, key, i0) * 4) : OOB);
             }
         } else {
-            const int k = p - 5, c = T + 4, r0 = rw0 + 128 - 32 * c, rg = r0 + lrow[k];
-            dma16(rr, sR + (c % NCH) * TILE + w * 2048 + k * 1024,
-                  (rg >= 0 && rg < S) ? offR[k] + (uint32_t)(r0 * HS * 2) : OOB);
+            const int k = p - 5, c = T + 4, r0 = rw0 + 128 - 32 * c;
+            dma16(rr, sR + (c % NCH) * TILE + w * 2048 + k * 1024, offR[k] + (uint32_t)(r0 * HS * 2));
         }
     };
 
@@ -275,7 +271,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
         const int row = (ltid >> 4) + 16 * k, ch = ltid & 15;
         const u32x4 v = *(const u32x4*)(smem + O_T + sbuf * T_BYTES + row * T_PITCH + ch * 16);
         const int i = ip + row, j = j0 + 8 * ch;
-        const bool in = valid && i < S;
+        const bool in = valid;  // rows past the sequence end: past num_records
         // 32-bit offsets (S * ldr * 2 < 4 GB, checked at launch)
         const uint32_t rowb = (uint32_t)i * (uint32_t)ldr2;
         const __amdgpu_buffer_rsrc_t rqr = make_rsrc(qr_rows, ds_bytes);
@@ -555,7 +551,9 @@ int flash_bwd_kv5(const AttnArgs& a, const float* lse, const float* Dv, const bf
                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
         attr = true;
     }
-    if (a.S * a.ldq * 2 >= (int64_t)OOB || a.S * ldo * 2 >= (int64_t)OOB || a.n_meta > 8) return -1;
+    // rows up to S + 127 (the staging DMA of the tiles past the end) stay below 2^32 bytes
+    if ((a.S + 128) * a.ldq * 2 >= (int64_t)OOB || (a.S + 128) * ldo * 2 >= (int64_t)OOB || a.n_meta > 8) return -1;
+    if ((a.S + 128) * ldr * 2 >= (int64_t)OOB) return -1;
     if (a.colmask && mask_bh_bytes(a.mask_ld) >= (int64_t)OOB) return -1;
     if (ldr < a.S + 128) return -1;
     const dim3 grid((unsigned)((a.S + KB - 1) / KB), (unsigned)a.H, (unsigned)a.B);

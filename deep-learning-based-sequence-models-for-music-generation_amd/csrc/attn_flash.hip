@@ -244,7 +244,7 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     // storing the j-indexed copy; 4 the older pass (both copies)
     static const int kv_ver = [] {
         const char* e = getenv("MSQ_ATTN_BWD_KV");
-        return e ? atoi(e) : 5;
+        return e ? atoi(e) : 50;
     }();
     const bool ds1 = kv_ver == 5;
     const int kv_rc = kv_ver == 4 ? flash_bwd_kv4(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s)
@@ -252,7 +252,13 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     if (kv_rc)
         return msq_set_error(MSQ_ERR_UNSUPPORTED, "flash_bwd: shape outside the key/value pass (n_meta > 8 or > 4 GB)");
     // dq (bf16, q columns of dqkv) = dSj . K + dQR . R
-    flash_bwd_dq(a, ds1 ? nullptr : dsj, dqr, ldr, dqkv, ldd, s);
+    static const int dq_ver = [] {
+        const char* e = getenv("MSQ_ATTN_DQ");
+        return e ? atoi(e) : 3;
+    }();
+    if (ds1 || dq_ver != 3) flash_bwd_dq(a, ds1 ? nullptr : dsj, dqr, ldr, dqkv, ldd, s);
+    else if (flash_bwd_dq3(a, dsj, dqr, ldr, dqkv, ldd, s))
+        return msq_set_error(MSQ_ERR_UNSUPPORTED, "flash_bwd: shape outside the query pass (> 4 GB)");
     // dR[h][r] += sum_{b,i} dQR[h][b,i][r] q_{b,i}   (batched over heads; per batch
     // segment only i >= S-1-r contributes: tri 2, split over segments)
     // (a strided-batched hipBLASLt product over the whole K range, 2x the

@@ -2,6 +2,7 @@
 // (hs = 128 rows of 256 B in LDS; XOR chunk swizzles, see attn_flash.hip).
 #pragma once
 #include "attn.h"
+#include "lds_dma.h"
 
 namespace attn {
 

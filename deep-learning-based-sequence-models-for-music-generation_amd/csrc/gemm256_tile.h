@@ -3,6 +3,7 @@
 // the tile structure.
 #pragma once
 #include "gemm.h"
+#include "lds_dma.h"
 
 namespace g256 {
 
@@ -73,7 +74,7 @@ struct Stage {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const uint32_t vo = (rv[h][j] && kk[j] < krem) ? off[h][j] + kadv : OOB;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(slot + (j * 8 + wu) * 1024), 16, vo, 0, 0, 0);
+            lds_dma16(rs, slot + (j * 8 + wu) * 1024, vo);
         }
     }
 };

@@ -616,9 +616,10 @@ __global__ __launch_bounds__(NT) void ssd_bwd_kernel(MambaArgs a, const T* __res
 }
 
 // ------------------------------------------------------------------ gated RMSNorm
-// out = (y * silu(z)) * rstd * w ; one wave per row (d_inner <= 4096)
+// out = (y * silu(z)) * rstd * w ; one wave per row (d_inner <= 4096); y is in
+// the compute dtype, like z (bf16 in the bf16 path, as mamba_ssm stores it)
 template <typename TZ, typename TO>
-__global__ __launch_bounds__(256) void gnorm_fwd_kernel(const float* __restrict__ y, int64_t ldy,
+__global__ __launch_bounds__(256) void gnorm_fwd_kernel(const TZ* __restrict__ y, int64_t ldy,
                                                         const TZ* __restrict__ z, int64_t ldz,
                                                         const float* __restrict__ w, TO* __restrict__ out,
                                                         int64_t ldo, float* __restrict__ rstd, int64_t rows, int dn,
@@ -628,7 +629,7 @@ __global__ __launch_bounds__(256) void gnorm_fwd_kernel(const float* __restrict_
     if (row >= rows) return;
     float ss = 0.f;
     for (int c = lane * 4; c < dn; c += 256) {
-        const f32x4 yv = *(const f32x4*)(y + row * ldy + c);
+        const f32x4 yv = load4(y + row * ldy + c);
         const f32x4 zv = load4(z + row * ldz + c);
 #pragma unroll
         for (int t = 0; t < 4; ++t) { const float g = yv[t] * silu(zv[t]); ss += g * g; }
@@ -636,7 +637,7 @@ __global__ __launch_bounds__(256) void gnorm_fwd_kernel(const float* __restrict_
     const float r = rsqrtf(wave_sum(ss) / dn + eps);
     if (lane == 0) rstd[row] = r;
     for (int c = lane * 4; c < dn; c += 256) {
-        const f32x4 yv = *(const f32x4*)(y + row * ldy + c);
+        const f32x4 yv = load4(y + row * ldy + c);
         const f32x4 zv = load4(z + row * ldz + c);
         const f32x4 wv = *(const f32x4*)(w + c);
         f32x4 o;
@@ -649,7 +650,7 @@ __global__ __launch_bounds__(256) void gnorm_fwd_kernel(const float* __restrict_
 // decode rows (few rows): one 256-thread block per row, the row in registers
 // (NK = ceil(dn / 1024) <= 4 float4 per thread), one block reduction
 template <typename TZ, typename TO, int NK>
-__global__ __launch_bounds__(256) void gnorm_fwd_row_kernel(const float* __restrict__ y, int64_t ldy,
+__global__ __launch_bounds__(256) void gnorm_fwd_row_kernel(const TZ* __restrict__ y, int64_t ldy,
                                                             const TZ* __restrict__ z, int64_t ldz,
                                                             const float* __restrict__ w, TO* __restrict__ out,
                                                             int64_t ldo, float* __restrict__ rstd, int dn, float eps) {
@@ -662,7 +663,7 @@ __global__ __launch_bounds__(256) void gnorm_fwd_row_kernel(const float* __restr
     for (int k = 0; k < NK; ++k) {
         const int c = tid * 4 + k * 1024;
         if (c < dn) {
-            const f32x4 yv = *(const f32x4*)(y + row * ldy + c);
+            const f32x4 yv = load4(y + row * ldy + c);
             const f32x4 zv = load4(z + row * ldz + c);
 #pragma unroll
             for (int t = 0; t < 4; ++t) { gv[k][t] = yv[t] * silu(zv[t]); ss += gv[k][t] * gv[k][t]; }
@@ -692,7 +693,7 @@ __global__ __launch_bounds__(256) void gnorm_fwd_row_kernel(const float* __restr
 constexpr int GN_K = 16;
 template <typename TZ, typename TD, int NK>
 __global__ __launch_bounds__(256, (NK >= 8 ? 3 : 1)) void gnorm_bwd_kernel(
-    const float* __restrict__ y, int64_t ldy, const TZ* __restrict__ z, int64_t ldz, const float* __restrict__ w,
+    const TZ* __restrict__ y, int64_t ldy, const TZ* __restrict__ z, int64_t ldz, const float* __restrict__ w,
     const float* __restrict__ rstd, const float* __restrict__ dout, int64_t ldd, float* __restrict__ dy,
     TD* __restrict__ dz, float* __restrict__ dw, int64_t rows, int dn) {
     // ZRE (d_inner > 1024): z is read again in the second pass instead of held,
@@ -713,7 +714,7 @@ __global__ __launch_bounds__(256, (NK >= 8 ? 3 : 1)) void gnorm_bwd_kernel(
             yv[k] = dv[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
             if (!ZRE) zv[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
             if (c < dn) {
-                yv[k] = *(const f32x4*)(y + row * ldy + c);
+                yv[k] = load4(y + row * ldy + c);
                 dv[k] = *(const f32x4*)(dout + row * ldd + c);
                 if (!ZRE) zv[k] = load4(z + row * ldz + c);
             }
@@ -760,7 +761,7 @@ __global__ __launch_bounds__(256, (NK >= 8 ? 3 : 1)) void gnorm_bwd_kernel(
 }
 
 template <typename TZ, typename TD>
-void gnorm_bwd_launch(dim3 grid, hipStream_t s, const float* y, int64_t ldy, const TZ* z, int64_t ldz, const float* w,
+void gnorm_bwd_launch(dim3 grid, hipStream_t s, const TZ* y, int64_t ldy, const TZ* z, int64_t ldz, const float* w,
                       const float* rstd, const float* dout, int64_t ldd, float* dy, TD* dz, float* dw, int64_t rows,
                       int dn) {
     const int need = (dn + 255) / 256;
@@ -982,7 +983,7 @@ __global__ __launch_bounds__(256) void pass_kernel(float* __restrict__ states, c
 __global__ __launch_bounds__(256) void out_kernel(MambaArgs a, const bf16* __restrict__ xc,
                                                   const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
                                                   const float* __restrict__ A_log, const float* __restrict__ Dp,
-                                                  float* __restrict__ y, int64_t ldy, const float* __restrict__ states,
+                                                  bf16* __restrict__ y, int64_t ldy, const float* __restrict__ states,
                                                   int nch, float* __restrict__ clast) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sCB = smem;           // half 0: C [t][n];     half 1: B [s][n]
@@ -1050,7 +1051,7 @@ __global__ __launch_bounds__(256) void out_kernel(MambaArgs a, const bf16* __res
         for (int j = 0; j < 2; ++j) {
             const int pcol = cb + 16 * j + 4 * g;
             const f32x4 xv = load4(xc + row * a.ldxc + k.h * P + pcol);
-            *(f32x4*)(y + row * ldy + k.h * P + pcol) = y1[i][j] + et * y2[i][j] + Dh * xv;
+            store4(y + row * ldy + k.h * P + pcol, y1[i][j] + et * y2[i][j] + Dh * xv);
         }
     }
 }
@@ -1635,7 +1636,7 @@ extern "C" int msq_mamba_conv_fwd(void* xc, int64_t ldxc, const void* zxbcdt, in
     return MSQ_OK;
 }
 
-extern "C" int msq_mamba_ssd_fwd_state(float* y, int64_t ldy, float* states, float* final_state, const void* xc,
+extern "C" int msq_mamba_ssd_fwd_state(void* y, int64_t ldy, float* states, float* final_state, const void* xc,
                                        int64_t ldxc, const void* zxbcdt, int64_t ldz, int dtype,
                                        const float* dt_bias, const float* A_log, const float* D, int64_t B,
                                        int64_t L, int64_t d_inner, int64_t nheads, void* stream) {
@@ -1661,20 +1662,19 @@ extern "C" int msq_mamba_ssd_fwd_state(float* y, int64_t ldy, float* states, flo
                                final_state);
         }
         hipLaunchKernelGGL(ssd2::out_kernel, gch, dim3(256), ssd2::OUT_LDS, s, a, (const bf16*)xc,
-                           (const bf16*)zxbcdt, dt_bias, A_log, D, y, ldy, states, nch, clast);
+                           (const bf16*)zxbcdt, dt_bias, A_log, D, (bf16*)y, ldy, states, nch, clast);
         MSQ_LAUNCH_CHECK();
         return MSQ_OK;
     }
     const dim3 grid((unsigned)(B * nheads));
-    allow_lds(ssd_fwd_kernel<bf16>, FWD_LDS);
     allow_lds(ssd_fwd_kernel<float>, FWD_LDS);
-    if (dtype == MSQ_BF16) hipLaunchKernelGGL(ssd_fwd_kernel<bf16>, grid, dim3(NT), FWD_LDS, s, a, (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, D, y, ldy, states, final_state);
-    else hipLaunchKernelGGL(ssd_fwd_kernel<float>, grid, dim3(NT), FWD_LDS, s, a, (const float*)xc, (const float*)zxbcdt, dt_bias, A_log, D, y, ldy, states, final_state);
+    hipLaunchKernelGGL(ssd_fwd_kernel<float>, grid, dim3(NT), FWD_LDS, s, a, (const float*)xc, (const float*)zxbcdt,
+                       dt_bias, A_log, D, (float*)y, ldy, states, final_state);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }
 
-extern "C" int msq_mamba_ssd_fwd(float* y, int64_t ldy, float* states, const void* xc, int64_t ldxc,
+extern "C" int msq_mamba_ssd_fwd(void* y, int64_t ldy, float* states, const void* xc, int64_t ldxc,
                                  const void* zxbcdt, int64_t ldz, int dtype, const float* dt_bias,
                                  const float* A_log, const float* D, int64_t B, int64_t L, int64_t d_inner,
                                  int64_t nheads, void* stream) {
@@ -1682,7 +1682,7 @@ extern "C" int msq_mamba_ssd_fwd(float* y, int64_t ldy, float* states, const voi
                                    d_inner, nheads, stream);
 }
 
-extern "C" int msq_mamba_gnorm_fwd(void* out, int64_t ldo, float* rstd, const float* y, int64_t ldy,
+extern "C" int msq_mamba_gnorm_fwd(void* out, int64_t ldo, float* rstd, const void* y, int64_t ldy,
                                    const void* zxbcdt, int64_t ldz, int dtype, const float* w, int64_t rows,
                                    int64_t d_inner, float eps, void* stream) {
     MSQ_CHECK_ARG(rows > 0 && d_inner % 4 == 0 && d_inner <= 4096, "mamba gnorm: bad sizes");
@@ -1690,21 +1690,21 @@ extern "C" int msq_mamba_gnorm_fwd(void* out, int64_t ldo, float* rstd, const fl
     if (rows <= 1024) {  // decode steps: a block per row
         const int nk = (int)((d_inner + 1023) / 1024);
 #define GN_ROW(NK)                                                                                                     \
-    if (dtype == MSQ_BF16) hipLaunchKernelGGL((gnorm_fwd_row_kernel<bf16, bf16, NK>), dim3((unsigned)rows), dim3(256), 0, s, y, ldy, (const bf16*)zxbcdt, ldz, w, (bf16*)out, ldo, rstd, (int)d_inner, eps); \
-    else hipLaunchKernelGGL((gnorm_fwd_row_kernel<float, float, NK>), dim3((unsigned)rows), dim3(256), 0, s, y, ldy, (const float*)zxbcdt, ldz, w, (float*)out, ldo, rstd, (int)d_inner, eps);
+    if (dtype == MSQ_BF16) hipLaunchKernelGGL((gnorm_fwd_row_kernel<bf16, bf16, NK>), dim3((unsigned)rows), dim3(256), 0, s, (const bf16*)y, ldy, (const bf16*)zxbcdt, ldz, w, (bf16*)out, ldo, rstd, (int)d_inner, eps); \
+    else hipLaunchKernelGGL((gnorm_fwd_row_kernel<float, float, NK>), dim3((unsigned)rows), dim3(256), 0, s, (const float*)y, ldy, (const float*)zxbcdt, ldz, w, (float*)out, ldo, rstd, (int)d_inner, eps);
         if (nk == 1) { GN_ROW(1) } else if (nk == 2) { GN_ROW(2) } else if (nk == 3) { GN_ROW(3) } else { GN_ROW(4) }
 #undef GN_ROW
         MSQ_LAUNCH_CHECK();
         return MSQ_OK;
     }
     const dim3 grid((unsigned)((rows + 3) / 4));
-    if (dtype == MSQ_BF16) hipLaunchKernelGGL((gnorm_fwd_kernel<bf16, bf16>), grid, dim3(256), 0, s, y, ldy, (const bf16*)zxbcdt, ldz, w, (bf16*)out, ldo, rstd, rows, (int)d_inner, eps);
-    else hipLaunchKernelGGL((gnorm_fwd_kernel<float, float>), grid, dim3(256), 0, s, y, ldy, (const float*)zxbcdt, ldz, w, (float*)out, ldo, rstd, rows, (int)d_inner, eps);
+    if (dtype == MSQ_BF16) hipLaunchKernelGGL((gnorm_fwd_kernel<bf16, bf16>), grid, dim3(256), 0, s, (const bf16*)y, ldy, (const bf16*)zxbcdt, ldz, w, (bf16*)out, ldo, rstd, rows, (int)d_inner, eps);
+    else hipLaunchKernelGGL((gnorm_fwd_kernel<float, float>), grid, dim3(256), 0, s, (const float*)y, ldy, (const float*)zxbcdt, ldz, w, (float*)out, ldo, rstd, rows, (int)d_inner, eps);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }
 
-extern "C" int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const float* y, int64_t ldy, const void* zxbcdt,
+extern "C" int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const void* y, int64_t ldy, const void* zxbcdt,
                                    int64_t ldz, int dtype, const float* w, const float* rstd, const float* dout,
                                    int64_t ldd, float* dw, int64_t rows, int64_t d_inner, void* stream) {
     MSQ_CHECK_ARG(rows > 0 && d_inner % 4 == 0 && d_inner <= 256 * GN_K, "mamba gnorm bwd: bad sizes");
@@ -1713,10 +1713,10 @@ extern "C" int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const float* y, int
     // reduces its dw partials in LDS first
     const dim3 grid(768);
     if (dtype == MSQ_BF16)
-        gnorm_bwd_launch<bf16, bf16>(grid, s, y, ldy, (const bf16*)zxbcdt, ldz, w, rstd, dout, ldd, dy, (bf16*)dzxbcdt,
+        gnorm_bwd_launch<bf16, bf16>(grid, s, (const bf16*)y, ldy, (const bf16*)zxbcdt, ldz, w, rstd, dout, ldd, dy, (bf16*)dzxbcdt,
                                      dw, rows, (int)d_inner);
     else
-        gnorm_bwd_launch<float, float>(grid, s, y, ldy, (const float*)zxbcdt, ldz, w, rstd, dout, ldd, dy,
+        gnorm_bwd_launch<float, float>(grid, s, (const float*)y, ldy, (const float*)zxbcdt, ldz, w, rstd, dout, ldd, dy,
                                        (float*)dzxbcdt, dw, rows, (int)d_inner);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;

@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void conv_step_kernel(T* __restrict__ xc, int6
 // 15.6 us per layer at B = 64, H = 32 (4.3 TB/s) against 19.0 us for the
 // previous row-per-4-threads mapping (rocprofv3, same box)
 template <typename T>
-__global__ __launch_bounds__(256) void ssd_step_kernel(float* __restrict__ y, int64_t ldy, float* __restrict__ state,
+__global__ __launch_bounds__(256) void ssd_step_kernel(T* __restrict__ y, int64_t ldy, float* __restrict__ state,
                                                        const T* __restrict__ xc, int64_t ldxc, const T* __restrict__ zx,
                                                        int64_t ldz, int64_t d_inner, int64_t conv_dim, int64_t H,
                                                        const float* __restrict__ dt_bias,
@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void ssd_step_kernel(float* __restrict__ y, in
         ys += __shfl_xor(ys, 2, 64);
         ys += __shfl_xor(ys, 4, 64);
         ys += __shfl_xor(ys, 8, 64);
-        if (c4 == 0) y[b * ldy + h * P + p] = ys + Dh * x;
+        if (c4 == 0) y[b * ldy + h * P + p] = (T)(ys + Dh * x);
     }
 }
 
@@ -137,7 +137,7 @@ extern "C" int msq_mamba_conv_step(void* xc, int64_t ldxc, float* conv_state, co
     return MSQ_OK;
 }
 
-extern "C" int msq_mamba_ssd_step(float* y, int64_t ldy, float* ssm_state, const void* xc, int64_t ldxc,
+extern "C" int msq_mamba_ssd_step(void* y, int64_t ldy, float* ssm_state, const void* xc, int64_t ldxc,
                                   const void* zxbcdt, int64_t ldz, int dtype, const float* dt_bias,
                                   const float* A_log, const float* D, int64_t B, int64_t d_inner, int64_t nheads,
                                   void* stream) {
@@ -148,10 +148,10 @@ extern "C" int msq_mamba_ssd_step(float* y, int64_t ldy, float* ssm_state, const
     const dim3 grid((unsigned)(B * nheads));
     hipStream_t s = (hipStream_t)stream;
     if (dtype == MSQ_BF16)
-        hipLaunchKernelGGL(ssd_step_kernel<bf16>, grid, dim3(256), 0, s, y, ldy, ssm_state, (const bf16*)xc, ldxc,
+        hipLaunchKernelGGL(ssd_step_kernel<bf16>, grid, dim3(256), 0, s, (bf16*)y, ldy, ssm_state, (const bf16*)xc, ldxc,
                            (const bf16*)zxbcdt, ldz, d_inner, cd, nheads, dt_bias, A_log, D);
     else
-        hipLaunchKernelGGL(ssd_step_kernel<float>, grid, dim3(256), 0, s, y, ldy, ssm_state, (const float*)xc, ldxc,
+        hipLaunchKernelGGL(ssd_step_kernel<float>, grid, dim3(256), 0, s, (float*)y, ldy, ssm_state, (const float*)xc, ldxc,
                            (const float*)zxbcdt, ldz, d_inner, cd, nheads, dt_bias, A_log, D);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;

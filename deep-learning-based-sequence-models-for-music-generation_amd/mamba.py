@@ -122,7 +122,7 @@ class _MActs:
         self.xa = e(n + 1 if save else 2, M, cfg.d_model)    # act copies (in_proj inputs)
         self.zx = e(n, M, cfg.d_in_proj)
         self.xc = e(n, M, cfg.conv_dim)
-        self.y = e(n, M, cfg.d_inner, dt=f32)
+        self.y = e(n, M, cfg.d_inner)                        # SSD output, compute dtype
         self.yn = e(n, M, cfg.d_inner)
         self.rstd = e(n, M, dt=f32)
         nst = L.lib().msq_mamba_states_size(B, L_, cfg.nheads) // 4
@@ -162,7 +162,7 @@ class DecodeCache:
         self.xa = e(B, cfg.d_model)
         self.zx = e(B, cfg.d_in_proj)
         self.xc = e(B, cfg.conv_dim)
-        self.y = e(B, cfg.d_inner, dt=f32)
+        self.y = e(B, cfg.d_inner)
         self.yn = e(B, cfg.d_inner)
         self.rstd = e(B, dt=f32)
         self.f = e(B, cfg.d_model)

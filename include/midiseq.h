@@ -332,17 +332,19 @@ int msq_decode_sample(int64_t* hist, int64_t ld_hist, int64_t cur_len, float* z_
 size_t msq_mamba_states_size(int64_t B, int64_t L, int64_t nheads);
 int msq_mamba_conv_fwd(void* xc, int64_t ldxc, const void* zxbcdt, int64_t ldz, int dtype, const float* conv_w,
                        const float* conv_b, int64_t B, int64_t L, int64_t d_inner, int64_t nheads, void* stream);
-/* y fp32 [B*L, ldy] = SSD(x, dt, A, B, C) + D x; states receive the fp32
- * chunk-entry states (msq_mamba_states_size bytes) used by the backward.    */
-int msq_mamba_ssd_fwd(float* y, int64_t ldy, float* states, const void* xc, int64_t ldxc, const void* zxbcdt,
+/* y [B*L, ldy] (in dtype: bf16 as mamba_ssm stores it, or fp32) = SSD(x, dt,
+ * A, B, C) + D x; states receive the fp32 chunk-entry states
+ * (msq_mamba_states_size bytes) used by the backward.                        */
+int msq_mamba_ssd_fwd(void* y, int64_t ldy, float* states, const void* xc, int64_t ldxc, const void* zxbcdt,
                       int64_t ldz, int dtype, const float* dt_bias, const float* A_log, const float* D, int64_t B,
                       int64_t L, int64_t d_inner, int64_t nheads, void* stream);
-/* out = (y * silu(z)) * rsqrt(mean((y*silu(z))^2) + eps) * w  (RMSNormGated) */
-int msq_mamba_gnorm_fwd(void* out, int64_t ldo, float* rstd, const float* y, int64_t ldy, const void* zxbcdt,
+/* out = (y * silu(z)) * rsqrt(mean((y*silu(z))^2) + eps) * w  (RMSNormGated);
+ * y in dtype (msq_mamba_ssd_fwd's output)                                    */
+int msq_mamba_gnorm_fwd(void* out, int64_t ldo, float* rstd, const void* y, int64_t ldy, const void* zxbcdt,
                         int64_t ldz, int dtype, const float* w, int64_t rows, int64_t d_inner, float eps,
                         void* stream);
 /* dy (fp32, ld = ldy) and dz (into dzxbcdt[:, :d_inner]); dw accumulates.   */
-int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const float* y, int64_t ldy, const void* zxbcdt, int64_t ldz,
+int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const void* y, int64_t ldy, const void* zxbcdt, int64_t ldz,
                         int dtype, const float* w, const float* rstd, const float* dout, int64_t ldd, float* dw,
                         int64_t rows, int64_t d_inner, void* stream);
 /* dxc fp32 [B*L, ldxc]: dx (written) | dB, dC (reduced over heads); dt_raw
@@ -364,7 +366,7 @@ int msq_mamba_conv_bwd(void* dzxbcdt, const float* dxc, int64_t ld_dxc, const vo
  * mixer is causal and the per-step full forward equals one recurrent step).
  * msq_mamba_ssd_fwd_state = msq_mamba_ssd_fwd + the state after the last
  * position, final_state fp32 [B][H][64][64] (NULL = none): the prefill.      */
-int msq_mamba_ssd_fwd_state(float* y, int64_t ldy, float* states, float* final_state, const void* xc,
+int msq_mamba_ssd_fwd_state(void* y, int64_t ldy, float* states, float* final_state, const void* xc,
                             int64_t ldxc, const void* zxbcdt, int64_t ldz, int dtype, const float* dt_bias,
                             const float* A_log, const float* D, int64_t B, int64_t L, int64_t d_inner,
                             int64_t nheads, void* stream);
@@ -375,8 +377,8 @@ int msq_mamba_conv_step(void* xc, int64_t ldxc, float* conv_state, const void* z
                         const float* conv_w, const float* conv_b, int64_t B, int64_t d_inner, int64_t nheads,
                         void* stream);
 /* one position: h = exp(dt A) h + dt x B^T (ssm_state fp32 [B][H][64][64],
- * in place); y[b] (fp32) = h C + D x.                                        */
-int msq_mamba_ssd_step(float* y, int64_t ldy, float* ssm_state, const void* xc, int64_t ldxc, const void* zxbcdt,
+ * in place); y[b] (in dtype) = h C + D x.                                    */
+int msq_mamba_ssd_step(void* y, int64_t ldy, float* ssm_state, const void* xc, int64_t ldxc, const void* zxbcdt,
                        int64_t ldz, int dtype, const float* dt_bias, const float* A_log, const float* D, int64_t B,
                        int64_t d_inner, int64_t nheads, void* stream);
 /* filtered logit of one new position (train.py:133-138): col_lse fp32 [B][V]

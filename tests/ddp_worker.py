@@ -43,6 +43,7 @@ def full_batch(T=128, B=4):
 def rank_slice(mode, rank, world, B=4):
     if mode == "same":
         return slice(0, B // world)
+    # "split" and "bucketcheck": each rank its own rows
     n = B // world
     return slice(rank * n, (rank + 1) * n)
 
@@ -92,13 +93,27 @@ def _main():
             model.flat.data.mul_(1.5)
     step = TrainStep(model)
     assert step.buckets is not None
+    flat0 = model.flat.data.clone()  # after the parameter broadcast
     src, trg, meta = full_batch()
     sl = rank_slice(mode, rank, world)
     loss = step(src[sl].cuda(), trg[sl].cuda(), meta[sl].cuda())
     torch.cuda.synchronize()
+    extra = {}
+    if mode == "bucketcheck":
+        # the same step's reduced gradients through one global fused Adam (the
+        # MSQ_GLOBAL_ADAM=1 update) from the same start: the per-bucket Adam
+        # inside the backward must have produced these parameters bit for bit
+        from midiseq import ops
+        ref = flat0.clone()
+        m, v = torch.zeros_like(ref), torch.zeros_like(ref)
+        ops.adam_step(ref, step.grads, m, v, step.step_no, step.lr, step.betas[0], step.betas[1], step.eps,
+                      grad_scale=1.0 / world)
+        torch.cuda.synchronize()
+        extra = dict(ref=ref.cpu().numpy(), m=step.m.cpu().numpy(), m_ref=m.cpu().numpy(), v=step.v.cpu().numpy(),
+                     v_ref=v.cpu().numpy())
     if rank == 0:
         np.savez(out, grads=(step.grads / world).cpu().numpy(), flat=model.flat.data.cpu().numpy(),
-                 loss=loss.item())
+                 loss=loss.item(), **extra)
     dist.barrier()
     dist.destroy_process_group()
 

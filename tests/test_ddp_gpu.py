@@ -82,10 +82,16 @@ def test_world2_split_batch_averages_gradients(kind, tmp_path):
 @pytest.mark.parametrize("kind", ["transformer", "mamba"])
 def test_world2_per_bucket_adam_equals_global_adam(kind, tmp_path):
     """The per-bucket Adam (run on the all-reduce side stream as each bucket's
-    SUM arrives, TrainStep default) gives the parameters of one global Adam
-    after the backward (MSQ_GLOBAL_ADAM=1) bit for bit: the update is
-    elementwise and the buckets tile the flat buffer."""
-    a = _run_world2(kind, "split", tmp_path)
+    SUM arrives, TrainStep default) gives, from the same start and the same
+    reduced gradients, the parameters and moments of one global Adam after the
+    backward (the MSQ_GLOBAL_ADAM=1 update) bit for bit: the update is
+    elementwise and the buckets tile the flat buffer. (Two separate runs are
+    not compared: the backward's atomics make their gradients differ in the
+    last bits.) The MSQ_GLOBAL_ADAM=1 path itself must also run and agree to
+    within that gradient noise."""
+    a = _run_world2(kind, "bucketcheck", tmp_path)
+    assert np.array_equal(a["flat"], a["ref"])
+    assert np.array_equal(a["m"], a["m_ref"]) and np.array_equal(a["v"], a["v_ref"])
     b = _run_world2(kind, "split", tmp_path, env={"MSQ_GLOBAL_ADAM": "1"})
-    assert np.array_equal(a["grads"], b["grads"])
-    assert np.array_equal(a["flat"], b["flat"])
+    d = np.abs(a["flat"] - b["flat"])
+    assert d.max() <= 1e-6 and (d > 2e-7).sum() <= 16, (d.max(), (d > 2e-7).sum())

@@ -1,5 +1,5 @@
-"""GEMM shapes of the cfg-2 train step: 128x128 tile (MSQ_GEMM128=1) vs the
-256x256 LDS-DMA tile vs torch.matmul (hipBLASLt) as the known-good
+"""GEMM shapes of the cfg-2 train step: the per-tile 256x256 kernel vs the
+default route (persistent tile / split-K) vs torch.matmul (hipBLASLt) as the known-good
 reference, random bf16 operands, HIP-event timing on the current stream.
 Usage: python tools/gemm_bench.py"""
 import os
@@ -61,20 +61,15 @@ def main():
                   bias=bias if epi in (L.EPI_BIAS, L.EPI_BIAS_RELU, L.EPI_BIAS_RESID) else None, aux=aux)
         fl = 2.0 * m * n * k
         res = {}
-        for tag, env in (("g128", "MSQ_GEMM128"), ("g256nt", "MSQ_GEMM_NOTAIL"), ("g256", None)):
-            os.environ.pop("MSQ_GEMM128", None)
-            os.environ.pop("MSQ_GEMM_NOTAIL", None)
-            if env:
-                os.environ[env] = "1"
+        for tag, route in (("tile256", L.ROUTE_TILE256), ("default", L.ROUTE_DEFAULT)):
             out.zero_()
-            ms = timeit(lambda: ops.gemm(A, Bm, **kw))
-            res[tag] = (ms, fl / ms / 1e9)
-            if tag == "g256":
-                out.zero_()
-                ops.gemm(A, Bm, **kw)
-                got = out.float()
-        os.environ.pop("MSQ_GEMM128", None)
-        os.environ.pop("MSQ_GEMM_NOTAIL", None)
+            with ops.gemm_route(route):
+                ms = timeit(lambda: ops.gemm(A, Bm, **kw))
+                res[tag] = (ms, fl / ms / 1e9)
+                if tag == "default":
+                    out.zero_()
+                    ops.gemm(A, Bm, **kw)
+                    got = out.float()
         At = A.t() if ta else A
         Bt = Bm if tb else Bm.t()
         ms = timeit(lambda: torch.matmul(At, Bt))
