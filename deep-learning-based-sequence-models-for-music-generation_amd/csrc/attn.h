@@ -44,20 +44,12 @@ int exact_bwd(const AttnArgs& a, const float* lse, const float* dout, int64_t ld
 // bf16 flash path (attn_flash.hip), hs == 128
 int64_t flash_dqr_ld(int64_t S);
 size_t flash_bwd_workspace(int64_t B, int64_t S, int64_t H);
-// v4 key/value pass (attn_bwd4.hip): dS to dqr (r-indexed) and dsj (j-indexed),
-// both [H][B][S][ldr]; 32x32x16 MFMAs, one
-// wave per SIMD; -1 if unsupported (ldr < S + 128, n_meta > 8, > 4 GB)
-int flash_bwd_kv4(const AttnArgs& a, const float* lse, const float* Dv, const bf16* dout, int64_t ldo, bf16* dqkv,
-                  int64_t ldd, bf16* dqr, bf16* dsj, int64_t ldr, float* meta_ds, hipStream_t s);
-// v5 key/value pass (attn_bwd5.hip): software-pipelined v4; dsj == nullptr
-// writes dS only r-indexed (dqr); -1 if unsupported
+// v5 key/value pass (attn_bwd5.hip): dS to dqr (r-indexed) and dsj
+// (j-indexed), both [H][B][S][ldr]; -1 if unsupported
 int flash_bwd_kv5(const AttnArgs& a, const float* lse, const float* Dv, const bf16* dout, int64_t ldo, bf16* dqkv,
                   int64_t ldd, bf16* dqr, bf16* dsj, int64_t ldr, hipStream_t s);
 // dq = dSj.K + dQR.R into the q columns of dqkv (attn_dq.hip)
 void flash_bwd_dq(const AttnArgs& a, const bf16* dsj, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd,
-                  hipStream_t s);
-// dq v3 (attn_dq3.hip): 256-row tiles, LDS-DMA pipeline over dSj and dQR; -1 if unsupported
-int flash_bwd_dq3(const AttnArgs& a, const bf16* dsj, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd,
                   hipStream_t s);
 // v3 forward (attn_fwd3.hip): 8 waves x 32 queries, 32-key tiles; -1 if unsupported
 int flash_fwd3(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s);

@@ -6,12 +6,12 @@
 //   dV_j  = ks sum_i P_ij m_ij dO_i,  dK_j = sum_i dS_ij q_i   (accumulated here)
 //   (m_ij the dropout keep bit, ks = 1/(1-p); m = 1, ks = 1 without dropout)
 //   dS written r-indexed, dQR[h][b][i][r = S-1-i+j] (the dq kernel reads its
-//   j-view, the dR product its r-view), and with DSJ also j-indexed (dSj).
+//   j-view, the dR product its r-view), and j-indexed (dSj, dq's K term).
 //   The metadata-block entries j > i (i < j < n_meta: keys every query sees)
 //   are masked here like the rest of the upper triangle; flash_bwd_meta_kernel
 //   adds their dK / dV / dq / dR terms.
 //
-// Geometry as v4 (attn_bwd4.hip): one workgroup = 4 waves, one per SIMD, =
+// Geometry as v4 (round 3, replaced by this pass): one workgroup = 4 waves, one per SIMD, =
 // 128 keys of one (b, h); a wave owns 32 keys on the lanes of
 // v_mfma_f32_32x32x16; K / V rows stay in AGPRs as the B operands of S = Q.K^T
 // and dP = dO.V^T, whose accumulators (key on the lane) are the B operands of
@@ -130,14 +130,14 @@ struct Acc {
 };
 
 // l2 = lse * log2(e), dsc = D * scale (per query row, flash_bwd_pre_vec_kernel)
-template <bool DROP, bool DSJ>
+template <bool DROP>
 __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const float* __restrict__ lse,
                                                               const float* __restrict__ Dv,
                                                               const bf16* __restrict__ dout, int64_t ldo,
                                                               bf16* __restrict__ dqkv, int64_t ldd,
                                                               bf16* __restrict__ dqr, bf16* __restrict__ dsj,
                                                               int64_t ldr) {
-    constexpr int NST = DSJ ? 4 : 2;
+    constexpr int NST = 4;  // dS row stores per wave and iteration (2 r-indexed, 2 j-indexed)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sR = smem + O_R;
     const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, c32 = lane & 31;
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
     const __amdgpu_buffer_rsrc_t rl = make_rsrc(Lp, (uint32_t)(S * 4));
     const __amdgpu_buffer_rsrc_t rd = make_rsrc(Dp, (uint32_t)(S * 4));
     bf16* qr_rows = dqr + ((int64_t)h * a.B + b) * S * ldr;
-    bf16* sj_rows = DSJ ? dsj + ((int64_t)h * a.B + b) * S * ldr : nullptr;
+    bf16* sj_rows = dsj + ((int64_t)h * a.B + b) * S * ldr;
     const float c2 = a.scale * LOG2E;
     // dS = P (dP m ks - D) scale = P fma(dP m, ks scale, -D scale)
     const float ks_scale = (DROP ? a.keep_scale : 1.f) * a.scale;
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
     // dS row stores of the staged tile ip (NST / 2 per row half): thread t
     // stores 8 keys of query rows t/16 and 16 + t/16, r-indexed at
     // r = S-1-i+j (2-byte aligned rows, unaligned 16-B stores; entries j > i
-    // land at r >= S, in the row padding) and with DSJ j-indexed. Rows past the
+    // land at r >= S, in the row padding) and j-indexed. Rows past the
     // sequence end and the slot before tile 0 use the dropped offset, so every
     // wave issues exactly NST stores per iteration.
     const uint32_t ds_bytes = (uint32_t)min<int64_t>((int64_t)S * ldr * 2, OOB - 1);
@@ -276,10 +276,8 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
         const uint32_t rowb = (uint32_t)i * (uint32_t)ldr2;
         const __amdgpu_buffer_rsrc_t rqr = make_rsrc(qr_rows, ds_bytes);
         __builtin_amdgcn_raw_buffer_store_b128(v, rqr, in ? rowb + (uint32_t)(S - 1 - i + j) * 2u : OOB, 0, 0);
-        if (DSJ) {
-            const __amdgpu_buffer_rsrc_t rsj = make_rsrc(sj_rows, ds_bytes);
-            __builtin_amdgcn_raw_buffer_store_b128(v, rsj, in ? rowb + (uint32_t)j * 2u : OOB, 0, 0);
-        }
+        const __amdgpu_buffer_rsrc_t rsj = make_rsrc(sj_rows, ds_bytes);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rsj, in ? rowb + (uint32_t)j * 2u : OOB, 0, 0);
     };
 
     // skew: register e of lane c32 takes the window value from lane
@@ -541,33 +539,23 @@ int flash_bwd_kv5(const AttnArgs& a, const float* lse, const float* Dv, const bf
                   int64_t ldd, bf16* dqr, bf16* dsj, int64_t ldr, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)flash_bwd_kv5_kernel<false, false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)flash_bwd_kv5_kernel<true, false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)flash_bwd_kv5_kernel<false, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)flash_bwd_kv5_kernel<true, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)flash_bwd_kv5_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)flash_bwd_kv5_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS_BYTES);
         attr = true;
     }
     // rows up to S + 127 (the staging DMA of the tiles past the end) stay below 2^32 bytes
     if ((a.S + 128) * a.ldq * 2 >= (int64_t)OOB || (a.S + 128) * ldo * 2 >= (int64_t)OOB || a.n_meta > 8) return -1;
     if ((a.S + 128) * ldr * 2 >= (int64_t)OOB) return -1;
     if (a.colmask && mask_bh_bytes(a.mask_ld) >= (int64_t)OOB) return -1;
-    if (ldr < a.S + 128) return -1;
+    if (ldr < a.S + 128 || !dsj) return -1;
     const dim3 grid((unsigned)((a.S + KB - 1) / KB), (unsigned)a.H, (unsigned)a.B);
-    const bool drop = a.colmask != nullptr, sj = dsj != nullptr;
-#define KV5_LAUNCH(D, J)                                                                                          \
-    hipLaunchKernelGGL((flash_bwd_kv5_kernel<D, J>), grid, dim3(NT), LDS_BYTES, s, a, lse, Dv, dout, ldo, dqkv, ldd, \
-                       dqr, dsj, ldr)
-    if (drop) {
-        if (sj) KV5_LAUNCH(true, true);
-        else KV5_LAUNCH(true, false);
-    } else {
-        if (sj) KV5_LAUNCH(false, true);
-        else KV5_LAUNCH(false, false);
-    }
-#undef KV5_LAUNCH
+    if (a.colmask)
+        hipLaunchKernelGGL((flash_bwd_kv5_kernel<true>), grid, dim3(NT), LDS_BYTES, s, a, lse, Dv, dout, ldo, dqkv, ldd,
+                           dqr, dsj, ldr);
+    else
+        hipLaunchKernelGGL((flash_bwd_kv5_kernel<false>), grid, dim3(NT), LDS_BYTES, s, a, lse, Dv, dout, ldo, dqkv,
+                           ldd, dqr, dsj, ldr);
     return 0;
 }

@@ -2,13 +2,13 @@
 // differentiated w.r.t. q):
 //   dq_i = sum_j dS_ij k_j  +  sum_j dS_ij R[S-1-i+j]
 //        = sum_j dSj[i][j] K[j]  +  sum_r dQR[i][r] R[r]          (r = S-1-i+j)
-// The key/value pass (attn_bwd3.hip) writes dS twice: j-indexed (dSj, zero for
+// The key/value pass (attn_bwd5.hip) writes dS twice: j-indexed (dSj, zero for
 // j > i inside the tiles it visits) and r-indexed (dQR). Both products are plain
 // contractions over one K axis, so one kernel runs them back to back into the
 // same accumulators: a 128-query x 128-dim output tile per (b, h), K range
 // j in [0, i0+128) then r in [S-1-i_last rounded down to 64, S) (rows below
 // S-1-i are zero: the band the dQR writer zeroes). The metadata entries j > i
-// are added afterwards by flash_bwd_meta_kernel.
+// are added afterwards by flash_bwd_meta5_kernel.
 //
 // Tile: 256 threads = 4 waves (2x2), each 64x64 from v_mfma_f32_16x16x32_bf16;
 // operands staged global -> registers -> LDS (double buffered, one barrier per
@@ -57,19 +57,6 @@ __device__ __forceinline__ bf16x8 frag_mn(const char* s, int rb, int ks, int lan
     return u.v;
 }
 
-// bf16 elements [s, s + 8) of the 32-byte window lo:hi (s wave-uniform, 0..7):
-// four v_alignbyte over the dword pairs the window straddles
-__device__ __forceinline__ u32x4 funnel8(u32x4 lo, u32x4 hi, int s) {
-    const uint32_t bs = (uint32_t)(s & 1) * 2u;
-    auto ab = [&](uint32_t h, uint32_t l) { return __builtin_amdgcn_alignbyte(h, l, bs); };
-    switch (s >> 1) {
-        case 0: return (u32x4){ab(lo[1], lo[0]), ab(lo[2], lo[1]), ab(lo[3], lo[2]), ab(hi[0], lo[3])};
-        case 1: return (u32x4){ab(lo[2], lo[1]), ab(lo[3], lo[2]), ab(hi[0], lo[3]), ab(hi[1], hi[0])};
-        case 2: return (u32x4){ab(lo[3], lo[2]), ab(hi[0], lo[3]), ab(hi[1], hi[0]), ab(hi[2], hi[1])};
-        default: return (u32x4){ab(hi[0], lo[3]), ab(hi[1], hi[0]), ab(hi[2], hi[1]), ab(hi[3], hi[2])};
-    }
-}
-
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t dq_rsrc(const void* base, uint32_t bytes) {
     const uint64_t a = (uint64_t)base;
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
@@ -78,16 +65,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t dq_rsrc(const void* base, uint
     return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
-// 64 KB of LDS, two workgroups per CU. DS1 (dS stored once, r-indexed): the
-// dS.K term reads the j-view of dQR, row i's run starting at key j being the
-// dQR run starting at r = S-1-i+j. That start is 2-byte aligned, so each
-// 16-B chunk is cut from two ALIGNED chunk loads by a funnel shift; the shift
-// (S-1-i) mod 8 depends on the row only through i mod 8, so each A-operand
-// load instruction covers 8 rows of one residue class (rows 64 rb + r8 + 8 m,
-// one per 8 lanes) and its shift is wave-uniform. The entries past the
-// diagonal read the row's stored zeros (j > i inside a 128-key block) or its
-// padding (never written, zeroed once per workspace: ldr >= S + 200).
-template <bool DS1>
+// 64 KB of LDS, two workgroups per CU.
 __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const bf16* __restrict__ dsj,
                                                              const bf16* __restrict__ dqr, int64_t ldr,
                                                              bf16* __restrict__ dqkv, int64_t ldd) {
@@ -105,7 +83,7 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
     const int64_t rows = ((h * a.B + b) * S) * ldr;
     const uint32_t slab = (uint32_t)(S * ldr * 2);
     const __amdgpu_buffer_rsrc_t rR = dq_rsrc(dqr + rows, slab);
-    const __amdgpu_buffer_rsrc_t rJ = dq_rsrc((DS1 ? dqr : dsj) + rows, slab);
+    const __amdgpu_buffer_rsrc_t rJ = dq_rsrc(dsj + rows, slab);
     const bf16* B0 = (const bf16*)a.qkv + b * S * ldq + (H + h) * HSZ;
     const bf16* B1 = (const bf16*)a.R + h * a.S_max * HSZ;
     const int64_t ke0 = min<int64_t>(S, i0 + BM);        // j range [0, ke0)
@@ -113,12 +91,11 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
     const int n0 = (int)((ke0 + BK - 1) / BK), nt = n0 + (int)((S - kb1 + BK - 1) / BK);
     // A-operand load u of this wave: rows 64 rb + r8 + 8 m (m = lane / 8), chunk lane % 8
     const int m8 = lane >> 3, ch8 = lane & 7;
-    int arow[NU], ashift[NU];
+    int arow[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
         const int cls = wid * NU + u, r8 = cls & 7, rb = cls >> 3;
         arow[u] = 64 * rb + r8 + 8 * m8;
-        ashift[u] = __builtin_amdgcn_readfirstlane((int)((S - 1 - r8) & 7));  // i0, k0: multiples of 8
     }
 
     u32x4 ra[NU], rb[NU];
@@ -132,16 +109,8 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
         for (int u = 0; u < NU; ++u) {
             {  // A [128 rows][BK k]
                 const int64_t gi = i0 + arow[u];
-                if (DS1 && !s1) {  // j-view of dQR: r = S-1-gi+k0+8ch .. +7
-                    const int64_t r = S - 1 - gi + k0 + 8 * ch8;
-                    const uint32_t off = gi < S ? (uint32_t)((gi * ldr + (r & ~(int64_t)7)) * 2) : 0xFFFF0000u;
-                    const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(rJ, off, 0, 0);
-                    const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(rJ, off + 16u, 0, 0);
-                    ra[u] = funnel8(lo, hi, ashift[u]);
-                } else {
-                    const uint32_t off = gi < S ? (uint32_t)((gi * ldr + k0 + 8 * ch8) * 2) : 0xFFFF0000u;
-                    ra[u] = __builtin_amdgcn_raw_buffer_load_b128(s1 ? rR : rJ, off, 0, 0);
-                }
+                const uint32_t off = gi < S ? (uint32_t)((gi * ldr + k0 + 8 * ch8) * 2) : 0xFFFF0000u;
+                ra[u] = __builtin_amdgcn_raw_buffer_load_b128(s1 ? rR : rJ, off, 0, 0);
             }
             {  // B [BK k][128 d]
                 const int c = tid + NT * u;
@@ -213,6 +182,5 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
 void flash_bwd_dq(const AttnArgs& a, const bf16* dsj, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd,
                   hipStream_t s) {
     const dim3 grid((unsigned)((a.S + BM - 1) / BM), (unsigned)a.H, (unsigned)a.B);
-    if (dsj) hipLaunchKernelGGL(flash_bwd_dq_kernel<false>, grid, dim3(NT), 0, s, a, dsj, dqr, ldr, dqkv, ldd);
-    else hipLaunchKernelGGL(flash_bwd_dq_kernel<true>, grid, dim3(NT), 0, s, a, dsj, dqr, ldr, dqkv, ldd);
+    hipLaunchKernelGGL(flash_bwd_dq_kernel, grid, dim3(NT), 0, s, a, dsj, dqr, ldr, dqkv, ldd);
 }

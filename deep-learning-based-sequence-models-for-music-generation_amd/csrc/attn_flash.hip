@@ -50,37 +50,6 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_vec_kernel(AttnArgs a, cons
 }
 
 // ------------------------------------------------------------ backward: fix-up
-// metadata prefix, j > i (only i < n_meta - 1): dS_ij was written to meta_ds.
-//   dq_i     += dS_ij k_j            (AC term; pass B only sees j <= i)
-//   dq_{i+1} += dS_ij R[j-i-2]        (j >= i+2)
-//   dR[j-i-2] += dS_ij q_{i+1}        (j >= i+2)
-__global__ void flash_bwd_meta_kernel(AttnArgs a, const float* __restrict__ meta_ds, bf16* __restrict__ dqkv,
-                                      int64_t ldd, float* __restrict__ dR) {
-    const int64_t h = blockIdx.y, b = blockIdx.z;
-    const int d = threadIdx.x;  // 128 threads
-    const int64_t S = a.S, H = a.H, ldq = a.ldq;
-    const bf16* qkv = (const bf16*)a.qkv;
-    const float* md = meta_ds + (b * H + h) * 64;
-    const bf16* Rp = (const bf16*)a.R + h * a.S_max * HS;
-    const int64_t nm = min<int64_t>(a.n_meta, S);
-    for (int64_t i = 0; i + 1 < nm; ++i) {
-        float gq = 0.f;
-        for (int64_t j = i + 1; j < nm; ++j) gq += md[i * 8 + j] * (float)qkv[(b * S + j) * ldq + H * HS + h * HS + d];
-        bf16* p = dqkv + (b * S + i) * ldd + h * HS + d;
-        *p = (bf16)((float)*p + gq);
-    }
-    for (int64_t i = 0; i + 2 < nm; ++i) {
-        float gq = 0.f;
-        for (int64_t j = i + 2; j < nm; ++j) {
-            const float ds = md[i * 8 + j];
-            gq += ds * (float)Rp[(j - i - 2) * HS + d];
-            atomicAdd(dR + (h * a.S_max + (j - i - 2)) * HS + d, ds * (float)qkv[(b * S + i + 1) * ldq + h * HS + d]);
-        }
-        bf16* p = dqkv + (b * S + i + 1) * ldd + h * HS + d;
-        *p = (bf16)((float)*p + gq);
-    }
-}
-
 // metadata prefix, v5 form: the key/value pass v5 masks the entries j > i
 // inside the metadata prefix (i < j < n_meta, keys every query sees) like the
 // rest of the upper triangle, so this kernel owns them whole: per (b, h) and
@@ -195,7 +164,7 @@ __global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, bf16* __restrict__ 
 // the funnel shift's second chunk): padding, zeroed once per workspace
 int64_t flash_dqr_ld(int64_t S) { return (S + 200 + 7) / 8 * 8; }
 
-// workspace: dQR bf16 [H][B][S][ldr] | dSj bf16 [H][B][S][ldr] | D f32 [B][H][S] | meta_ds f32 [B][H][8][8]
+// workspace: dQR bf16 [H][B][S][ldr] | dSj bf16 [H][B][S][ldr] | D f32 [B][H][S]
 //            | l2 f32 [B][H][S] | dsc f32 [B][H][S]
 //            | dR split-K partials f32 [ksplit][H][S][HS]
 static size_t align256(size_t x) { return (x + 255) / 256 * 256; }
@@ -206,7 +175,7 @@ static size_t dr_ws_bytes(int64_t B, int64_t S, int64_t H) {
 size_t flash_bwd_workspace(int64_t B, int64_t S, int64_t H) {
     const int64_t ldr = flash_dqr_ld(S);
     return 2 * align256((size_t)H * B * S * ldr * 2) + 3 * align256((size_t)B * H * S * 4) +
-           align256((size_t)B * H * 64 * 4) + align256(dr_ws_bytes(B, S, H));
+           align256(dr_ws_bytes(B, S, H));
 }
 
 int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo, const bf16* out, bf16* dqkv,
@@ -219,8 +188,6 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     p += align256((size_t)H * B * S * ldr * 2);
     float* Dv = (float*)p;
     p += align256((size_t)B * H * S * 4);
-    float* meta_ds = (float*)p;
-    p += align256((size_t)B * H * 64 * 4);
     float* dr_ws = (float*)p;
     p += align256(dr_ws_bytes(B, S, H));
     float* l2 = (float*)p;
@@ -233,32 +200,16 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     if (!ws_ready)
         hipLaunchKernelGGL(dqr_band_zero_kernel, dim3((unsigned)((H * B * S + 3) / 4)), dim3(256), 0, s, dqr, dsj, ldr,
                            S, H * B * S);
-    hipMemsetAsync(meta_ds, 0, (size_t)B * H * 64 * 4, s);
     if (ldo % 8 || ((uintptr_t)dout % 16) || ((uintptr_t)out % 16))
         return msq_set_error(MSQ_ERR_ARG, "flash_bwd: dout / out need 16-B aligned rows");
     hipLaunchKernelGGL(flash_bwd_pre_vec_kernel, dim3((unsigned)((B * S * H + 15) / 16)), dim3(256), 0, s, a, dout, ldo,
                        out, lse, Dv, l2, dsc);
-    // key/value pass: dK, dV, and dS in both layouts (v4; MSQ_ATTN_BWD_KV=3
-    // selects the v3 pass, kept for A/B measurements)
-    // MSQ_ATTN_BWD_KV: 5 (default) the v5 pass storing dS once; 50 v5 also
-    // storing the j-indexed copy; 4 the older pass (both copies)
-    static const int kv_ver = [] {
-        const char* e = getenv("MSQ_ATTN_BWD_KV");
-        return e ? atoi(e) : 50;
-    }();
-    const bool ds1 = kv_ver == 5;
-    const int kv_rc = kv_ver == 4 ? flash_bwd_kv4(a, lse, Dv, dout, ldo, dqkv, ldd, dqr, dsj, ldr, meta_ds, s)
-                                    : flash_bwd_kv5(a, l2, dsc, dout, ldo, dqkv, ldd, dqr, ds1 ? nullptr : dsj, ldr, s);
-    if (kv_rc)
+    // key/value pass v5: dK, dV, and dS in both layouts (dQR r-indexed, dSj
+    // j-indexed; storing it once measured slower overall)
+    if (flash_bwd_kv5(a, l2, dsc, dout, ldo, dqkv, ldd, dqr, dsj, ldr, s))
         return msq_set_error(MSQ_ERR_UNSUPPORTED, "flash_bwd: shape outside the key/value pass (n_meta > 8 or > 4 GB)");
     // dq (bf16, q columns of dqkv) = dSj . K + dQR . R
-    static const int dq_ver = [] {
-        const char* e = getenv("MSQ_ATTN_DQ");
-        return e ? atoi(e) : 3;
-    }();
-    if (ds1 || dq_ver != 3) flash_bwd_dq(a, ds1 ? nullptr : dsj, dqr, ldr, dqkv, ldd, s);
-    else if (flash_bwd_dq3(a, dsj, dqr, ldr, dqkv, ldd, s))
-        return msq_set_error(MSQ_ERR_UNSUPPORTED, "flash_bwd: shape outside the query pass (> 4 GB)");
+    flash_bwd_dq(a, dsj, dqr, ldr, dqkv, ldd, s);
     // dR[h][r] += sum_{b,i} dQR[h][b,i][r] q_{b,i}   (batched over heads; per batch
     // segment only i >= S-1-r contributes: tri 2, split over segments)
     // (a strided-batched hipBLASLt product over the whole K range, 2x the
@@ -266,11 +217,7 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     int rc = gemm_bf16_tri(2, S, 1, 1, S, HS, B * S, dqr, ldr, B * S * ldr, a.qkv, a.ldq, HS, dR, MSQ_F32, HS,
                            a.S_max * HS, H, MSQ_EPI_ACCUM, nullptr, MSQ_F32, 0, 0, s, dr_ws, dr_ws_bytes(B, S, H));
     if (rc) return msq_set_error(MSQ_ERR_ARG, "flash_bwd: dR product");
-    if (kv_ver == 4)
-        hipLaunchKernelGGL(flash_bwd_meta_kernel, dim3(1, (unsigned)H, (unsigned)B), dim3(HS), 0, s, a, meta_ds, dqkv,
-                           ldd, dR);
-    else
-        hipLaunchKernelGGL(flash_bwd_meta5_kernel, dim3(1, (unsigned)H, (unsigned)B), dim3(HS), 0, s, a, lse, Dv, dout,
-                           ldo, dqkv, ldd, dR);
+    hipLaunchKernelGGL(flash_bwd_meta5_kernel, dim3(1, (unsigned)H, (unsigned)B), dim3(HS), 0, s, a, lse, Dv, dout,
+                       ldo, dqkv, ldd, dR);
     return 0;
 }

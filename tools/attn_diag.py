@@ -1,6 +1,5 @@
 """Diagnostic: relative-attention bf16 backward against the oracle, error per
-gradient and per row region, for the key/value pass version in
-MSQ_ATTN_BWD_KV (one process per version). Usage: python tools/attn_diag.py B S H"""
+gradient and per row region. Usage: python tools/attn_diag.py B S H"""
 import os
 import sys
 
@@ -23,7 +22,7 @@ out, lse = att.relattn_fwd(qkv.cuda(), R.cuda(), B, S, H, hs, scale)
 dqkv, dR = att.relattn_bwd(dout.cuda(), out, lse, qkv.cuda(), R.cuda(), B, S, H, hs, scale)
 torch.cuda.synchronize()
 nq = H * hs
-tag = os.environ.get("MSQ_ATTN_BWD_KV", "5")
+tag = "kv5"
 
 
 def rel(a, b):
