@@ -10,7 +10,8 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime before libmidiseq)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmidiseq.so")
+# MSQ_LIB_PATH: an alternate build of the same library (same-box A/B tools only)
+LIB_PATH = os.environ.get("MSQ_LIB_PATH") or os.path.join(HERE, "libmidiseq.so")
 
 F32, BF16 = 0, 1
 ROUTE_DEFAULT, ROUTE_TILE256, ROUTE_TILE128 = range(3)  # msq_gemm_set_route

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Builds an A/B twin of libmidiseq.so: the in-tree objects with one source
+# replaced by the version at a git revision. Load it with MSQ_LIB_PATH=<out>.
+# usage: tools/build_ab.sh <rev> <csrc/file.hip> <out.so>
+set -e
+rev=$1; src=$2; out=$3
+P=deep-learning-based-sequence-models-for-music-generation_amd
+tmp=$(mktemp -d /tmp/abXXXX)
+git show "$rev:$P/$src" > "$P/csrc/_ab_$(basename $src)"
+/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -I include -Wno-unused-result -c "$P/csrc/_ab_$(basename $src)" -o "$tmp/ab.o"
+rm -f "$P/csrc/_ab_$(basename $src)"
+objs=$(ls $P/build/*.o | grep -v "/$(basename $src).o$")
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$out" $objs "$tmp/ab.o"
+rm -rf "$tmp"
+echo "built $out ($src at $rev)"

@@ -18,7 +18,7 @@ from collections import defaultdict
 
 # (regex on the kernel name, class, class launches per train step)
 CLASSES = [
-    (r"flash_bwd_kv[34]|flash_bwd_dq|flash_bwd_pre|dqr_band_zero|flash_bwd_meta|gemm_bf16_kernel<1, 1, 5", "attn_bwd", 8),
+    (r"flash_bwd_kv[345]|flash_bwd_dq|flash_bwd_pre|dqr_band_zero|flash_bwd_meta|gemm_bf16_kernel<1, 1, 5", "attn_bwd", 8),
     (r"flash_fwd3", "attn_fwd", 8),
     (r"attn_mask_kernel", "dropout_mask", 8),
     (r"colstats2|rowlse|cspart|cs_reduce|finish2|dbias_reduce|pad_table|wrange|mean_kernel", "loss", 1),
