@@ -58,12 +58,14 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_vec_kernel(AttnArgs a, cons
 //   dS   = p (dO_i.v_j m_ij ks - D_i) scale
 //   dV_j += p m_ij ks dO_i,  dK_j += dS q_i,  dq_i += dS k_j
 //   j >= i+2: dq_{i+1} += dS R[j-i-2],  dR[j-i-2] += dS q_{i+1}
-// (model_transformer.py:70-90 with the _rel_shift wrap of :84-90 for j > i)
+// (model_transformer.py:70-90 with the _rel_shift wrap of :84-90 for j > i).
+// The dR rows go to mdr[b][h][r] (plain stores); flash_bwd_meta_dr_kernel adds
+// them over b in a fixed order, so the backward has no atomics here.
 __global__ __launch_bounds__(HS) void flash_bwd_meta5_kernel(AttnArgs a, const float* __restrict__ lse,
                                                              const float* __restrict__ Dv,
                                                              const bf16* __restrict__ dout, int64_t ldo,
                                                              bf16* __restrict__ dqkv, int64_t ldd,
-                                                             float* __restrict__ dR) {
+                                                             float* __restrict__ mdr) {
     __shared__ float red[3][2];
     const int64_t h = blockIdx.y, b = blockIdx.z;
     const int d = threadIdx.x, lane = d & 63, wv = d >> 6;  // 128 threads, one per dim
@@ -72,9 +74,9 @@ __global__ __launch_bounds__(HS) void flash_bwd_meta5_kernel(AttnArgs a, const f
     const bf16* Rp = (const bf16*)a.R + h * a.S_max * HS;
     const bf16* dob = dout + b * S * ldo;
     const int nm = (int)min<int64_t>(a.n_meta, S);
-    float gq[8], gk[8], gv[8];
+    float gq[8], gk[8], gv[8], gr[8];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) gq[r] = gk[r] = gv[r] = 0.f;
+    for (int r = 0; r < 8; ++r) gq[r] = gk[r] = gv[r] = gr[r] = 0.f;
     auto q = [&](int i) { return (float)qkv[i * ldq + h * HS + d]; };
     auto k = [&](int j) { return (float)qkv[j * ldq + (H + h) * HS + d]; };
     auto v = [&](int j) { return (float)qkv[j * ldq + (2 * H + h) * HS + d]; };
@@ -111,8 +113,8 @@ __global__ __launch_bounds__(HS) void flash_bwd_meta5_kernel(AttnArgs a, const f
                 }
                 if (r == i) gq[r] += ds * k(j);
                 if (far && r == i + 1) gq[r] += ds * rr;
+                if (far && r == j - i - 2) gr[r] += ds * q1;
             }
-            if (far) atomicAdd(dR + (h * a.S_max + (j - i - 2)) * HS + d, ds * q1);
         }
     }
 #pragma unroll
@@ -123,6 +125,19 @@ __global__ __launch_bounds__(HS) void flash_bwd_meta5_kernel(AttnArgs a, const f
         row[(H + h) * HS + d] = (bf16)((float)row[(H + h) * HS + d] + gk[r]);
         row[(2 * H + h) * HS + d] = (bf16)((float)row[(2 * H + h) * HS + d] + gv[r]);
     }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) mdr[(bh * 8 + r) * HS + d] = gr[r];
+}
+
+// dR[h][r] += sum over b (in order) of mdr[b][h][r], r < 8
+__global__ __launch_bounds__(HS) void flash_bwd_meta_dr_kernel(AttnArgs a, const float* __restrict__ mdr,
+                                                              float* __restrict__ dR) {
+    const int64_t h = blockIdx.x, r = blockIdx.y;
+    const int d = threadIdx.x;
+    if (r + 2 >= min<int64_t>(a.n_meta, a.S)) return;  // only j - i - 2 < n_meta - 2 occurs
+    float s = 0.f;
+    for (int64_t b = 0; b < a.B; ++b) s += mdr[((b * a.H + h) * 8 + r) * HS + d];
+    dR[(h * a.S_max + r) * HS + d] += s;
 }
 
 }  // namespace
@@ -165,8 +180,8 @@ __global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, bf16* __restrict__ 
 int64_t flash_dqr_ld(int64_t S) { return (S + 200 + 7) / 8 * 8; }
 
 // workspace: dQR bf16 [H][B][S][ldr] | dSj bf16 [H][B][S][ldr] | D f32 [B][H][S]
-//            | l2 f32 [B][H][S] | dsc f32 [B][H][S]
 //            | dR split-K partials f32 [ksplit][H][S][HS]
+//            | l2 f32 [B][H][S] | dsc f32 [B][H][S] | mdr f32 [B][H][8][HS]
 static size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 static size_t dr_ws_bytes(int64_t B, int64_t S, int64_t H) {
     return splitk_ws_bytes(S, HS, H, gemm_bf16_tri_ksplit(2, S, HS, B * S, S, H));
@@ -175,6 +190,7 @@ static size_t dr_ws_bytes(int64_t B, int64_t S, int64_t H) {
 size_t flash_bwd_workspace(int64_t B, int64_t S, int64_t H) {
     const int64_t ldr = flash_dqr_ld(S);
     return 2 * align256((size_t)H * B * S * ldr * 2) + 3 * align256((size_t)B * H * S * 4) +
+           align256((size_t)B * H * 8 * HS * 4) +
            align256(dr_ws_bytes(B, S, H));
 }
 
@@ -193,6 +209,8 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     float* l2 = (float*)p;
     p += align256((size_t)B * H * S * 4);
     float* dsc = (float*)p;
+    p += align256((size_t)B * H * S * 4);
+    float* mdr = (float*)p;  // the metadata block's dR rows per (b, h)
 
     // the band and row pads are never written non-zero by the passes below
     // (their dS entries there are 0 by the mask), so a workspace that already
@@ -218,6 +236,7 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
                            a.S_max * HS, H, MSQ_EPI_ACCUM, nullptr, MSQ_F32, 0, 0, s, dr_ws, dr_ws_bytes(B, S, H));
     if (rc) return msq_set_error(MSQ_ERR_ARG, "flash_bwd: dR product");
     hipLaunchKernelGGL(flash_bwd_meta5_kernel, dim3(1, (unsigned)H, (unsigned)B), dim3(HS), 0, s, a, lse, Dv, dout,
-                       ldo, dqkv, ldd, dR);
+                       ldo, dqkv, ldd, mdr);
+    hipLaunchKernelGGL(flash_bwd_meta_dr_kernel, dim3((unsigned)H, 8), dim3(HS), 0, s, a, mdr, dR);
     return 0;
 }

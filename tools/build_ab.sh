@@ -1,12 +1,12 @@
 #!/bin/bash
 # Builds an A/B twin of libmidiseq.so: the in-tree objects with one source
 # replaced by the version at a git revision. Load it with MSQ_LIB_PATH=<out>.
-# usage: tools/build_ab.sh <rev> <csrc/file.hip> <out.so>
+# usage: tools/build_ab.sh <rev | FILE:path> <csrc/file.hip> <out.so>
 set -e
 rev=$1; src=$2; out=$3
 P=deep-learning-based-sequence-models-for-music-generation_amd
 tmp=$(mktemp -d /tmp/abXXXX)
-git show "$rev:$P/$src" > "$P/csrc/_ab_$(basename $src)"
+if [ "${rev#FILE:}" != "$rev" ]; then cp "${rev#FILE:}" "$P/csrc/_ab_$(basename $src)"; else git show "$rev:$P/$src" > "$P/csrc/_ab_$(basename $src)"; fi
 /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -I include -Wno-unused-result -c "$P/csrc/_ab_$(basename $src)" -o "$tmp/ab.o"
 rm -f "$P/csrc/_ab_$(basename $src)"
 objs=$(ls $P/build/*.o | grep -v "/$(basename $src).o$")
