@@ -429,7 +429,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
     for (int64_t row = blockIdx.x * 4LL + wid; row < rows; row += (int64_t)gridDim.x * 4) {
         const float mu = mean[row], rs = rstd[row];
         const int64_t xrow = map_row(row, seg, skip);
-        f32x4 xh[MAXC], g[MAXC];
+        f32x4 xh[MAXC], g[MAXC], acc[MAXC];
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int c = 0; c < MAXC; ++c) {
@@ -437,6 +437,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
             if (col < d) {
                 const f32x4 xv = *(const f32x4*)(x + xrow * d + col);
                 const f32x4 dv = load4(dy + row * d + col);
+                // the accumulated gradient row is loaded with the inputs, so its
+                // latency overlaps theirs instead of following the reductions
+                acc[c] = *(const f32x4*)(dxa + xrow * d + col);
                 const f32x4 gm = *(const f32x4*)(gamma + col);
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
@@ -448,7 +451,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
                     pb[c][t] += dv[t];
                 }
             } else {
-                xh[c] = g[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                xh[c] = g[c] = acc[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
             }
         }
         const float m1 = wave_sum(s1) / d, m2 = wave_sum(s2) / d;
@@ -457,7 +460,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
             const int col = (c * 64 + lane) * 4;
             if (col < d) {
                 float* dp = dxa + xrow * d + col;
-                f32x4 o = *(f32x4*)dp;
+                f32x4 o = acc[c];
 #pragma unroll
                 for (int t = 0; t < 4; ++t) o[t] += rs * (g[c][t] - m1 - xh[c][t] * m2);
                 *(f32x4*)dp = o;
