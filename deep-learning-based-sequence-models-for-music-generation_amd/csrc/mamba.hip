@@ -896,19 +896,21 @@ struct Chunk {
     int64_t b, h, c, t0;
     int nval;
 };
-__device__ __forceinline__ Chunk chunk_of(const MambaArgs& a, int nch) {
+// hg > 1: one workgroup per group of hg heads (k.h = the group's first head)
+__device__ __forceinline__ Chunk chunk_of(const MambaArgs& a, int nch, int hg = 1) {
     Chunk k;
+    const int64_t ng = a.nheads / hg;
     if (a.xcd) {  // logical id (h fastest, then chunk, then b), contiguous per XCD
         const int64_t id = __builtin_amdgcn_readfirstlane(xcd_remap((int)blockIdx.x, (int)gridDim.x));
-        k.h = id % a.nheads;
-        const int64_t r = id / a.nheads;
+        k.h = id % ng * hg;
+        const int64_t r = id / ng;
         k.c = r % nch;
         k.b = r / nch;
     } else {
         const int64_t bh = blockIdx.x / nch;
         k.c = blockIdx.x % nch;
-        k.b = bh / a.nheads;
-        k.h = bh % a.nheads;
+        k.b = bh / ng;
+        k.h = bh % ng * hg;
     }
     k.t0 = k.c * Q;
     k.nval = (int)min<int64_t>(Q, a.L - k.t0);
@@ -1380,7 +1382,7 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
                                                       float* __restrict__ dxc, float* __restrict__ dbc,
                                                       TD* __restrict__ dzx,
                                                       float* __restrict__ gA_log, float* __restrict__ gD,
-                                                      float* __restrict__ gdt_bias, int nch) {
+                                                      float* __restrict__ gdt_bias, int nch, int hg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sCB = smem;            // C [t][n]   | B [s][n]
     char* sXY = smem + IMG;      // dt x [s][p] | dY [t][p]
@@ -1392,7 +1394,25 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
     float* sddt = sdcum + 64;
     float* sred = sddt + 64;  // 8 block-reduction slots
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, il = lane & 15, g = lane >> 4;
-    const Chunk k = chunk_of(a, nch);
+    const Chunk kg = chunk_of(a, nch, hg);
+    const int nv = kg.nval;
+    const int rb = 32 * (w >> 1), cb = 32 * (w & 1);
+    // the chunk's B / C rows, shared by the group's heads
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
+        *(u32x4*)(sCB + offd(row, 8 + ch)) = ld_chunk(a, kg, xc, a.d_inner, e);
+        *(u32x4*)(sCB + offd(row, ch)) = ld_chunk(a, kg, xc, a.d_inner + N, e);
+    }
+    // dC [t][n] / dB [s][n] of the chunk summed over the group's heads (fp32, in
+    // registers); dbc_reduce_kernel adds the nheads / hg group rows
+    f32x4 dcs[2][2], dbs[2][2];
+    zero22(dcs);
+    zero22(dbs);
+    for (int hh = 0; hh < hg; ++hh) {
+    if (hh) __syncthreads();  // the previous head's last LDS reads are done
+    Chunk k = kg;
+    k.h = kg.h + hh;
     const float A = -expf(A_log[k.h]), Dh = Dp[k.h];
     const int64_t slot = ((k.b * a.nheads + k.h) * nch + k.c) * (int64_t)(P * N);
     const float* Hs = states + slot;
@@ -1403,8 +1423,6 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
     for (int u = 0; u < 2; ++u) {
         const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
         xr[u] = ld_chunk(a, k, xc, k.h * P, e);
-        *(u32x4*)(sCB + offd(row, 8 + ch)) = ld_chunk(a, k, xc, a.d_inner, e);
-        *(u32x4*)(sCB + offd(row, ch)) = ld_chunk(a, k, xc, a.d_inner + N, e);
         float hv[8], dv[8], yv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         {
             const f32x4 h0 = *(const f32x4*)(Hs + row * N + ch * 8), h1 = *(const f32x4*)(Hs + row * N + ch * 8 + 4);
@@ -1429,7 +1447,6 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
     hdh = wave_sum(hdh);
     if (lane == 0) sred[w] = hdh;
     __syncthreads();
-    const int nv = k.nval;
     const float cl = scum[nv - 1];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -1440,7 +1457,6 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
         for (int q = 0; q < 8; ++q) v[q] *= sdt[row];
         *(u32x4*)(sXY + offd(row, e & 7)) = pack8(v);
     }
-    const int rb = 32 * (w >> 1), cb = 32 * (w & 1);
     // M = (C B^T) o L ; dM = dY XS^T (s <= t)
     f32x4 mt[2][2], dm[2][2];
     zero22(mt);
@@ -1532,10 +1548,9 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
     }
     // dC = dG B + e^{cum_t} dY H ; dcum_t += e^{cum_t} sum_n C dyh
     {
-        f32x4 dc[2][2], dyh[2][2];
-        zero22(dc);
+        f32x4 dyh[2][2];
         zero22(dyh);
-        mm<false, true>(dc, sMG, 1, sCB, 1, rb, cb, lane);   // [t][n] = sum_s dG[t][s] B[s][n]
+        mm<false, true>(dcs, sMG, 1, sCB, 1, rb, cb, lane);  // [t][n] += sum_s dG[t][s] B[s][n]
         mm<false, true>(dyh, sXY, 1, sHD, 0, rb, cb, lane);  // [t][n] = sum_p dY[t][p] H[p][n]
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -1550,10 +1565,8 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     rs += et * (float)cv.e[r] * dyh[i][j][r];
-                    dc[i][j][r] += et * dyh[i][j][r];
+                    dcs[i][j][r] += et * dyh[i][j][r];
                 }
-                if (t < nv)  // this head's dC row (summed over heads by dbc_reduce_kernel)
-                    *(f32x4*)(dbc + ((k.b * a.L + k.t0 + t) * a.nheads + k.h) * (2 * N) + N + n0) = dc[i][j];
             }
             rs += __shfl_xor(rs, 16, 64);
             rs += __shfl_xor(rs, 32, 64);
@@ -1562,19 +1575,16 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
     }
     // dB = dG^T C + w_s (XS dH)
     {
-        f32x4 db[2][2], tb[2][2];
-        zero22(db);
+        f32x4 tb[2][2];
         zero22(tb);
-        mm<true, true>(db, sMG, 1, sCB, 0, rb, cb, lane);    // [s][n] = sum_t dG[t][s] C[t][n]
+        mm<true, true>(dbs, sMG, 1, sCB, 0, rb, cb, lane);   // [s][n] += sum_t dG[t][s] C[t][n]
         mm<false, true>(tb, sXY, 0, sHD, 1, rb, cb, lane);   // [s][n] = sum_p XS[s][p] dH[p][n]
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int s = rb + 16 * i + il;
-            if (s >= nv) continue;
-            const float ws = expf(cl - scum[s]);
-            float* rowp = dbc + ((k.b * a.L + k.t0 + s) * a.nheads + k.h) * (2 * N);
+            const float ws = expf(cl - scum[s]);  // rows s >= nv are never stored
 #pragma unroll
-            for (int j = 0; j < 2; ++j) *(f32x4*)(rowp + cb + 16 * j + 4 * g) = db[i][j] + ws * tb[i][j];
+            for (int j = 0; j < 2; ++j) dbs[i][j] += ws * tb[i][j];
         }
     }
     // dcum_last += sum_s dws_s + e^{cum_last} sum dH o H
@@ -1613,9 +1623,23 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
             atomicAdd(gD + k.h, sred[4] + sred[5] + sred[6] + sred[7]);
         }
     }
+    }  // heads of the group
+    const int64_t ng = a.nheads / hg, grp = kg.h / hg;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int t = rb + 16 * i + il;
+        if (t >= nv) continue;
+        float* rowp = dbc + ((kg.b * a.L + kg.t0 + t) * ng + grp) * (2 * N);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n0 = cb + 16 * j + 4 * g;
+            *(f32x4*)(rowp + n0) = dbs[i][j];
+            *(f32x4*)(rowp + N + n0) = dcs[i][j];
+        }
+    }
 }
 
-// dxc[bt][d_inner + c] = sum_h dbc[bt][h][c]   (dB | dC, c < 2N)
+// dxc[bt][d_inner + c] = sum_g dbc[bt][g][c]   (dB | dC, c < 2N; g < nheads / hg head groups)
 __global__ __launch_bounds__(256) void dbc_reduce_kernel(const float* __restrict__ dbc, float* __restrict__ dxc,
                                                          int64_t rows, int64_t nheads, int64_t ldxc, int64_t d_inner) {
     const int64_t e = blockIdx.x * 256LL + threadIdx.x;  // (row, 4-column group)
@@ -1767,6 +1791,9 @@ extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, cons
         float* U = (float*)workspace;
         float* dbc = U + B * nheads * nch * (int64_t)(P * N);
         const dim3 gch((unsigned)(B * nheads * nch));
+        // grad: one workgroup per (b, chunk, group of hg heads); the group's B / C
+        // tile is staged once and its dB / dC rows summed in registers
+        const int hg = nheads % 4 == 0 ? 4 : nheads % 2 == 0 ? 2 : 1;
         allow_lds(ssd2::grad_kernel<bf16>, ssd2::GRAD_LDS);
         if (getenv("MSQ_MAMBA_SSD_3K")) {
             allow_lds(ssd2::uterm_kernel, ssd2::UTERM_LDS);
@@ -1780,11 +1807,11 @@ extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, cons
                                (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, dY, ldy, U, nch,
                                dbc + B * L * nheads * 2 * N);
         }
-        hipLaunchKernelGGL(ssd2::grad_kernel<bf16>, gch, dim3(256), ssd2::GRAD_LDS, s, a, (const bf16*)xc,
-                           (const bf16*)zxbcdt, dt_bias, A_log, D, dY, ldy, states, U, dxc, dbc, (bf16*)dzxbcdt,
-                           gA_log, gD, gdt_bias, nch);
+        hipLaunchKernelGGL(ssd2::grad_kernel<bf16>, dim3((unsigned)(B * (nheads / hg) * nch)), dim3(256),
+                           ssd2::GRAD_LDS, s, a, (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, D, dY, ldy,
+                           states, U, dxc, dbc, (bf16*)dzxbcdt, gA_log, gD, gdt_bias, nch, hg);
         hipLaunchKernelGGL(ssd2::dbc_reduce_kernel, dim3((unsigned)((B * L * (2 * N / 4) + 255) / 256)), dim3(256), 0,
-                           s, dbc, dxc, B * L, nheads, ldxc, d_inner);
+                           s, dbc, dxc, B * L, nheads / hg, ldxc, d_inner);
         MSQ_LAUNCH_CHECK();
         return MSQ_OK;
     }
