@@ -98,6 +98,8 @@ SIGNATURES = {
     "msq_mamba_ssd_fwd_state": (_i, [_p, _i64, _p, _p, _p, _i64, _p, _i64, _i, _p, _p, _p, _i64, _i64, _i64, _i64,
                                      _p]),
     "msq_mamba_conv_step": (_i, [_p, _i64, _p, _p, _i64, _i, _p, _p, _i64, _i64, _i64, _p]),
+    "msq_mamba_in_proj_conv_step": (_i, [_p, _i64, _p, _i64, _p, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64,
+                                         _i64, _p]),
     "msq_mamba_ssd_step": (_i, [_p, _i64, _p, _p, _i64, _p, _i64, _i, _p, _p, _p, _i64, _i64, _i64, _p]),
     "msq_filtered_logit_step": (_i, [_p, _i64, _p, _p, _i, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p]),
     "msq_mamba_conv_bwd":(_i, [_p, _p, _i64, _p, _i64, _i, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),

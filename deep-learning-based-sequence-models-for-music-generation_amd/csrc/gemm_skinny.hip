@@ -23,6 +23,45 @@ namespace {
 
 constexpr int SK_WAVES = 16, SK_U = 4;
 
+// Mamba2 decode: the depthwise causal conv of the new row fused into the
+// in_proj epilogue (msq_mamba_in_proj_conv_step). Output columns c0 + c,
+// c < cd, are the pre-conv xBC channels; the lane holding C[m][n..n+3] runs
+// conv_step_kernel's arithmetic (csrc/mamba_step.hip) on those 4 channels of
+// row m: xc = silu(b + w0 s0 + w1 s1 + w2 s2 + w3 in), (s0, s1, s2) <- (s1, s2, in),
+// in = the stored bf16 value. Each (m, channel) has one owner: no race.
+struct SkinnyConv {
+    bf16* xc;
+    int64_t ldxc;
+    float* st;  // [M][3][cd]
+    const float* w;  // [cd][4]
+    const float* b;  // [cd]
+    int64_t c0, cd;
+};
+__device__ __forceinline__ float conv_silu(float x) { return x / (1.f + expf(-x)); }
+__device__ __forceinline__ void conv_apply(const SkinnyConv& cv, int64_t m, int64_t n, f32x4 v) {
+    const int64_t c = n - cv.c0;
+    if (c < 0 || c >= cv.cd) return;  // c0, cd % 4 == 0: the 4 columns are wholly in or out
+    float* s = cv.st + m * 3 * cv.cd + c;
+    const f32x4 s0 = *(const f32x4*)s, s1 = *(const f32x4*)(s + cv.cd), s2 = *(const f32x4*)(s + 2 * cv.cd);
+    const f32x4 bv = *(const f32x4*)(cv.b + c);
+    f32x4 xo, in;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const f32x4 wc = *(const f32x4*)(cv.w + (c + t) * 4);
+        in[t] = (float)(bf16)v[t];
+        float acc = bv[t];
+        acc += wc[0] * s0[t];
+        acc += wc[1] * s1[t];
+        acc += wc[2] * s2[t];
+        acc += wc[3] * in[t];
+        xo[t] = conv_silu(acc);
+    }
+    store4(cv.xc + m * cv.ldxc + c, xo);
+    *(f32x4*)s = s1;
+    *(f32x4*)(s + cv.cd) = s2;
+    *(f32x4*)(s + 2 * cv.cd) = in;
+}
+
 template <int EPI, typename TC, typename TX, int MT, bool PART>
 __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(GemmArgs g) {
     __shared__ f32x4 red[SK_WAVES - 1][MT][64];
@@ -103,8 +142,9 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(GemmArgs g, int ks) 
 // W slices blockIdx.x, + gridDim.x, ... with the next slice's W fragments
 // loaded before the current slice's MFMAs, reduction and epilogue, so each
 // CU keeps streaming W without launch rounds.
-template <int EPI, typename TC, typename TX, int MT, int KS>
-__global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_pk_kernel(GemmArgs g, int64_t ntiles) {
+template <int EPI, typename TC, typename TX, int MT, int KS, bool CONV = false>
+__global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_pk_kernel(GemmArgs g, int64_t ntiles,
+                                                                     SkinnyConv cv = {}) {
     __shared__ f32x4 red[SK_WAVES][MT][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const bf16* W = (const bf16*)g.B;
@@ -155,7 +195,10 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_pk_kernel(GemmArgs 
 #pragma unroll
             for (int q = 1; q < SK_WAVES; ++q) v += red[q][w][lane];
             const int64_t m = w * 16 + (lane & 15), n = tile * 16 + 4 * (lane >> 4);
-            if (m < g.M && n < g.N) epi_apply<EPI, TC, TX>(g, C, X, m, n, v);
+            if (m < g.M && n < g.N) {
+                epi_apply<EPI, TC, TX>(g, C, X, m, n, v);
+                if constexpr (CONV) conv_apply(cv, m, n, v);
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -163,14 +206,16 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_pk_kernel(GemmArgs 
     }
 }
 
-template <int EPI, typename TC, typename TX, int MT>
-void launch_pk(const GemmArgs& g, hipStream_t s) {
+template <int EPI, typename TC, typename TX, int MT, bool CONV = false>
+void launch_pk(const GemmArgs& g, hipStream_t s, const SkinnyConv& cv = {}) {
     const int64_t ntiles = (g.N + 15) / 16;
     const dim3 grid((unsigned)std::min<int64_t>(ntiles, 256));
     const int64_t ks = (g.K + SK_WAVES * 32 - 1) / (SK_WAVES * 32);
     // (KS = 4 would not fit the activation fragments in 128 VGPRs at MT = 4)
-    if (ks <= 1) hipLaunchKernelGGL((gemm_skinny_pk_kernel<EPI, TC, TX, MT, 1>), grid, dim3(64 * SK_WAVES), 0, s, g, ntiles);
-    else hipLaunchKernelGGL((gemm_skinny_pk_kernel<EPI, TC, TX, MT, 2>), grid, dim3(64 * SK_WAVES), 0, s, g, ntiles);
+    if (ks <= 1)
+        hipLaunchKernelGGL((gemm_skinny_pk_kernel<EPI, TC, TX, MT, 1, CONV>), grid, dim3(64 * SK_WAVES), 0, s, g, ntiles, cv);
+    else
+        hipLaunchKernelGGL((gemm_skinny_pk_kernel<EPI, TC, TX, MT, 2, CONV>), grid, dim3(64 * SK_WAVES), 0, s, g, ntiles, cv);
 }
 
 template <int EPI, typename TC, typename TX, bool PART>
@@ -248,4 +293,46 @@ bool gemm_skinny_launch(const GemmArgs& g, int ta, int tb, int epi, int c_dtype,
         return false;
     return c_dtype == MSQ_BF16 ? launch_epi<bf16>(g, epi, aux_dtype, ws_bytes, s)
                                 : launch_epi<float>(g, epi, aux_dtype, ws_bytes, s);
+}
+
+// Mamba2 decode step, first half of a mixer: zx = x . in_w^T (bf16 [B][d_in_proj],
+// msq_gemm's skinny product) and, in the same launch, the conv step of the new
+// row (msq_mamba_conv_step: xc, conv_state). Outside the fused kernel's range
+// (B > 64 rows, d_model > 1024) the two launches run instead.
+extern "C" int msq_mamba_in_proj_conv_step(void* zx, int64_t ldz, void* xc, int64_t ldxc, float* conv_state,
+                                           const void* x, int64_t ldx, const void* in_w, int64_t ldw,
+                                           const float* conv_w, const float* conv_b, int64_t B, int64_t d_model,
+                                           int64_t d_in_proj, int64_t d_inner, int64_t nheads, void* stream) {
+    const int64_t cd = d_inner + 2 * 64;
+    MSQ_CHECK_ARG(zx && xc && conv_state && x && in_w && conv_w && conv_b && B > 0 && d_model > 0 && nheads > 0 &&
+                      d_inner == nheads * 64 && d_in_proj == d_inner + cd + nheads && ldz >= d_in_proj &&
+                      ldxc >= cd && ldx >= d_model && ldw >= d_model,
+                  "msq_mamba_in_proj_conv_step: bad args");
+    hipStream_t s = (hipStream_t)stream;
+    const bool fused = B <= 64 && d_model <= SK_WAVES * 2 * 32 && d_model % 8 == 0 && ldx % 8 == 0 && ldw % 8 == 0 &&
+                       ldz % 4 == 0 && ldxc % 4 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)in_w % 16 == 0 &&
+                       (uintptr_t)zx % 16 == 0 && (uintptr_t)xc % 8 == 0 && (uintptr_t)conv_state % 16 == 0 &&
+                       (uintptr_t)conv_w % 16 == 0 && (uintptr_t)conv_b % 16 == 0;
+    if (!fused) {
+        const int rc = msq_gemm_ex(MSQ_BF16, 0, 0, B, d_in_proj, d_model, x, ldx, 0, in_w, ldw, 0, zx, MSQ_BF16, ldz, 0,
+                                   1, MSQ_EPI_NONE, nullptr, nullptr, MSQ_F32, 0, 0, 0u, 0u, 0.f, nullptr, 0, stream);
+        if (rc != MSQ_OK) return rc;
+        return msq_mamba_conv_step(xc, ldxc, conv_state, zx, ldz, MSQ_BF16, conv_w, conv_b, B, d_inner, nheads,
+                                   stream);
+    }
+    GemmArgs g{};
+    g.M = B; g.N = d_in_proj; g.K = d_model;
+    g.A = x; g.lda = ldx;
+    g.B = in_w; g.ldb = ldw;
+    g.C = zx; g.ldc = ldz;
+    g.batch = 1;
+    g.vec = 1;
+    const SkinnyConv cv{(bf16*)xc, ldxc, conv_state, conv_w, conv_b, d_inner, cd};
+    const int mt = (int)((B + 15) / 16);
+    if (mt == 1) launch_pk<MSQ_EPI_NONE, bf16, float, 1, true>(g, s, cv);
+    else if (mt == 2) launch_pk<MSQ_EPI_NONE, bf16, float, 2, true>(g, s, cv);
+    else if (mt == 3) launch_pk<MSQ_EPI_NONE, bf16, float, 3, true>(g, s, cv);
+    else launch_pk<MSQ_EPI_NONE, bf16, float, 4, true>(g, s, cv);
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
 }

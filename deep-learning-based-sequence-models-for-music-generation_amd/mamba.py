@@ -329,9 +329,14 @@ class MambaEngine:
         call("msq_embed_fwd", ptr(cache.x), ptr(P["tok_emb"]), ptr(P["meta_emb"]), ptr(tok), None, B, 1, 0, d, s)
         ops.cast(cache.xa, cache.x)
         for l in range(cfg.n_layers):
-            ops.gemm(cache.xa, W[f"{l}.in_w"], out=cache.zx)
-            call("msq_mamba_conv_step", ptr(cache.xc), cfg.conv_dim, ptr(cache.conv[l]), ptr(cache.zx), cfg.d_in_proj,
-                 dtc, ptr(P[f"{l}.conv_w"]), ptr(P[f"{l}.conv_b"]), B, di, H, s)
+            if dtc == L.BF16:  # in_proj with the conv step in its epilogue (one launch)
+                call("msq_mamba_in_proj_conv_step", ptr(cache.zx), cfg.d_in_proj, ptr(cache.xc), cfg.conv_dim,
+                     ptr(cache.conv[l]), ptr(cache.xa), d, ptr(W[f"{l}.in_w"]), d, ptr(P[f"{l}.conv_w"]),
+                     ptr(P[f"{l}.conv_b"]), B, d, cfg.d_in_proj, di, H, s)
+            else:
+                ops.gemm(cache.xa, W[f"{l}.in_w"], out=cache.zx)
+                call("msq_mamba_conv_step", ptr(cache.xc), cfg.conv_dim, ptr(cache.conv[l]), ptr(cache.zx),
+                     cfg.d_in_proj, dtc, ptr(P[f"{l}.conv_w"]), ptr(P[f"{l}.conv_b"]), B, di, H, s)
             call("msq_mamba_ssd_step", ptr(cache.y), di, ptr(cache.ssm[l]), ptr(cache.xc), cfg.conv_dim, ptr(cache.zx),
                  cfg.d_in_proj, dtc, ptr(P[f"{l}.dt_bias"]), ptr(P[f"{l}.A_log"]), ptr(P[f"{l}.D"]), B, di, H, s)
             call("msq_mamba_gnorm_fwd", ptr(cache.yn), di, ptr(cache.rstd), ptr(cache.y), di, ptr(cache.zx),
@@ -342,7 +347,8 @@ class MambaEngine:
                 ops.gemm(cache.yn, W[f"{l}.out_w"], out=cache.xa)
             else:
                 ops.gemm(cache.yn, W[f"{l}.out_w"], out=cache.x)
-                ops.cast(cache.xa, cache.x)
+                if l < cfg.n_layers - 1:  # (the last layer's output feeds only the final LayerNorm)
+                    ops.cast(cache.xa, cache.x)
         ops.layernorm_fwd(cache.x, P["lnf_w"], P["lnf_b"], out=cache.f, mean=cache.stf[0], rstd=cache.stf[1])
         ops.gemm(cache.f, W["lm_w"], out=cache.logits, epilogue=L.EPI_BIAS, bias=P["lm_b"])
 

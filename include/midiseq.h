@@ -376,6 +376,16 @@ int msq_mamba_ssd_fwd_state(void* y, int64_t ldy, float* states, float* final_st
 int msq_mamba_conv_step(void* xc, int64_t ldxc, float* conv_state, const void* zxbcdt, int64_t ldz, int dtype,
                         const float* conv_w, const float* conv_b, int64_t B, int64_t d_inner, int64_t nheads,
                         void* stream);
+/* bf16 decode, first half of a mixer step (mamba_ssm Mamba2.step's in_proj
+ * + conv1d update): zxbcdt = x . in_w^T (bf16 [B][d_in_proj], in_w
+ * [d_in_proj][d_model]) and msq_mamba_conv_step on its xBC columns, one launch
+ * for B <= 64 rows and d_model <= 1024 (the conv runs in the product's
+ * epilogue), the two launches otherwise. Same results as msq_gemm +
+ * msq_mamba_conv_step.                                                      */
+int msq_mamba_in_proj_conv_step(void* zxbcdt, int64_t ldz, void* xc, int64_t ldxc, float* conv_state, const void* x,
+                                int64_t ldx, const void* in_w, int64_t ldw, const float* conv_w, const float* conv_b,
+                                int64_t B, int64_t d_model, int64_t d_in_proj, int64_t d_inner, int64_t nheads,
+                                void* stream);
 /* one position: h = exp(dt A) h + dt x B^T (ssm_state fp32 [B][H][64][64],
  * in place); y[b] (in dtype) = h C + D x.                                    */
 int msq_mamba_ssd_step(void* y, int64_t ldy, float* ssm_state, const void* xc, int64_t ldxc, const void* zxbcdt,

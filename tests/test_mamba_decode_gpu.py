@@ -122,3 +122,36 @@ def test_unknown_mode_rejected():
     m = Transformer(TransformerConfig(n_embd=64, n_heads=4, n_layer=1, block_len=16, precision="fp32")).to("cuda")
     with pytest.raises(ValueError):
         generate(m, 16, tokens(1, 8, 0), META[:1], num_tokens=2, mode="kv")
+
+
+@pytest.mark.parametrize("B,d_model", [(1, 256), (37, 1024), (64, 1024), (65, 512), (8, 1536)])
+def test_in_proj_conv_step_matches_two_launches(B, d_model):
+    """msq_mamba_in_proj_conv_step (the conv step in the skinny in_proj's
+    epilogue for B <= 64, d_model <= 1024; the two launches past that) against
+    msq_gemm + msq_mamba_conv_step on the same inputs: zx and the shifted conv
+    state bitwise, the conv output within one bf16 step (the two kernels may
+    contract the tap sum into FMAs differently)."""
+    from midiseq import _lib as L, ops
+    from midiseq._lib import call, ptr
+    torch.manual_seed(B)
+    H = 32
+    di, cd = H * 64, H * 64 + 128
+    dp = di + cd + H
+    x = torch.randn(B, d_model, device="cuda").bfloat16()
+    w = (torch.randn(dp, d_model, device="cuda") * d_model ** -0.5).bfloat16()
+    cw = torch.randn(cd, 4, device="cuda") * 0.5
+    cb = torch.randn(cd, device="cuda") * 0.1
+    st0 = torch.randn(B, 3, cd, device="cuda")
+    zx_a, xc_a, st_a = torch.empty(B, dp, device="cuda", dtype=torch.bfloat16), torch.empty(B, cd, device="cuda", dtype=torch.bfloat16), st0.clone()
+    zx_b, xc_b, st_b = torch.empty_like(zx_a), torch.empty_like(xc_a), st0.clone()
+    s = ops.stream()
+    call("msq_mamba_in_proj_conv_step", ptr(zx_a), dp, ptr(xc_a), cd, ptr(st_a), ptr(x), d_model, ptr(w), d_model,
+         ptr(cw), ptr(cb), B, d_model, dp, di, H, s)
+    ops.gemm(x, w, out=zx_b)
+    call("msq_mamba_conv_step", ptr(xc_b), cd, ptr(st_b), ptr(zx_b), dp, L.BF16, ptr(cw), ptr(cb), B, di, H, s)
+    torch.cuda.synchronize()
+    assert torch.equal(zx_a, zx_b)
+    assert torch.equal(st_a, st_b)
+    assert torch.equal(st_a[:, :2], st0[:, 1:])  # the window shifted by one row
+    d = (xc_a.float() - xc_b.float()).abs()
+    assert d.max().item() <= 2 ** -7 * max(1.0, xc_b.float().abs().max().item()), d.max().item()
