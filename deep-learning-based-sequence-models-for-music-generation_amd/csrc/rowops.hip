@@ -779,30 +779,50 @@ extern "C" int msq_cast(void* dst, int dst_dtype, const void* src, int src_dtype
 // ------------------------------------------------------------------ transpose
 // dst[c][r] = src[r][c] (bf16): the transposed weight shadows of the backward's
 // dX products (dY . W reads W^T K-contiguous: the 256 tile's tb = 0 path).
-// 64 x 64 tiles through LDS (one padding column: conflict-free columns).
+// 64 x 64 tiles through LDS with 16-B global loads and stores: a wave moves 8
+// rows x 128 B either way. The LDS image keeps row r's 16-B chunk ch at chunk
+// ch ^ (r >> 3): the transposed reads (8 rows r0 .. r0 + 7 of one column per
+// lane, lanes over 8 row octets x 8 columns) then fall on 32 distinct dwords.
+// Ragged edges (rows / cols not multiples of 8, or past the tile) take the
+// element path.
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(bf16* __restrict__ dst, int64_t ldd,
                                                              const bf16* __restrict__ src, int64_t lds,
                                                              int64_t rows, int64_t cols) {
-    __shared__ bf16 tile[64][66];
+    __shared__ __attribute__((aligned(16))) bf16 tile[64 * 64];
     const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
-    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    const int t = threadIdx.x;
+    const bool vec = (lds % 8 == 0) && (ldd % 8 == 0) && ((uintptr_t)src % 16 == 0) && ((uintptr_t)dst % 16 == 0);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int64_t r = r0 + ty + 8 * k;
+    for (int p = 0; p < 2; ++p) {
+        const int r = (t >> 3) + 32 * p, ch = t & 7;
+        const int64_t gr = r0 + r, gc = c0 + ch * 8;
+        union { u32x4 v; bf16 e[8]; } u;
+        if (vec && gr < rows && gc + 8 <= cols) {
+            u.v = *(const u32x4*)(src + gr * lds + gc);
+        } else {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const int64_t c = c0 + tx + 32 * e;
-            tile[ty + 8 * k][tx + 32 * e] = (r < rows && c < cols) ? src[r * lds + c] : (bf16)0.f;
+            for (int i = 0; i < 8; ++i) u.e[i] = (gr < rows && gc + i < cols) ? src[gr * lds + gc + i] : (bf16)0.f;
         }
+        *(u32x4*)(tile + r * 64 + ((ch ^ (r >> 3)) * 8)) = u.v;
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int64_t c = c0 + ty + 8 * k;
+    for (int p = 0; p < 2; ++p) {
+        const int rch = t & 7, c = (t >> 3) + 32 * p;  // dst row c0 + c, columns r0 + 8 rch .. + 7
+        union { u32x4 v; bf16 e[8]; } u;
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const int64_t r = r0 + tx + 32 * e;
-            if (r < rows && c < cols) dst[c * ldd + r] = tile[tx + 32 * e][ty + 8 * k];
+        for (int i = 0; i < 8; ++i) {
+            const int r = rch * 8 + i;
+            u.e[i] = tile[r * 64 + (((c >> 3) ^ rch) * 8) + (c & 7)];
+        }
+        const int64_t gc = c0 + c, gr = r0 + rch * 8;
+        if (gc >= cols) continue;
+        if (vec && gr + 8 <= rows) {
+            *(u32x4*)(dst + gc * ldd + gr) = u.v;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (gr + i < rows) dst[gc * ldd + gr + i] = u.e[i];
         }
     }
 }

@@ -391,3 +391,18 @@ def test_gemm256_tail_rows_split(epi):
     else:
         o = ops.gemm(A, W, out_dtype=torch.float32)
         assert _rel(o, base) < 2e-3
+
+
+@pytest.mark.parametrize("rows,cols,lds,ldd", [(4256, 1024, 1024, 4256), (1024, 2048, 2048, 1024),
+                                               (17914, 1024, 1024, 17920), (70, 130, 136, 72), (33, 45, 47, 35)])
+def test_transpose_bf16(rows, cols, lds, ldd):
+    """msq_transpose_bf16 (the backward's transposed weight shadows): 16-B
+    vector path for aligned rows, element path at ragged edges / odd strides."""
+    from midiseq._lib import call, ptr
+    g = torch.Generator(device=dev).manual_seed(rows + cols)
+    src = torch.randn(rows, lds, device=dev, generator=g).bfloat16()
+    dst = torch.full((cols, ldd), 7.0, device=dev, dtype=torch.bfloat16)
+    call("msq_transpose_bf16", ptr(dst), ldd, ptr(src), lds, rows, cols, ops.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dst[:, :rows], src[:, :cols].t())
+    assert bool((dst[:, rows:] == 7.0).all())  # nothing written past the rows
