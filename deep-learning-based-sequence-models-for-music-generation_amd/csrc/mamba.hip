@@ -37,121 +37,162 @@ __device__ __forceinline__ float softplus(float x) { return x > 20.f ? x : log1p
 
 // ------------------------------------------------------------------ conv
 // out[b,t,c] = silu(bias[c] + sum_k w[c,k] * in[b, t-3+k, c]), in = zxbcdt[:, off + c]
-// block: 64 channels (lanes) x 4 waves, each wave a contiguous segment of CONV_SEG
-// steps with a sliding 4-tap window (one load per input element)
-constexpr int CONV_SEG = 64;
+// block: 64 lanes x 2 channels each (4-B bf16 / 8-B fp32 loads and stores: a wave
+// instruction moves 128 channels of one time step) x 4 waves, each wave a
+// contiguous segment of CONV_SEG steps with a sliding 4-tap window (one load per
+// input element). Per channel the arithmetic is the scalar form's, in its order.
+// Measured per step (cfg 3, same box): 1 channel per lane, 64 steps 2.71 ms;
+// 2 channels, 32 steps 2.47 (64 steps: the same); 4 channels (222 VGPRs in the
+// backward) 3.38.
+constexpr int CONV_SEG = 32;
 constexpr int CONV_U = 8;
+constexpr int CONV_CV = 2;  // channels per lane
+typedef float f32x2c __attribute__((ext_vector_type(2)));
+typedef f32x2c conv_vec;
+template <typename T>
+using conv_raw_t = typename std::conditional<sizeof(T) == 2, uint32_t, f32x2c>::type;
+template <typename T>
+__device__ __forceinline__ conv_raw_t<T> conv_ld(const T* p) {
+    return *(const conv_raw_t<T>*)p;
+}
+__device__ __forceinline__ conv_vec conv_widen(uint32_t v) {
+    return (conv_vec){__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
+}
+__device__ __forceinline__ conv_vec conv_widen(f32x2c v) { return v; }
+__device__ __forceinline__ void conv_st(bf16* p, conv_vec v) {
+    union { uint32_t u; bf16 e[2]; } h;
+    h.e[0] = (bf16)v[0];
+    h.e[1] = (bf16)v[1];
+    *(uint32_t*)p = h.u;
+}
+__device__ __forceinline__ void conv_st(float* p, conv_vec v) { *(f32x2c*)p = v; }
+
 template <typename T, typename TO>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(MambaArgs a, const T* __restrict__ zx, const float* __restrict__ w,
                                                        const float* __restrict__ bias, TO* __restrict__ out) {
     const int lane = threadIdx.x & 63, ws = threadIdx.x >> 6;
-    const int64_t c = blockIdx.x * 64 + lane;
+    const int64_t c = (blockIdx.x * 64 + lane) * CONV_CV;
     const int64_t b = blockIdx.y;
     const int64_t t0 = ((int64_t)blockIdx.z * 4 + ws) * CONV_SEG, t1 = min(a.L, t0 + CONV_SEG);
     if (c >= a.conv_dim || t0 >= a.L) return;
     const T* src = zx + b * a.L * a.ldz + a.d_inner + c;
     TO* dst = out + b * a.L * a.ldxc + c;
-    float wk[4], win[4];
+    conv_vec wk[4], win[4], bc;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) wk[k] = w[c * 4 + k];
-    const float bc = bias[c];
+    for (int v = 0; v < CONV_CV; ++v) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wk[k][v] = w[(c + v) * 4 + k];
+        bc[v] = bias[c + v];
+    }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int64_t tt = t0 - 3 + k;
-        win[k + 1] = tt >= 0 ? (float)src[tt * a.ldz] : 0.f;
+        win[k + 1] = tt >= 0 ? conv_widen(conv_ld(src + tt * a.ldz)) : (conv_vec){0.f, 0.f};
     }
     // CONV_U steps per batch: their loads are issued together (clamped to the
     // segment, so no branch skips one), then the sliding window runs over them
     for (int64_t tb = t0; tb < t1; tb += CONV_U) {
-        T xin[CONV_U];
+        conv_raw_t<T> xin[CONV_U];
 #pragma unroll
-        for (int u = 0; u < CONV_U; ++u) xin[u] = src[min(tb + u, t1 - 1) * a.ldz];
+        for (int u = 0; u < CONV_U; ++u) xin[u] = conv_ld(src + min(tb + u, t1 - 1) * a.ldz);
 #pragma unroll
         for (int u = 0; u < CONV_U; ++u) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) win[k] = win[k + 1];
-            win[3] = (float)xin[u];
-            float acc = bc;
+            win[3] = conv_widen(xin[u]);
+            conv_vec o;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) acc += wk[k] * win[k];
-            if (tb + u < t1) dst[(tb + u) * a.ldxc] = (TO)silu(acc);
+            for (int v = 0; v < CONV_CV; ++v) {
+                float acc = bc[v];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc += wk[k][v] * win[k][v];
+                o[v] = silu(acc);
+            }
+            if (tb + u < t1) conv_st(dst + (tb + u) * a.ldxc, o);
         }
     }
 }
 
 // dpre = dout * silu'(pre); dzx_in[t] = sum_k w[k] dpre[t+3-k]; dw, dbias via per-block partials (atomics)
-// block: 64 channels (lanes) x 4 waves; wave ws walks the contiguous time segment
-// [t0, t1) of CONV_SEG steps with a sliding window: each input and each dout is
-// loaded once (plus a 3-step halo), pre / dpre computed once per step.
+// block: 64 lanes x 4 channels x 4 waves; wave ws walks the contiguous time
+// segment [t0, t1) of CONV_SEG steps with a sliding window: each input and each
+// dout is loaded once (plus a 3-step halo), pre / dpre computed once per step.
 template <typename T, typename TD>
 __global__ __launch_bounds__(256) void conv_bwd_kernel(MambaArgs a, const T* __restrict__ zx, const float* __restrict__ w,
                                                        const float* __restrict__ bias, const float* __restrict__ dout,
                                                        int64_t ldd, TD* __restrict__ dzx, float* __restrict__ dw,
                                                        float* __restrict__ dbias) {
-    __shared__ float red[4][5][64];
+    __shared__ conv_vec red[4][5][64];
     const int lane = threadIdx.x & 63, ws = threadIdx.x >> 6;
-    const int64_t c = blockIdx.x * 64 + lane;
+    const int64_t c = (blockIdx.x * 64 + lane) * CONV_CV;
     const int64_t b = blockIdx.y;
     const int64_t t0 = ((int64_t)blockIdx.z * 4 + ws) * CONV_SEG, t1 = min(a.L, t0 + CONV_SEG);
-    float gw[4] = {0.f, 0.f, 0.f, 0.f}, gb = 0.f;
+    const conv_vec z4 = (conv_vec){0.f, 0.f};
+    conv_vec gw[4] = {z4, z4, z4, z4}, gb = z4;
     if (c < a.conv_dim && t0 < a.L) {
         const T* src = zx + b * a.L * a.ldz + a.d_inner + c;
         const float* dsrc = dout + b * a.L * ldd + c;
-        float wk[4];
+        conv_vec wk[4], bc;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) wk[k] = w[c * 4 + k];
-        const float bc = bias[c];
+        for (int v = 0; v < CONV_CV; ++v) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) wk[k][v] = w[(c + v) * 4 + k];
+            bc[v] = bias[c + v];
+        }
         // input window in[tau-3 .. tau], dpre ring of tau-3 .. tau
-        float win[4], dp[4] = {0.f, 0.f, 0.f, 0.f};
+        conv_vec win[4], dp[4] = {z4, z4, z4, z4};
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const int64_t tt = t0 - 3 + k;
-            win[k + 1] = tt >= 0 ? (float)src[tt * a.ldz] : 0.f;
+            win[k + 1] = tt >= 0 ? conv_widen(conv_ld(src + tt * a.ldz)) : z4;
         }
         const int64_t tend = min(a.L, t1 + 3);
         // CONV_U steps per batch, their input / dout loads issued together
         // (clamped to tend - 1: no branch skips a load)
         for (int64_t tb = t0; tb < t1 + 3; tb += CONV_U) {
-        T xin[CONV_U];
-        float dyin[CONV_U];
+            conv_raw_t<T> xin[CONV_U];
+            conv_vec dyin[CONV_U];
 #pragma unroll
-        for (int u = 0; u < CONV_U; ++u) {
-            const int64_t tl = min(tb + u, tend - 1);
-            xin[u] = src[tl * a.ldz];
-            dyin[u] = dsrc[tl * ldd];
-        }
+            for (int u = 0; u < CONV_U; ++u) {
+                const int64_t tl = min(tb + u, tend - 1);
+                xin[u] = conv_ld(src + tl * a.ldz);
+                dyin[u] = *(const conv_vec*)(dsrc + tl * ldd);
+            }
 #pragma unroll
-        for (int u = 0; u < CONV_U; ++u) {
-            const int64_t tau = tb + u;
-            if (tau >= t1 + 3) break;
+            for (int u = 0; u < CONV_U; ++u) {
+                const int64_t tau = tb + u;
+                if (tau >= t1 + 3) break;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) win[k] = win[k + 1], dp[k] = dp[k + 1];
-            float d = 0.f;
-            if (tau < tend) {
-                win[3] = (float)xin[u];
-                float pre = bc;
+                for (int k = 0; k < 3; ++k) win[k] = win[k + 1], dp[k] = dp[k + 1];
+                conv_vec d = z4;
+                if (tau < tend) {
+                    win[3] = conv_widen(xin[u]);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) pre += wk[k] * win[k];
-                const float sg = sigm(pre);
-                d = dyin[u] * sg * (1.f + pre * (1.f - sg));
-                if (tau < t1) {
-                    gb += d;
+                    for (int v = 0; v < CONV_CV; ++v) {
+                        float pre = bc[v];
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) gw[k] += d * win[k];
+                        for (int k = 0; k < 4; ++k) pre += wk[k][v] * win[k][v];
+                        const float sg = sigm(pre);
+                        d[v] = dyin[u][v] * sg * (1.f + pre * (1.f - sg));
+                    }
+                    if (tau < t1) {
+                        gb += d;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) gw[k] += d * win[k];
+                    }
+                } else {
+                    win[3] = z4;
                 }
-            } else {
-                win[3] = 0.f;
-            }
-            dp[3] = d;
-            // dzx_in[tau - 3] = sum_k w[k] dpre[tau - k]
-            const int64_t t = tau - 3;
-            if (t >= t0 && t < t1) {
-                float di = 0.f;
+                dp[3] = d;
+                // dzx_in[tau - 3] = sum_k w[k] dpre[tau - k]
+                const int64_t t = tau - 3;
+                if (t >= t0 && t < t1) {
+                    conv_vec di = z4;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) di += wk[k] * dp[3 - k];
-                dzx[(b * a.L + t) * a.ldz + a.d_inner + c] = (TD)di;
+                    for (int k = 0; k < 4; ++k) di += wk[k] * dp[3 - k];
+                    conv_st(dzx + (b * a.L + t) * a.ldz + a.d_inner + c, di);
+                }
             }
-        }
         }
     }
 #pragma unroll
@@ -161,9 +202,12 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(MambaArgs a, const T* __r
     if (ws == 0 && c < a.conv_dim) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
-            const float v = red[0][k][lane] + red[1][k][lane] + red[2][k][lane] + red[3][k][lane];
-            if (k < 4) atomicAdd(dw + c * 4 + k, v);
-            else atomicAdd(dbias + c, v);
+            const conv_vec v = red[0][k][lane] + red[1][k][lane] + red[2][k][lane] + red[3][k][lane];
+#pragma unroll
+            for (int e = 0; e < CONV_CV; ++e) {
+                if (k < 4) atomicAdd(dw + (c + e) * 4 + k, v[e]);
+                else atomicAdd(dbias + c + e, v[e]);
+            }
         }
     }
 }
@@ -1673,7 +1717,9 @@ extern "C" int msq_mamba_conv_fwd(void* xc, int64_t ldxc, const void* zxbcdt, in
                                   int64_t nheads, void* stream) {
     MAMBA_CHECK();
     const MambaArgs a = mk(B, L, d_inner, nheads, ldz, ldxc);
-    const dim3 grid((unsigned)((a.conv_dim + 63) / 64), (unsigned)B, (unsigned)((L + 4 * CONV_SEG - 1) / (4 * CONV_SEG)));
+    MSQ_CHECK_ARG((uintptr_t)zxbcdt % 16 == 0 && (uintptr_t)xc % 16 == 0, "msq_mamba_conv_fwd: 16-B aligned buffers");
+    const dim3 grid((unsigned)((a.conv_dim + 64 * CONV_CV - 1) / (64 * CONV_CV)), (unsigned)B,
+                    (unsigned)((L + 4 * CONV_SEG - 1) / (4 * CONV_SEG)));
     hipStream_t s = (hipStream_t)stream;
     if (dtype == MSQ_BF16) hipLaunchKernelGGL((conv_fwd_kernel<bf16, bf16>), grid, dim3(256), 0, s, a, (const bf16*)zxbcdt, conv_w, conv_b, (bf16*)xc);
     else hipLaunchKernelGGL((conv_fwd_kernel<float, float>), grid, dim3(256), 0, s, a, (const float*)zxbcdt, conv_w, conv_b, (float*)xc);
@@ -1829,11 +1875,14 @@ extern "C" int msq_mamba_conv_bwd(void* dzxbcdt, const float* dxc, int64_t ld_dx
                                   int dtype, const float* conv_w, const float* conv_b, float* g_conv_w,
                                   float* g_conv_b, int64_t B, int64_t L, int64_t d_inner, int64_t nheads,
                                   void* stream) {
-    MSQ_CHECK_ARG(B > 0 && L > 0 && d_inner == nheads * P && ldz % 4 == 0, "mamba conv bwd: bad sizes");
+    MSQ_CHECK_ARG(B > 0 && L > 0 && d_inner == nheads * P && ldz % 4 == 0 && ld_dxc % 4 == 0,
+                  "mamba conv bwd: bad sizes");
+    MSQ_CHECK_ARG((uintptr_t)zxbcdt % 16 == 0 && (uintptr_t)dzxbcdt % 16 == 0 && (uintptr_t)dxc % 16 == 0,
+                  "msq_mamba_conv_bwd: 16-B aligned buffers");
     const MambaArgs a = mk(B, L, d_inner, nheads, ldz, ld_dxc);
     hipStream_t s = (hipStream_t)stream;
     const unsigned tch = (unsigned)((L + 4 * CONV_SEG - 1) / (4 * CONV_SEG));
-    const dim3 grid((unsigned)((a.conv_dim + 63) / 64), (unsigned)B, tch);
+    const dim3 grid((unsigned)((a.conv_dim + 64 * CONV_CV - 1) / (64 * CONV_CV)), (unsigned)B, tch);
     if (dtype == MSQ_BF16) hipLaunchKernelGGL((conv_bwd_kernel<bf16, bf16>), grid, dim3(256), 0, s, a, (const bf16*)zxbcdt, conv_w, conv_b, dxc, ld_dxc, (bf16*)dzxbcdt, g_conv_w, g_conv_b);
     else hipLaunchKernelGGL((conv_bwd_kernel<float, float>), grid, dim3(256), 0, s, a, (const float*)zxbcdt, conv_w, conv_b, dxc, ld_dxc, (float*)dzxbcdt, g_conv_w, g_conv_b);
     MSQ_LAUNCH_CHECK();
