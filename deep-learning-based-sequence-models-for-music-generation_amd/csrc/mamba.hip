@@ -825,6 +825,91 @@ __global__ __launch_bounds__(256, (NK >= 8 ? 2 : 1)) void gnorm_bwd_kernel(
     }
 }
 
+// The same backward with each row split over a pair of waves (bf16 y / z, dn in
+// (256 (NKH - 1) * 2, 512 NKH]): wave h of pair q owns columns 4 lane + 256 (h NKH
+// + k), k < NKH, so a lane holds half the row (114 VGPRs at NKH = 4: 4 waves per
+// SIMD instead of 2). The row's sum is the two waves' sums through LDS (double
+// buffered by iteration, one barrier per row pair); every wave runs the same
+// number of iterations (rows past the end skip their loads and stores).
+template <typename TD, int NKH>
+__global__ __launch_bounds__(256, 4) void gnorm_bwd2_kernel(
+    const bf16* __restrict__ y, int64_t ldy, const bf16* __restrict__ z, int64_t ldz, const float* __restrict__ w,
+    const float* __restrict__ rstd, const float* __restrict__ dout, int64_t ldd, float* __restrict__ dy,
+    TD* __restrict__ dz, float* __restrict__ dw, int64_t rows, int dn) {
+    auto widen = [](uint2 v) -> f32x4 {
+        return (f32x4){__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u), __uint_as_float(v.y << 16),
+                       __uint_as_float(v.y & 0xffff0000u)};
+    };
+    const int lane = threadIdx.x & 63, ws = threadIdx.x >> 6, q = ws >> 1, h = ws & 1;
+    __shared__ f32x4 red[4][64 * NKH];
+    __shared__ float sred[2][2][2];  // [iteration parity][pair][half]
+#pragma unroll
+    for (int k = 0; k < NKH; ++k) red[ws][lane + 64 * k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    int it = 0;
+    for (int64_t base = blockIdx.x * 2LL; base < rows; base += (int64_t)gridDim.x * 2, ++it) {
+        const int64_t row = base + q;
+        const bool ok = row < rows;
+        const float r = ok ? rstd[row] : 0.f;
+        uint2 yv[NKH], zv[NKH];
+        f32x4 dv[NKH];
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < NKH; ++k) {
+            const int c = lane * 4 + 256 * (h * NKH + k);
+            yv[k] = zv[k] = uint2{};
+            dv[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (ok && c < dn) {
+                yv[k] = *(const uint2*)(y + row * ldy + c);
+                dv[k] = *(const f32x4*)(dout + row * ldd + c);
+                zv[k] = *(const uint2*)(z + row * ldz + c);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NKH; ++k) {
+            const int c = lane * 4 + 256 * (h * NKH + k);
+            if (c >= dn) continue;
+            const f32x4 wv = *(const f32x4*)(w + c);
+            const f32x4 zk = widen(zv[k]), yk = widen(yv[k]);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) s += dv[k][t] * wv[t] * yk[t] * silu(zk[t]) * r;
+        }
+        s = wave_sum(s);
+        if (lane == 0) sred[it & 1][q][h] = s;
+        __syncthreads();
+        const float mdn = (sred[it & 1][q][0] + sred[it & 1][q][1]) / dn;
+        if (!ok) continue;
+#pragma unroll
+        for (int k = 0; k < NKH; ++k) {
+            const int c = lane * 4 + 256 * (h * NKH + k);
+            if (c >= dn) continue;
+            const f32x4 wv = *(const f32x4*)(w + c);
+            const f32x4 zk = widen(zv[k]), yk = widen(yv[k]);
+            f32x4 o, zo, pw = red[ws][lane + 64 * k];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float sg = sigm(zk[t]);
+                const float sl = zk[t] * sg;
+                const float n = yk[t] * sl * r;
+                const float dg = r * (dv[k][t] * wv[t] - n * mdn);
+                o[t] = dg * sl;
+                zo[t] = dg * yk[t] * sg * (1.f + zk[t] * (1.f - sg));
+                pw[t] += dv[k][t] * n;
+            }
+            red[ws][lane + 64 * k] = pw;
+            *(f32x4*)(dy + row * ldy + c) = o;
+            store4(dz + row * ldz + c, zo);
+        }
+    }
+    // dw: column c's partials sit with wave h = (c / 256) / NKH of both pairs
+    __syncthreads();
+    const float* rf = (const float*)red;
+    for (int c = threadIdx.x; c < dn; c += 256) {
+        const int kk = c / 256, hh = kk / NKH, k = kk % NKH;
+        const int i = ((c % 256) / 4 + 64 * k) * 4 + c % 4;
+        atomicAdd(dw + c, rf[hh * 64 * NKH * 4 + i] + rf[(2 + hh) * 64 * NKH * 4 + i]);
+    }
+}
+
 template <typename TZ, typename TD>
 void gnorm_bwd_launch(dim3 grid, hipStream_t s, const TZ* y, int64_t ldy, const TZ* z, int64_t ldz, const float* w,
                       const float* rstd, const float* dout, int64_t ldd, float* dy, TD* dz, float* dw, int64_t rows,
@@ -1803,6 +1888,13 @@ extern "C" int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const void* y, int6
     // persistent: 3 workgroups per CU (the wide-row kernel's occupancy); each
     // reduces its dw partials in LDS first
     const dim3 grid(768);
+    if (dtype == MSQ_BF16 && d_inner > 1024 && d_inner <= 2048) {
+        // the row over a wave pair (4 waves per SIMD: 4 workgroups per CU)
+        hipLaunchKernelGGL((gnorm_bwd2_kernel<bf16, 4>), dim3(1024), dim3(256), 0, s, (const bf16*)y, ldy,
+                           (const bf16*)zxbcdt, ldz, w, rstd, dout, ldd, dy, (bf16*)dzxbcdt, dw, rows, (int)d_inner);
+        MSQ_LAUNCH_CHECK();
+        return MSQ_OK;
+    }
     if (dtype == MSQ_BF16)
         gnorm_bwd_launch<bf16, bf16>(grid, s, (const bf16*)y, ldy, (const bf16*)zxbcdt, ldz, w, rstd, dout, ldd, dy, (bf16*)dzxbcdt,
                                      dw, rows, (int)d_inner);

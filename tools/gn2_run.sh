@@ -1,0 +1,4 @@
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 python -u -m pytest tests/test_mamba_gpu.py -x -q --timeout 120 --timeout-method thread -k gnorm > gpurun_out/gn2_test.log 2>&1 || { tail -30 gpurun_out/gn2_test.log; exit 1; }
+tail -1 gpurun_out/gn2_test.log
+bash tools/ab_mamba.sh gn2b $1
