@@ -41,7 +41,7 @@ MAMBA_CLASSES = [
     (r"scan_fwd_kernel|ssd2::state_kernel|ssd2::pass_kernel|ssd2::out_kernel|state_kernel|pass_kernel|out_kernel", "ssd_fwd", 10),
     (r"scan_bwd_kernel|uterm_kernel|rpass_kernel|grad_kernel|dbc_reduce", "ssd_bwd", 10),
     (r"conv_fwd_kernel|conv_bwd_kernel", "mamba_conv", 20),
-    (r"gnorm_fwd_kernel|gnorm_bwd_kernel", "mamba_gnorm", 20),
+    (r"gnorm_fwd_kernel|gnorm_bwd_kernel|gnorm_bwd2_kernel", "mamba_gnorm", 20),
     (r"gemm256_kernel<1, 1, 5|splitk_reduce", "gemm_dW", 21),
     (r"gemm256p_kernel|gemm256_kernel<0|gemm256_kernelILi0E", "gemm_fwd_dX", 42),
     (r"colstats2|rowlse|cspart|cs_reduce|finish2|dbias_reduce|pad_table|wrange|mean_kernel", "loss", 1),
