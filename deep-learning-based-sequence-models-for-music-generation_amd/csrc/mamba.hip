@@ -983,22 +983,22 @@ __device__ __forceinline__ bf16x8 fm(const char* s, int cb, int ks, int lane, in
 }
 // acc[i][j] (lane (il, g), element r) = sum_k A[rb + 16 i + il][k] Bt[cb + 16 j + 4 g + r][k]
 // over k < 64; A rows from image sa (K-contiguous, or transposed when AT), Bt rows likewise
-template <bool AT, bool BT>
-__device__ __forceinline__ void mm(f32x4 (&acc)[2][2], const char* sa, int ha, const char* sb, int hb, int rb, int cb,
+template <bool AT, bool BT, int NJ = 2>
+__device__ __forceinline__ void mm(f32x4 (&acc)[2][NJ], const char* sa, int ha, const char* sb, int hb, int rb, int cb,
                                    int lane) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 av[2], bv[2];
+        bf16x8 av[2], bv[NJ];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
             av[i] = AT ? fm(sa, rb + 16 * i, ks, lane, ha) : fk(sa, rb + 16 * i, ks, lane, ha);
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
             bv[j] = BT ? fm(sb, cb + 16 * j, ks, lane, hb) : fk(sb, cb + 16 * j, ks, lane, hb);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = attn::mfma(bv[j], av[i], acc[i][j]);
+            for (int j = 0; j < NJ; ++j) acc[i][j] = attn::mfma(bv[j], av[i], acc[i][j]);
     }
 }
 __device__ __forceinline__ void zero22(f32x4 (&a)[2][2]) {
@@ -1345,7 +1345,7 @@ __device__ __forceinline__ void dt_cum_raw(const Chunk& k, unsigned raw, float b
 // alternate with the chunk parity), and the LDS image / dt / cum rows are double
 // buffered, so one iteration has two barriers and no load on its critical path.
 constexpr size_t SCAN_LDS = 2 * (IMG + 512);
-__global__ __launch_bounds__(256) void scan_fwd_kernel(MambaArgs a, const bf16* __restrict__ xc,
+__global__ __launch_bounds__(512) void scan_fwd_kernel(MambaArgs a, const bf16* __restrict__ xc,
                                                        const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
                                                        const float* __restrict__ A_log, float* __restrict__ states,
                                                        float* __restrict__ clast, int nch, float* __restrict__ fin) {
@@ -1354,67 +1354,56 @@ __global__ __launch_bounds__(256) void scan_fwd_kernel(MambaArgs a, const bf16* 
     const int64_t bh = blockIdx.x;
     const int64_t h = bh % a.nheads;
     const float A = -expf(A_log[h]), bias = dt_bias[h];
-    const int rb = 32 * (w >> 1), cb = 32 * (w & 1);
-    f32x4 H[2][2];
-    zero22(H);
-    u32x4 x0[2], b0[2], x1[2], b1[2];
+    // 8 waves: wave w owns state rows 32 (w >> 2) .. +31, columns 16 (w & 3) .. +15
+    const int rb = 32 * (w >> 2), cb = 16 * (w & 3);
+    f32x4 H[2][1];
+    H[0][0] = H[1][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    u32x4 x0[1], b0[1], x1[1], b1[1];
     unsigned r0 = 0u, r1 = 0u;
     auto store_state = [&](float* st) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-                *(f32x4*)(st + (rb + 16 * i + (lane & 15)) * N + cb + 16 * j + 4 * (lane >> 4)) = H[i][j];
+            *(f32x4*)(st + (rb + 16 * i + (lane & 15)) * N + cb + 4 * (lane >> 4)) = H[i][0];
     };
-    auto load = [&](int c, u32x4 (&xr)[2], u32x4 (&br)[2], unsigned& raw) {
+    auto load = [&](int c, u32x4 (&xr)[1], u32x4 (&br)[1], unsigned& raw) {
         const Chunk k = chunk_at(a, bh, c);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            xr[u] = ld_clamped(a, k, xc, h * P, tid + 256 * u);
-            br[u] = ld_clamped(a, k, xc, a.d_inner, tid + 256 * u);
-        }
+        xr[0] = ld_clamped(a, k, xc, h * P, tid);
+        br[0] = ld_clamped(a, k, xc, a.d_inner, tid);
         raw = dt_raw_clamped(a, k, zx, tid);
     };
     // chunk c from its register set; then that set takes chunk c + 2
     // c == nch (the odd tail of the unrolled pair) repeats chunk nch - 1 without
     // updating H: every trip runs both bodies, so no branch skips a load or store
-    auto body = [&](int c0, u32x4 (&xr)[2], u32x4 (&br)[2], unsigned& raw) {
+    auto body = [&](int c0, u32x4 (&xr)[1], u32x4 (&br)[1], unsigned& raw) {
         const bool valid = c0 < nch;
         const int c = min(c0, nch - 1);
         const Chunk k = chunk_at(a, bh, c);
         char* sXB = smem + (c & 1) * (IMG + 512);  // half 0: dt x e^{cum_last - cum_s} [s][p]; half 1: B [s][n]
         float* sdt = (float*)(sXB + IMG);
         float* scum = sdt + 64;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int e = tid + 256 * u;
-            *(u32x4*)(sXB + offd(e >> 3, 8 + (e & 7))) = br[u];
-        }
+        *(u32x4*)(sXB + offd(tid >> 3, 8 + (tid & 7))) = br[0];
         dt_cum_raw(k, raw, bias, A, sdt, scum, tid);
         __syncthreads();
         const float cl = scum[k.nval - 1];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int e = tid + 256 * u, row = e >> 3;
+        {
+            const int row = tid >> 3;
             const float f = row < k.nval ? sdt[row] * expf(cl - scum[row]) : 0.f;
             float v[8];
-            unpack8(xr[u], v);
+            unpack8(xr[0], v);
 #pragma unroll
             for (int q = 0; q < 8; ++q) v[q] *= f;
-            *(u32x4*)(sXB + offd(row, e & 7)) = pack8(v);
+            *(u32x4*)(sXB + offd(row, tid & 7)) = pack8(v);
         }
         load(min(c + 2, nch - 1), xr, br, raw);  // unconditional: the wait counts stay static
         __syncthreads();
-        f32x4 acc[2][2];
-        zero22(acc);
-        mm<true, true>(acc, sXB, 0, sXB, 1, rb, cb, lane);  // [p][n] = sum_s X[s][p] B[s][n]
+        f32x4 acc[2][1];
+        acc[0][0] = acc[1][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        mm<true, true, 1>(acc, sXB, 0, sXB, 1, rb, cb, lane);  // [p][n] = sum_s X[s][p] B[s][n]
         const float ecl = expf(cl);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) H[i][j][r] = valid ? ecl * H[i][j][r] + acc[i][j][r] : H[i][j][r];
+            for (int r = 0; r < 4; ++r) H[i][0][r] = valid ? ecl * H[i][0][r] + acc[i][0][r] : H[i][0][r];
         // the entry state of chunk c + 1 (or the final state) is stored right after
         // the update: H is next overwritten one chunk later, so the wait the store's
         // source registers need does not also wait for the next loads
@@ -1847,7 +1836,7 @@ extern "C" int msq_mamba_ssd_fwd_state(void* y, int64_t ldy, float* states, floa
         } else {
             allow_lds(ssd2::scan_fwd_kernel, ssd2::SCAN_LDS);
             if (!final_state) final_state = clast + B * nheads * nch;  // scratch past cum_last
-            hipLaunchKernelGGL(ssd2::scan_fwd_kernel, dim3((unsigned)(B * nheads)), dim3(256), ssd2::SCAN_LDS, s, a,
+            hipLaunchKernelGGL(ssd2::scan_fwd_kernel, dim3((unsigned)(B * nheads)), dim3(512), ssd2::SCAN_LDS, s, a,
                                (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, states, clast, nch,
                                final_state);
         }
