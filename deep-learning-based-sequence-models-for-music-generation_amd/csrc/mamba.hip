@@ -1135,7 +1135,7 @@ __global__ __launch_bounds__(256) void pass_kernel(float* __restrict__ states, c
 // One workgroup per (b, chunk, group of hg heads): the chunk's B / C rows and
 // C B^T (head-independent: only the decay mask L is per head) are staged /
 // computed once and serve the group's heads in turn.
-__global__ __launch_bounds__(256) void out_kernel(MambaArgs a, const bf16* __restrict__ xc,
+__global__ __launch_bounds__(512) void out_kernel(MambaArgs a, const bf16* __restrict__ xc,
                                                   const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
                                                   const float* __restrict__ A_log, const float* __restrict__ Dp,
                                                   bf16* __restrict__ y, int64_t ldy, const float* __restrict__ states,
@@ -1148,28 +1148,27 @@ __global__ __launch_bounds__(256) void out_kernel(MambaArgs a, const bf16* __res
     float* scum = sdt + 64;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, il = lane & 15, g = lane >> 4;
     const Chunk kg = chunk_of(a, nch, hg);
-    const int rb = 32 * (w >> 1), cb = 32 * (w & 1);
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
-        *(u32x4*)(sCB + offd(row, 8 + ch)) = ld_chunk(a, kg, xc, a.d_inner, e);
-        *(u32x4*)(sCB + offd(row, ch)) = ld_chunk(a, kg, xc, a.d_inner + N, e);
+    // 8 waves: wave w computes output rows 32 (w >> 2) .. +31, columns 16 (w & 3) .. +15
+    const int rb = 32 * (w >> 2), cb = 16 * (w & 3);
+    {
+        const int row = tid >> 3, ch = tid & 7;
+        *(u32x4*)(sCB + offd(row, 8 + ch)) = ld_chunk(a, kg, xc, a.d_inner, tid);
+        *(u32x4*)(sCB + offd(row, ch)) = ld_chunk(a, kg, xc, a.d_inner + N, tid);
     }
     __syncthreads();
-    f32x4 gm[2][2];  // C B^T [t][s], shared by the group's heads
-    zero22(gm);
-    mm<false, false>(gm, sCB, 0, sCB, 1, rb, cb, lane);  // [t][s] = sum_n C[t][n] B[s][n]
+    f32x4 gm[2][1];  // C B^T [t][s], shared by the group's heads
+    gm[0][0] = gm[1][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    mm<false, false, 1>(gm, sCB, 0, sCB, 1, rb, cb, lane);  // [t][s] = sum_n C[t][n] B[s][n]
     for (int hh = 0; hh < hg; ++hh) {
         if (hh) __syncthreads();  // the previous head's reads of sXH / sM / scum are done
         Chunk k = kg;
         k.h = kg.h + hh;
         const float A = -expf(A_log[k.h]), Dh = Dp[k.h];
-        u32x4 xr[2];
+        u32x4 xr;
         const float* st = states + ((k.b * a.nheads + k.h) * nch + k.c) * (int64_t)(P * N);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
-            xr[u] = ld_chunk(a, k, xc, k.h * P, e);
+        {
+            const int row = tid >> 3, ch = tid & 7;
+            xr = ld_chunk(a, k, xc, k.h * P, tid);
             const f32x4 h0 = *(const f32x4*)(st + row * N + ch * 8), h1 = *(const f32x4*)(st + row * N + ch * 8 + 4);
             const float hv[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
             *(u32x4*)(sXH + offd(row, 8 + ch)) = pack8(hv);
@@ -1177,22 +1176,21 @@ __global__ __launch_bounds__(256) void out_kernel(MambaArgs a, const bf16* __res
         dt_cum(a, k, zx, dt_bias, A, sdt, scum, tid);
         __syncthreads();
         if (tid == 0) clast[(k.b * a.nheads + k.h) * nch + k.c] = scum[k.nval - 1];  // for rpass
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int e = tid + 256 * u, row = e >> 3;
+        {
+            const int row = tid >> 3;
             float v[8];
-            unpack8(xr[u], v);
+            unpack8(xr, v);
 #pragma unroll
             for (int q = 0; q < 8; ++q) v[q] *= sdt[row];
-            *(u32x4*)(sXH + offd(row, e & 7)) = pack8(v);
+            *(u32x4*)(sXH + offd(row, tid & 7)) = pack8(v);
         }
-        f32x4 y2[2][2];
-        zero22(y2);
-        mm<false, false>(y2, sCB, 0, sXH, 1, rb, cb, lane);  // [t][p] = sum_n C[t][n] H[p][n]
+        f32x4 y2[2][1];
+        y2[0][0] = y2[1][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        mm<false, false, 1>(y2, sCB, 0, sXH, 1, rb, cb, lane);  // [t][p] = sum_n C[t][n] H[p][n]
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
+            for (int j = 0; j < 1; ++j) {
                 const int t = rb + 16 * i + il, s0 = cb + 16 * j + 4 * g;
                 union { uint64_t u; bf16 e[4]; } mv;
 #pragma unroll
@@ -1203,9 +1201,9 @@ __global__ __launch_bounds__(256) void out_kernel(MambaArgs a, const bf16* __res
                 *(uint64_t*)(sM + offd(t, s0 >> 3) + (s0 & 7) * 2) = mv.u;
             }
         __syncthreads();
-        f32x4 y1[2][2];
-        zero22(y1);
-        mm<false, true>(y1, sM, 0, sXH, 0, rb, cb, lane);  // [t][p] = sum_s M[t][s] X[s][p]
+        f32x4 y1[2][1];
+        y1[0][0] = y1[1][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        mm<false, true, 1>(y1, sM, 0, sXH, 0, rb, cb, lane);  // [t][p] = sum_s M[t][s] X[s][p]
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int t = rb + 16 * i + il;
@@ -1213,7 +1211,7 @@ __global__ __launch_bounds__(256) void out_kernel(MambaArgs a, const bf16* __res
             const float et = expf(scum[t]);
             const int64_t row = k.b * a.L + k.t0 + t;
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
+            for (int j = 0; j < 1; ++j) {
                 const int pcol = cb + 16 * j + 4 * g;
                 const f32x4 xv = load4(xc + row * a.ldxc + k.h * P + pcol);
                 store4(y + row * ldy + k.h * P + pcol, y1[i][j] + et * y2[i][j] + Dh * xv);
@@ -1842,7 +1840,7 @@ extern "C" int msq_mamba_ssd_fwd_state(void* y, int64_t ldy, float* states, floa
         }
         // out: one workgroup per (b, chunk, group of hg heads), as grad
         const int hg = nheads % 4 == 0 ? 4 : nheads % 2 == 0 ? 2 : 1;
-        hipLaunchKernelGGL(ssd2::out_kernel, dim3((unsigned)(B * (nheads / hg) * nch)), dim3(256), ssd2::OUT_LDS, s, a,
+        hipLaunchKernelGGL(ssd2::out_kernel, dim3((unsigned)(B * (nheads / hg) * nch)), dim3(512), ssd2::OUT_LDS, s, a,
                            (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, D, (bf16*)y, ldy, states, nch, clast,
                            hg);
         MSQ_LAUNCH_CHECK();
