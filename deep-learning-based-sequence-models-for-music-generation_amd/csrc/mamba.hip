@@ -739,7 +739,7 @@ constexpr int GN_K = 16;
 template <typename TZ, typename TD, int NK>
 __global__ __launch_bounds__(256, (NK >= 8 ? 2 : 1)) void gnorm_bwd_kernel(
     const TZ* __restrict__ y, int64_t ldy, const TZ* __restrict__ z, int64_t ldz, const float* __restrict__ w,
-    const float* __restrict__ rstd, const float* __restrict__ dout, int64_t ldd, float* __restrict__ dy,
+    const float* __restrict__ rstd, const float* __restrict__ dout, int64_t ldd, TZ* __restrict__ dy,
     TD* __restrict__ dz, float* __restrict__ dw, int64_t rows, int dn) {
     // bf16 y / z are held as their raw bits (8 B per 4 columns) and widened at
     // each use, so every load of a row is issued in one burst before the row's
@@ -812,7 +812,7 @@ __global__ __launch_bounds__(256, (NK >= 8 ? 2 : 1)) void gnorm_bwd_kernel(
                 pw[t] += dv[k][t] * n;
             }
             red[ws][lane + 64 * k] = pw;
-            *(f32x4*)(dy + row * ldy + c) = o;
+            store4(dy + row * ldy + c, o);
             store4(dz + row * ldz + c, zo);
         }
     }
@@ -834,7 +834,7 @@ __global__ __launch_bounds__(256, (NK >= 8 ? 2 : 1)) void gnorm_bwd_kernel(
 template <typename TD, int NKH>
 __global__ __launch_bounds__(256, 4) void gnorm_bwd2_kernel(
     const bf16* __restrict__ y, int64_t ldy, const bf16* __restrict__ z, int64_t ldz, const float* __restrict__ w,
-    const float* __restrict__ rstd, const float* __restrict__ dout, int64_t ldd, float* __restrict__ dy,
+    const float* __restrict__ rstd, const float* __restrict__ dout, int64_t ldd, bf16* __restrict__ dy,
     TD* __restrict__ dz, float* __restrict__ dw, int64_t rows, int dn) {
     auto widen = [](uint2 v) -> f32x4 {
         return (f32x4){__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u), __uint_as_float(v.y << 16),
@@ -896,7 +896,7 @@ __global__ __launch_bounds__(256, 4) void gnorm_bwd2_kernel(
                 pw[t] += dv[k][t] * n;
             }
             red[ws][lane + 64 * k] = pw;
-            *(f32x4*)(dy + row * ldy + c) = o;
+            store4(dy + row * ldy + c, o);
             store4(dz + row * ldz + c, zo);
         }
     }
@@ -912,7 +912,7 @@ __global__ __launch_bounds__(256, 4) void gnorm_bwd2_kernel(
 
 template <typename TZ, typename TD>
 void gnorm_bwd_launch(dim3 grid, hipStream_t s, const TZ* y, int64_t ldy, const TZ* z, int64_t ldz, const float* w,
-                      const float* rstd, const float* dout, int64_t ldd, float* dy, TD* dz, float* dw, int64_t rows,
+                      const float* rstd, const float* dout, int64_t ldd, TZ* dy, TD* dz, float* dw, int64_t rows,
                       int dn) {
     const int need = (dn + 255) / 256;
 #define GN(K) hipLaunchKernelGGL((gnorm_bwd_kernel<TZ, TD, K>), grid, dim3(256), 0, s, y, ldy, z, ldz, w, rstd, dout, \
@@ -1230,7 +1230,7 @@ __global__ __launch_bounds__(512) void out_kernel(MambaArgs a, const bf16* __res
 //           per-head parameter gradients (the same algebra as ssd_bwd_kernel above).
 __global__ __launch_bounds__(256) void uterm_kernel(MambaArgs a, const bf16* __restrict__ xc,
                                                     const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
-                                                    const float* __restrict__ A_log, const float* __restrict__ dY,
+                                                    const float* __restrict__ A_log, const bf16* __restrict__ dY,
                                                     int64_t ldy, float* __restrict__ U, int nch) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sYC = smem;  // half 0: e^{cum_t} dY [t][p]; half 1: C [t][n]
@@ -1251,11 +1251,10 @@ __global__ __launch_bounds__(256) void uterm_kernel(MambaArgs a, const bf16* __r
         const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
         float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         if (row < k.nval) {
-            const float* src = dY + (k.b * a.L + k.t0 + row) * ldy + k.h * P + ch * 8;
-            const f32x4 d0 = *(const f32x4*)src, d1 = *(const f32x4*)(src + 4);
+            unpack8(*(const u32x4*)(dY + (k.b * a.L + k.t0 + row) * ldy + k.h * P + ch * 8), v);
             const float et = expf(scum[row]);
-            v[0] = d0[0] * et; v[1] = d0[1] * et; v[2] = d0[2] * et; v[3] = d0[3] * et;
-            v[4] = d1[0] * et; v[5] = d1[1] * et; v[6] = d1[2] * et; v[7] = d1[3] * et;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] *= et;
         }
         *(u32x4*)(sYC + offd(row, ch)) = pack8(v);
     }
@@ -1421,7 +1420,7 @@ __global__ __launch_bounds__(512) void scan_fwd_kernel(MambaArgs a, const bf16* 
 // reverse: dH = 0; for c = last .. 0: U[c] = dH (exit gradient); dH = e^{cum_last_c} dH + U_c
 __global__ __launch_bounds__(256) void scan_bwd_kernel(MambaArgs a, const bf16* __restrict__ xc,
                                                        const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
-                                                       const float* __restrict__ A_log, const float* __restrict__ dY,
+                                                       const float* __restrict__ A_log, const bf16* __restrict__ dY,
                                                        int64_t ldy, float* __restrict__ U, int nch,
                                                        float* __restrict__ dh0) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1433,7 +1432,7 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(MambaArgs a, const bf16* 
     f32x4 D[2][2];
     zero22(D);
     u32x4 c0[2], c1[2];
-    f32x4 y0[2][2], y1[2][2];
+    u32x4 y0[2], y1[2];  // raw bf16 dY rows
     unsigned r0 = 0u, r1 = 0u;
     auto store_d = [&](float* dst) {
 #pragma unroll
@@ -1442,19 +1441,18 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(MambaArgs a, const bf16* 
             for (int j = 0; j < 2; ++j)
                 *(f32x4*)(dst + (rb + 16 * i + (lane & 15)) * N + cb + 16 * j + 4 * (lane >> 4)) = D[i][j];
     };
-    auto load = [&](int c, u32x4 (&cr)[2], f32x4 (&yr)[2][2], unsigned& raw) {
+    auto load = [&](int c, u32x4 (&cr)[2], u32x4 (&yr)[2], unsigned& raw) {
         const Chunk k = chunk_at(a, bh, c);
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
             cr[u] = ld_clamped(a, k, xc, a.d_inner + N, e);
-            const float* src = dY + (k.b * a.L + k.t0 + min(row, k.nval - 1)) * ldy + h * P + ch * 8;
-            yr[u][0] = *(const f32x4*)src;  // rows past nval: zeroed where used
-            yr[u][1] = *(const f32x4*)(src + 4);
+            // rows past nval: zeroed where used
+            yr[u] = *(const u32x4*)(dY + (k.b * a.L + k.t0 + min(row, k.nval - 1)) * ldy + h * P + ch * 8);
         }
         raw = dt_raw_clamped(a, k, zx, tid);
     };
-    auto body = [&](int c0, u32x4 (&cr)[2], f32x4 (&yr)[2][2], unsigned& raw) {
+    auto body = [&](int c0, u32x4 (&cr)[2], u32x4 (&yr)[2], unsigned& raw) {
         const bool valid = c0 >= 0;  // c0 == -1: the odd tail, chunk 0 again without an update
         const int c = max(c0, 0);
         const Chunk k = chunk_at(a, bh, c);
@@ -1473,8 +1471,9 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(MambaArgs a, const bf16* 
             const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
             const float et = row < k.nval ? expf(scum[row]) : 0.f;
             float v[8];
+            unpack8(yr[u], v);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = yr[u][0][q] * et, v[4 + q] = yr[u][1][q] * et;
+            for (int q = 0; q < 8; ++q) v[q] *= et;
             *(u32x4*)(sYC + offd(row, ch)) = pack8(v);
         }
         const float cl = scum[k.nval - 1];
@@ -1507,7 +1506,7 @@ template <typename TD>
 __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* __restrict__ xc,
                                                       const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
                                                       const float* __restrict__ A_log, const float* __restrict__ Dp,
-                                                      const float* __restrict__ dY, int64_t ldy,
+                                                      const bf16* __restrict__ dY, int64_t ldy,
                                                       const float* __restrict__ states, const float* __restrict__ dHx,
                                                       float* __restrict__ dxc, float* __restrict__ dbc,
                                                       TD* __restrict__ dzx,
@@ -1553,7 +1552,7 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
     for (int u = 0; u < 2; ++u) {
         const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
         xr[u] = ld_chunk(a, k, xc, k.h * P, e);
-        float hv[8], dv[8], yv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        float hv[8], dv[8];
         {
             const f32x4 h0 = *(const f32x4*)(Hs + row * N + ch * 8), h1 = *(const f32x4*)(Hs + row * N + ch * 8 + 4);
             const f32x4 d0 = *(const f32x4*)(dHs + row * N + ch * 8), d1 = *(const f32x4*)(dHs + row * N + ch * 8 + 4);
@@ -1562,15 +1561,12 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
 #pragma unroll
             for (int q = 0; q < 8; ++q) hdh += hv[q] * dv[q];
         }
-        if (row < k.nval) {
-            const float* src = dY + (k.b * a.L + k.t0 + row) * ldy + k.h * P + ch * 8;
-            const f32x4 d0 = *(const f32x4*)src, d1 = *(const f32x4*)(src + 4);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) yv[q] = d0[q], yv[4 + q] = d1[q];
-        }
         *(u32x4*)(sHD + offd(row, ch)) = pack8(hv);
         *(u32x4*)(sHD + offd(row, 8 + ch)) = pack8(dv);
-        *(u32x4*)(sXY + offd(row, 8 + ch)) = pack8(yv);
+        // dY rows are bf16 already: copied into the image as they are (zero past nval)
+        *(u32x4*)(sXY + offd(row, 8 + ch)) =
+            row < k.nval ? *(const u32x4*)(dY + (k.b * a.L + k.t0 + row) * ldy + k.h * P + ch * 8)
+                         : (u32x4){0u, 0u, 0u, 0u};
     }
     dt_cum(a, k, zx, dt_bias, A, sdt, scum, tid);
     if (tid < 64) sdcum[tid] = sddt[tid] = 0.f;
@@ -1653,7 +1649,7 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
             f32x4 xv = (f32x4){0.f, 0.f, 0.f, 0.f}, yv = xv;
             if (s < nv) {
                 xv = load4(xc + row * a.ldxc + k.h * P + pc);
-                yv = *(const f32x4*)(dY + row * ldy + k.h * P + pc);
+                yv = load4(dY + row * ldy + k.h * P + pc);
             }
             f32x4 o;
 #pragma unroll
@@ -1884,7 +1880,7 @@ extern "C" int msq_mamba_gnorm_fwd(void* out, int64_t ldo, float* rstd, const vo
     return MSQ_OK;
 }
 
-extern "C" int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const void* y, int64_t ldy, const void* zxbcdt,
+extern "C" int msq_mamba_gnorm_bwd(void* dy, void* dzxbcdt, const void* y, int64_t ldy, const void* zxbcdt,
                                    int64_t ldz, int dtype, const float* w, const float* rstd, const float* dout,
                                    int64_t ldd, float* dw, int64_t rows, int64_t d_inner, void* stream) {
     MSQ_CHECK_ARG(rows > 0 && d_inner % 4 == 0 && d_inner <= 256 * GN_K, "mamba gnorm bwd: bad sizes");
@@ -1895,15 +1891,16 @@ extern "C" int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const void* y, int6
     if (dtype == MSQ_BF16 && d_inner > 1024 && d_inner <= 2048) {
         // the row over a wave pair (4 waves per SIMD: 4 workgroups per CU)
         hipLaunchKernelGGL((gnorm_bwd2_kernel<bf16, 4>), dim3(1024), dim3(256), 0, s, (const bf16*)y, ldy,
-                           (const bf16*)zxbcdt, ldz, w, rstd, dout, ldd, dy, (bf16*)dzxbcdt, dw, rows, (int)d_inner);
+                           (const bf16*)zxbcdt, ldz, w, rstd, dout, ldd, (bf16*)dy, (bf16*)dzxbcdt, dw, rows,
+                           (int)d_inner);
         MSQ_LAUNCH_CHECK();
         return MSQ_OK;
     }
     if (dtype == MSQ_BF16)
-        gnorm_bwd_launch<bf16, bf16>(grid, s, (const bf16*)y, ldy, (const bf16*)zxbcdt, ldz, w, rstd, dout, ldd, dy, (bf16*)dzxbcdt,
+        gnorm_bwd_launch<bf16, bf16>(grid, s, (const bf16*)y, ldy, (const bf16*)zxbcdt, ldz, w, rstd, dout, ldd, (bf16*)dy, (bf16*)dzxbcdt,
                                      dw, rows, (int)d_inner);
     else
-        gnorm_bwd_launch<float, float>(grid, s, (const float*)y, ldy, (const float*)zxbcdt, ldz, w, rstd, dout, ldd, dy,
+        gnorm_bwd_launch<float, float>(grid, s, (const float*)y, ldy, (const float*)zxbcdt, ldz, w, rstd, dout, ldd, (float*)dy,
                                        (float*)dzxbcdt, dw, rows, (int)d_inner);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
@@ -1916,7 +1913,7 @@ extern "C" size_t msq_mamba_ssd_bwd_workspace(int64_t B, int64_t L, int64_t nhea
            (size_t)B * nheads * P * N * sizeof(float);
 }
 
-extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, const float* dY, int64_t ldy,
+extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, const void* dY, int64_t ldy,
                                  const float* states, const void* xc, int64_t ldxc, const void* zxbcdt, int64_t ldz,
                                  int dtype, const float* dt_bias, const float* A_log, const float* D, float* gA_log,
                                  float* gD, float* gdt_bias, int64_t B, int64_t L, int64_t d_inner, int64_t nheads,
@@ -1940,17 +1937,17 @@ extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, cons
         if (getenv("MSQ_MAMBA_SSD_3K")) {
             allow_lds(ssd2::uterm_kernel, ssd2::UTERM_LDS);
             hipLaunchKernelGGL(ssd2::uterm_kernel, gch, dim3(256), ssd2::UTERM_LDS, s, a, (const bf16*)xc,
-                               (const bf16*)zxbcdt, dt_bias, A_log, dY, ldy, U, nch);
+                               (const bf16*)zxbcdt, dt_bias, A_log, (const bf16*)dY, ldy, U, nch);
             hipLaunchKernelGGL(ssd2::rpass_kernel, dim3((unsigned)((B * nheads * P * N + 255) / 256)), dim3(256), 0,
                                s, U, clast, B * nheads, nch);
         } else {
             allow_lds(ssd2::scan_bwd_kernel, ssd2::SCAN_LDS);
             hipLaunchKernelGGL(ssd2::scan_bwd_kernel, dim3((unsigned)(B * nheads)), dim3(256), ssd2::SCAN_LDS, s, a,
-                               (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, dY, ldy, U, nch,
+                               (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, (const bf16*)dY, ldy, U, nch,
                                dbc + B * L * nheads * 2 * N);
         }
         hipLaunchKernelGGL(ssd2::grad_kernel<bf16>, dim3((unsigned)(B * (nheads / hg) * nch)), dim3(256),
-                           ssd2::GRAD_LDS, s, a, (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, D, dY, ldy,
+                           ssd2::GRAD_LDS, s, a, (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, D, (const bf16*)dY, ldy,
                            states, U, dxc, dbc, (bf16*)dzxbcdt, gA_log, gD, gdt_bias, nch, hg);
         hipLaunchKernelGGL(ssd2::dbc_reduce_kernel, dim3((unsigned)((B * L * (2 * N / 4) + 255) / 256)), dim3(256), 0,
                            s, dbc, dxc, B * L, nheads / hg, ldxc, d_inner);
@@ -1959,10 +1956,8 @@ extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, cons
     }
     hipMemset2DAsync(dxc + d_inner, ldxc * sizeof(float), 0, 2 * N * sizeof(float), B * L, s);
     const dim3 grid((unsigned)(B * nheads));
-    allow_lds(ssd_bwd_kernel<bf16, bf16>, BWD_LDS);
     allow_lds(ssd_bwd_kernel<float, float>, BWD_LDS);
-    if (dtype == MSQ_BF16) hipLaunchKernelGGL((ssd_bwd_kernel<bf16, bf16>), grid, dim3(NT), BWD_LDS, s, a, (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, D, dY, ldy, states, dxc, (bf16*)dzxbcdt, gA_log, gD, gdt_bias);
-    else hipLaunchKernelGGL((ssd_bwd_kernel<float, float>), grid, dim3(NT), BWD_LDS, s, a, (const float*)xc, (const float*)zxbcdt, dt_bias, A_log, D, dY, ldy, states, dxc, (float*)dzxbcdt, gA_log, gD, gdt_bias);
+    hipLaunchKernelGGL((ssd_bwd_kernel<float, float>), grid, dim3(NT), BWD_LDS, s, a, (const float*)xc, (const float*)zxbcdt, dt_bias, A_log, D, (const float*)dY, ldy, states, dxc, (float*)dzxbcdt, gA_log, gD, gdt_bias);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }

@@ -140,7 +140,7 @@ class _MActs:
             f32 = torch.float32
             e = lambda *s, dt=act: torch.empty(*s, device=device, dtype=dt)  # noqa: E731
             self._bwd = dict(gx=e(M, cfg.d_model, dt=f32), gxb=e(M, cfg.d_model), dyn=e(M, cfg.d_inner, dt=f32),
-                             dy=e(M, cfg.d_inner, dt=f32), dzx=e(M, cfg.d_in_proj), dxc=e(M, cfg.conv_dim, dt=f32),
+                             dy=e(M, cfg.d_inner), dzx=e(M, cfg.d_in_proj), dxc=e(M, cfg.conv_dim, dt=f32),
                              df=e(self.B * self.T, cfg.d_model), dlogits=torch.zeros(self.B * self.T, cfg.v_pad, device=device, dtype=act))
         return self._bwd
 

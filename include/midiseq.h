@@ -343,16 +343,18 @@ int msq_mamba_ssd_fwd(void* y, int64_t ldy, float* states, const void* xc, int64
 int msq_mamba_gnorm_fwd(void* out, int64_t ldo, float* rstd, const void* y, int64_t ldy, const void* zxbcdt,
                         int64_t ldz, int dtype, const float* w, int64_t rows, int64_t d_inner, float eps,
                         void* stream);
-/* dy (fp32, ld = ldy) and dz (into dzxbcdt[:, :d_inner]); dw accumulates.   */
-int msq_mamba_gnorm_bwd(float* dy, void* dzxbcdt, const void* y, int64_t ldy, const void* zxbcdt, int64_t ldz,
+/* dy (in dtype, ld = ldy: bf16 in the bf16 path, as mamba_ssm's gradient of its
+ * bf16 y) and dz (into dzxbcdt[:, :d_inner]); dw accumulates.               */
+int msq_mamba_gnorm_bwd(void* dy, void* dzxbcdt, const void* y, int64_t ldy, const void* zxbcdt, int64_t ldz,
                         int dtype, const float* w, const float* rstd, const float* dout, int64_t ldd, float* dw,
                         int64_t rows, int64_t d_inner, void* stream);
 /* dxc fp32 [B*L, ldxc]: dx (written) | dB, dC (reduced over heads); dt_raw
  * grads into dzxbcdt[:, d_inner+conv_dim+h]; gA_log / gD / gdt_bias accumulate.
  * workspace: msq_mamba_ssd_bwd_workspace() bytes (the bf16 path's per-chunk
- * state gradients; the fp32 path ignores it and accepts NULL).               */
+ * state gradients; the fp32 path ignores it and accepts NULL). dY in dtype
+ * (msq_mamba_gnorm_bwd's dy).                                                */
 size_t msq_mamba_ssd_bwd_workspace(int64_t B, int64_t L, int64_t nheads);
-int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, const float* dY, int64_t ldy, const float* states,
+int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, const void* dY, int64_t ldy, const float* states,
                       const void* xc, int64_t ldxc, const void* zxbcdt, int64_t ldz, int dtype, const float* dt_bias,
                       const float* A_log, const float* D, float* gA_log, float* gD, float* gdt_bias, int64_t B,
                       int64_t L, int64_t d_inner, int64_t nheads, void* workspace, void* stream);

@@ -162,8 +162,8 @@ def test_gnorm_bwd_kernel_matches_autograd(rows, dn):
     """msq_mamba_gnorm_bwd (bf16 y / z, fp32 dout; the wave-pair kernel for
     d_inner in (1024, 2048], the one-wave kernel below) against torch autograd
     of out = (y silu(z)) rstd w over the same bf16-rounded inputs, rstd from the
-    forward; dy / dw fp32, dz bf16. Tolerance 1e-2 relative to each gradient's
-    scale (dz is stored in bf16)."""
+    forward; dy / dz bf16, dw fp32. Tolerance 1e-2 relative to each gradient's
+    scale (dy / dz are stored in bf16)."""
     from midiseq import _lib as L, ops
     from midiseq._lib import call, ptr
     torch.manual_seed(rows + dn)
@@ -179,13 +179,13 @@ def test_gnorm_bwd_kernel_matches_autograd(rows, dn):
     rstd = torch.rsqrt(g.pow(2).mean(-1, keepdim=True) + eps)
     out = g * rstd * wf  # rstd is saved by the forward, the backward differentiates through it
     out.backward(dout)
-    dy = torch.empty(rows, dn, device="cuda")
+    dy = torch.empty(rows, dn, device="cuda", dtype=torch.bfloat16)  # dy in the compute dtype
     dzx = torch.zeros(rows, ldz, device="cuda", dtype=torch.bfloat16)
     dw = torch.zeros(dn, device="cuda")
     call("msq_mamba_gnorm_bwd", ptr(dy), ptr(dzx), ptr(y), dn, ptr(zx), ldz, L.BF16, ptr(w),
          ptr(rstd.detach().reshape(-1).contiguous()), ptr(dout), dn, ptr(dw), rows, dn, ops.stream())
     torch.cuda.synchronize()
-    for got, want in ((dy, yf.grad), (dzx[:, :dn].float(), zf.grad), (dw, wf.grad)):
+    for got, want in ((dy.float(), yf.grad), (dzx[:, :dn].float(), zf.grad), (dw, wf.grad)):
         err = (got - want).abs().max().item()
         assert err <= 1e-2 * want.abs().max().item(), err
     assert bool((dzx[:, dn:] == 0).all())  # dt / xBC columns untouched
