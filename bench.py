@@ -102,10 +102,10 @@ CLASSIFY = {
     "msq_mamba_ssd_fwd_state": lambda a: ("ssd_fwd", None, (4 * a[14] + 4 * 64 + 2 * a[15]) * float(a[12] * a[13])),
     # the rest of the Mamba2 mixer, bytes per token per layer as the kernels move
     # them (Mamba byte model; N = 64 states, conv_dim = di + 128):
-    # ssd_bwd: dy f32 + xc bf16 + dt + chunk states f32 (H P N 4 / 64 tokens) in,
-    #          dxc f32 + ddt out
+    # ssd_bwd: dy bf16 (the compute dtype, since 840be59) + xc bf16 + dt + chunk
+    #          states f32 (H P N 4 / 64 tokens) in, dxc f32 + ddt out
     "msq_mamba_ssd_bwd": lambda a: ("ssd_bwd", None, float(a[17] * a[18]) * (
-        4 * a[19] + 2 * (a[19] + 128) + 2 * a[20] + a[20] * 64 * 64 * 4 / 64 + 4 * (a[19] + 128) + 2 * a[20])),
+        2 * a[19] + 2 * (a[19] + 128) + 2 * a[20] + a[20] * 64 * 64 * 4 / 64 + 4 * (a[19] + 128) + 2 * a[20])),
     # conv fwd: xBC bf16 in, xc bf16 out; bwd: dxc f32 + xBC bf16 in, dxBC bf16 out
     "msq_mamba_conv_fwd": lambda a: ("mamba_conv", None, float(a[7] * a[8]) * 4 * (a[9] + 128)),
     "msq_mamba_conv_bwd": lambda a: ("mamba_conv", None, float(a[10] * a[11]) * 8 * (a[12] + 128)),

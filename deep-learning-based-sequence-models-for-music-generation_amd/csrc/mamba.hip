@@ -1922,7 +1922,9 @@ extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, cons
     MSQ_CHECK_ARG(ld_dxc == ldxc, "msq_mamba_ssd_bwd: dxc must share the xBC row stride");
     const MambaArgs a = mk(B, L, d_inner, nheads, ldz, ldxc);
     hipStream_t s = (hipStream_t)stream;
-    // dB / dC columns are accumulated with atomics across heads
+    // bf16 path: grad writes one dB / dC row per (token, head group) into dbc and
+    // dbc_reduce_kernel sums the groups' rows in a fixed order (no atomics); the
+    // fp32 path below accumulates the columns with atomics across heads
     if (dtype == MSQ_BF16) {
         MSQ_CHECK_ARG(workspace, "msq_mamba_ssd_bwd: the bf16 path needs msq_mamba_ssd_bwd_workspace() bytes");
         const int nch = (int)((L + Q - 1) / Q);

@@ -15,18 +15,21 @@ import torch.distributed as dist
 
 
 class GradBuckets:
-    def __init__(self, grads: torch.Tensor, ranges, group=None, on_reduced=None):
+    def __init__(self, grads: torch.Tensor, ranges, group=None, on_reduced=None, force=False):
         """ranges: dict key -> (start, end) slices of ``grads``; keys are the
         notification ids passed to ``ready``. on_reduced(start, end, scale):
         called on the all-reduce side stream as soon as a bucket's SUM is in
         (the per-bucket optimizer: train_parallel.TrainStep runs the fused Adam
         over that slice there, so the last buckets' updates no longer queue
-        behind one global Adam after the backward)."""
+        behind one global Adam after the backward). force: issue the bucket
+        collectives even at world size 1 (the RCCL path on one GPU: the SUM
+        is then the identity, every stream dependency still runs)."""
         self.grads = grads
         self.ranges = dict(ranges)
         self.group = group
         self.on_reduced = on_reduced
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.force = force and dist.is_initialized()
         self.handles = []
         self.side = torch.cuda.Stream(device=grads.device) if grads.is_cuda else None
 
@@ -50,7 +53,7 @@ class GradBuckets:
         self.on_reduced(s, e, 1.0 / self.world)
 
     def ready(self, key):
-        if self.world == 1 or key not in self.ranges:
+        if (self.world == 1 and not self.force) or key not in self.ranges:
             return
         s, e = self.ranges[key]
         buf = self.grads[s:e]
@@ -74,7 +77,7 @@ class GradBuckets:
         return 1.0 / self.world
 
     def broadcast_params(self, flat: torch.Tensor, src=0):
-        if self.world > 1:
+        if self.world > 1 or self.force:
             dist.broadcast(flat, src=src, group=self.group)
 
 

@@ -305,11 +305,12 @@ class MambaEngine:
         # ~7 launches per layer from the host
         # (the graph reads the token from the cache's staging buffer: a fresh
         # token tensor per step costs a device copy, not a re-capture)
+        # stage first: a token tensor of a new shape / device reallocates the
+        # staging buffer and drops the graph that read the old one
+        tb = cache.stage_tok(tok) if self.step_graphs else tok
         if self.step_graphs and cache.graph is not None:
-            cache.stage_tok(tok)
             cache.graph.replay()
         elif self.step_graphs and cache.eager_steps >= 1:
-            tb = cache.stage_tok(tok)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._step_body(tb, cache)

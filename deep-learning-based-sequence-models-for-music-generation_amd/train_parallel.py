@@ -26,7 +26,10 @@ class TrainStep:
     with DDP all-reduce, Adam(lr=5e-5)) for a Transformer or Mamba drop-in."""
 
     def __init__(self, model, lr=LEARNING_RATE, betas=(0.9, 0.999), eps=1e-8, grammar=None,
-                 group=None):
+                 group=None, ddp=None):
+        """ddp: None = bucketed all-reduce when the process group has more
+        than one rank; True = also at world size 1 (the RCCL bucket path on
+        one GPU; MSQ_DDP_BUCKETS=1 does the same)."""
         self.model = model
         self.eng = model.engine
         flat = model.flat.data
@@ -45,9 +48,11 @@ class TrainStep:
         # the whole buffer after the backward); slices of an elementwise
         # update, so the parameters are bitwise those of the global step
         self.bucket_adam = os.environ.get("MSQ_GLOBAL_ADAM") != "1"
-        if dist.is_initialized() and dist.get_world_size(group) > 1:
+        if ddp is None:
+            ddp = os.environ.get("MSQ_DDP_BUCKETS") == "1" or None
+        if dist.is_initialized() and (ddp or dist.get_world_size(group) > 1):
             self.buckets = GradBuckets(self.grads, self.eng.bucket_ranges(), group,
-                                       on_reduced=self._adam_slice if self.bucket_adam else None)
+                                       on_reduced=self._adam_slice if self.bucket_adam else None, force=bool(ddp))
             self.buckets.broadcast_params(flat)
             self.eng.refresh_shadow(force=True)
             self.eng.layer_grad_ready = self.buckets.ready

@@ -5,7 +5,12 @@ two-stream backward with the engine's per-layer bucket hooks (ddp.GradBuckets
 all-reducing on its side stream), fused Adam with the 1/world scale.
 Rank 0 writes the averaged gradient and the updated parameters to an .npz.
 
-usage (under torch.distributed.run): ddp_worker.py <transformer|mamba> <same|split> <out.npz>"""
+Mode "rccl1" (world 1, backend nccl = RCCL, through setup_distributed()):
+TrainStep(ddp=True) keeps the bucket path at world size 1, so every layer
+bucket is a real ProcessGroupNCCL all_reduce issued from the side stream,
+waited on that stream (h.wait()), with the per-bucket Adam after it.
+
+usage (under torch.distributed.run): ddp_worker.py <transformer|mamba> <same|split|bucketcheck|rccl1> <out.npz>"""
 import os
 import sys
 
@@ -84,6 +89,8 @@ def main():
 
 def _main():
     kind, mode, out = sys.argv[1], sys.argv[2], sys.argv[3]
+    if mode == "rccl1":
+        return _main_rccl1(kind, out)
     rank, _, world = setup_distributed(backend="gloo")
     assert world == 2
     torch.cuda.set_device(0)
@@ -114,6 +121,46 @@ def _main():
     if rank == 0:
         np.savez(out, grads=(step.grads / world).cpu().numpy(), flat=model.flat.data.cpu().numpy(),
                  loss=loss.item(), **extra)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _main_rccl1(kind, out):
+    """World 1 over RCCL: the bucketed step (two steps, so the second runs on
+    Adam moments the per-bucket updates wrote) against one global fused Adam
+    over the same reduced gradients (bitwise), and the step's gradients
+    against a non-DDP TrainStep from the same start."""
+    from midiseq import ops
+    rank, local, world = setup_distributed()
+    assert world == 1 and dist.get_backend() == "nccl", (world, dist.get_backend())
+    torch.manual_seed(0)
+    model = build_model(kind).to(torch.device("cuda", local))
+    start = model.flat.data.clone()
+    step = TrainStep(model, ddp=True)
+    assert step.buckets is not None and step.buckets.force and step.eng.layer_grad_ready is not None
+    src, trg, meta = (t[0:2].cuda() for t in full_batch())
+    ref, m, v = model.flat.data.clone(), torch.zeros_like(start), torch.zeros_like(start)
+    for _ in range(2):
+        loss = step(src, trg, meta)
+        torch.cuda.synchronize()
+        # the same reduced gradients through one global Adam from the same start
+        ops.adam_step(ref, step.grads, m, v, step.step_no, step.lr, step.betas[0], step.betas[1], step.eps)
+        torch.cuda.synchronize()
+    g_ddp = step.grads.cpu().numpy()
+    flat_ddp, ref_np = model.flat.data.cpu().numpy(), ref.cpu().numpy()
+    m_ddp, v_ddp = step.m.cpu().numpy(), step.v.cpu().numpy()
+    # a plain (bucket-free) TrainStep, two steps from the same start
+    model2 = build_model(kind).to(torch.device("cuda", local))
+    with torch.no_grad():
+        model2.flat.data.copy_(start)
+    plain = TrainStep(model2, ddp=False)
+    assert plain.buckets is None
+    for _ in range(2):
+        loss2 = plain(src, trg, meta)
+    torch.cuda.synchronize()
+    np.savez(out, grads=g_ddp, grads_plain=plain.grads.cpu().numpy(), flat=flat_ddp, ref=ref_np,
+             flat_plain=model2.flat.data.cpu().numpy(), m=m_ddp, m_ref=m.cpu().numpy(), v=v_ddp,
+             v_ref=v.cpu().numpy(), loss=loss.item(), loss_plain=loss2.item(), backend=dist.get_backend())
     dist.barrier()
     dist.destroy_process_group()
 

@@ -28,12 +28,12 @@ pytestmark = pytest.mark.gpu
 HERE = Path(__file__).parent
 
 
-def _run_world2(kind, mode, tmp_path, env=None):
+def _run_world2(kind, mode, tmp_path, env=None, nproc=2):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     out = tmp_path / f"{kind}_{mode}_{len(env or {})}.npz"
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={port}", str(HERE / "ddp_worker.py"), kind, mode, str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240,
                        env=dict(os.environ, OMP_NUM_THREADS="4", **(env or {})))
@@ -95,3 +95,26 @@ def test_world2_per_bucket_adam_equals_global_adam(kind, tmp_path):
     b = _run_world2(kind, "split", tmp_path, env={"MSQ_GLOBAL_ADAM": "1"})
     d = np.abs(a["flat"] - b["flat"])
     assert d.max() <= 1e-6 and (d > 2e-7).sum() <= 16, (d.max(), (d > 2e-7).sum())
+
+
+@pytest.mark.parametrize("kind", ["transformer", "mamba"])
+def test_rccl_world1_bucket_path(kind, tmp_path):
+    """The RCCL path itself: torch.distributed.run with one
+    rank, setup_distributed() -> backend nccl (= RCCL), TrainStep(ddp=True):
+    every layer bucket is a ProcessGroupNCCL all_reduce issued from the side
+    stream, waited on that stream, then the per-bucket Adam there. After two
+    steps the parameters and moments equal one global Adam over the same
+    reduced gradients bit for bit (a bucket whose Adam ran before its
+    collective, or never, or twice, breaks this), and the gradients equal a
+    bucket-free TrainStep's up to the backward's atomics noise.
+    Reference: train_parallel.py:144-151 (init_process_group nccl, DDP)."""
+    a = _run_world2(kind, "rccl1", tmp_path, nproc=1)
+    assert str(a["backend"]) == "nccl"
+    assert np.array_equal(a["flat"], a["ref"])
+    assert np.array_equal(a["m"], a["m_ref"]) and np.array_equal(a["v"], a["v_ref"])
+    g, gp = a["grads"], a["grads_plain"]
+    err = np.abs(g - gp).max()
+    assert err <= 1e-5 * np.abs(gp).max(), err
+    assert abs(float(a["loss"]) - float(a["loss_plain"])) <= 1e-5 * abs(float(a["loss_plain"]))
+    d = np.abs(a["flat"] - a["flat_plain"])
+    assert d.max() <= 2e-6 and (d > 2e-7).sum() <= 32, (d.max(), (d > 2e-7).sum())
