@@ -486,6 +486,12 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU check of the launch: init gloo ranks, verify the world size, print, exit")
     args = ap.parse_args()
+    # stdout carries exactly the one JSON line: everything else written to fd 1
+    # (RCCL's version banner at communicator init, library chatter) goes to stderr
+    out_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
+    emit = lambda obj: os.write(out_fd, (json.dumps(obj) + "\n").encode())  # noqa: E731
 
     rank, local, world = setup_distributed(backend="gloo" if args.dry_run else None)
     assert world == args.gpus, f"bench.py --gpus {args.gpus} but the process group has {world} ranks"
@@ -497,7 +503,7 @@ def main():
         else:
             ranks = [rank]
         if rank == 0:
-            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": ranks}), flush=True)
+            emit({"dry_run": True, "n_gpus": world, "ranks": ranks})
         return
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -507,7 +513,7 @@ def main():
         r = mamba_leg(dev, rank, world, timer, steps=args.steps, overlap=not args.serial, class_steps=args.class_steps)
         L.TAP = None
         if rank == 0:
-            print(json.dumps({"mamba_train": r}), flush=True)
+            emit({"mamba_train": r})
         return
     cfg = TransformerConfig(n_layer=args.layers, block_len=args.seq, precision="bf16", dropout=args.dropout)
     model = Transformer(cfg).to(dev)
@@ -615,9 +621,10 @@ def main():
         out.update(extra)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
+        emit(out)
+    if dist.is_initialized():
+        if world > 1:
+            dist.barrier()
         dist.destroy_process_group()
 
 

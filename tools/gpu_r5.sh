@@ -13,5 +13,5 @@ fi
 timeout -k 10 600 python -u bench.py > gpurun_out/$tag/bench.json 2> gpurun_out/$tag/bench.err || { echo "bench failed"; tail -30 gpurun_out/$tag/bench.err; exit 1; }
 cat gpurun_out/$tag/bench.json
 MSQ_DDP_BUCKETS=1 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr=127.0.0.1 --master-port=29531 bench.py --gpus 1 --no-extra --no-cpu-baseline > gpurun_out/$tag/bench_rccl1.json 2> gpurun_out/$tag/bench_rccl1.err || { echo "rccl bench failed"; tail -30 gpurun_out/$tag/bench_rccl1.err; exit 1; }
-cat gpurun_out/$tag/bench_rccl1.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('rccl1', d['ms_per_step'], d['value'])"
+grep "^{" gpurun_out/$tag/bench_rccl1.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('rccl1', d['ms_per_step'], d['value'])"
 echo done
