@@ -124,20 +124,56 @@ __device__ __forceinline__ void drain_a(f32x16 (&x)[4], f32x16 (&y)[4]) {
 // query row of accumulator register e in lane half hh (32x32 C/D map)
 __device__ __forceinline__ int acc_row(int e, int hh) { return (e & 3) + 8 * (e >> 2) + 4 * hh; }
 __device__ __forceinline__ float and_f(float x, int m) { return __int_as_float(__float_as_int(x) & m); }
+// D = A.B + C with C a separate register tuple (the row constants)
+__device__ __forceinline__ void mfma_init_va(f32x16& acc, bf16x8 a, const bf16x8& b, const f32x16& c) {
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(acc) : "v"(a), "a"(b), "v"(c));
+}
+// IR-level pin: a value passed through an empty volatile asm is (re)defined
+// at that point of the side-effect-ordered instruction stream, so arithmetic
+// on it cannot be hoisted into an earlier MFMA gap, and a pinned result exists
+// before the next gap's sched_barrier. Without them the IR passes gathered
+// the softmax of 16 gaps into 3 (one gap carried 71 VALU and 8 v_exp).
+template <typename T>
+__device__ __forceinline__ void pin(T& x) {
+#ifndef KV_NOPIN
+    asm volatile("" : "+v"(x));
+#endif
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+    const bf16x2 v = (bf16x2){(bf16)a, (bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ bf16x8 words8(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return __builtin_bit_cast(bf16x8, (u32x4){a, b, c, d});
+}
+__device__ __forceinline__ f32x16 cat16(const f32x4 (&v)[4]) {
+    f32x16 r;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) r[e] = v[e >> 2][e & 3];
+    return r;
+}
 
 struct Acc {
     f32x16 s, dp, q0, q1;  // S = Q.K^T, dP = dO.V^T, QR window blocks 0 / 1 (query rows x keys)
 };
 
-// l2 = lse * log2(e), dsc = D * scale (per query row, flash_bwd_pre_vec_kernel)
+// nls = -lse / scale, ndk = -D / ks (per query row, flash_bwd_pre_vec_kernel):
+// the initial accumulators of the S and dP chains, so that (c2 = scale log2 e)
+//   S' = q.k - lse/scale,  P ks scale = exp2(c2 (S' + q.R) + log2(ks scale)),
+//   dP' = dO.v - D/ks,     dS = (P ks scale) (m ? dP' : -D/ks)
+// (dV, accumulated from the same P ks scale, is divided by scale at the end)
 template <bool DROP>
-__global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const float* __restrict__ lse,
-                                                              const float* __restrict__ Dv,
+__global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const float* __restrict__ nls,
+                                                              const float* __restrict__ ndk,
                                                               const bf16* __restrict__ dout, int64_t ldo,
                                                               bf16* __restrict__ dqkv, int64_t ldd,
                                                               bf16* __restrict__ dqr, bf16* __restrict__ dsj,
                                                               int64_t ldr) {
+#ifndef KV_ABL_NOSTORE
     constexpr int NST = 4;  // dS row stores per wave and iteration (2 r-indexed, 2 j-indexed)
+#else
+    constexpr int NST = 0;  // (ablation build: no dS stores)
+#endif
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sR = smem + O_R;
     const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, c32 = lane & 31;
@@ -153,15 +189,16 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
     const __amdgpu_buffer_rsrc_t rq = make_rsrc(qkv_b, (uint32_t)((int64_t)S * ldq * 2));
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(dout_b, (uint32_t)((int64_t)S * ldo * 2));
     const __amdgpu_buffer_rsrc_t rr = make_rsrc((const bf16*)a.R + (int64_t)h * a.S_max * HS, (uint32_t)(S * HS * 2));
-    const float* Lp = lse + ((int64_t)b * H + h) * S;
-    const float* Dp = Dv + ((int64_t)b * H + h) * S;
+    const float* Lp = nls + ((int64_t)b * H + h) * S;
+    const float* Dp = ndk + ((int64_t)b * H + h) * S;
     const __amdgpu_buffer_rsrc_t rl = make_rsrc(Lp, (uint32_t)(S * 4));
     const __amdgpu_buffer_rsrc_t rd = make_rsrc(Dp, (uint32_t)(S * 4));
     bf16* qr_rows = dqr + ((int64_t)h * a.B + b) * S * ldr;
     bf16* sj_rows = dsj + ((int64_t)h * a.B + b) * S * ldr;
     const float c2 = a.scale * LOG2E;
-    // dS = P (dP m ks - D) scale = P fma(dP m, ks scale, -D scale)
+    // P ks scale = exp2(c2 x + lks): the dS factor ks scale rides in P
     const float ks_scale = (DROP ? a.keep_scale : 1.f) * a.scale;
+    const float lks = __builtin_log2f(ks_scale);
 
     // key-side B operands: lane (key c32, half hh) holds K[key][16 ks + 8 hh + 0..7]
     bf16x8 kf[8], vf[8];
@@ -184,7 +221,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
         for (int e = 0; e < 16; ++e) dk[n][e] = dv[n][e] = 0.f;
 
     // mutable copies of the lane constants the loop uses (made opaque per iteration)
-    int ltid = tid, lhh = hh, lc32 = c32, ljk = jk, lhh7 = hh << 7, lz0 = c32 + 4 * hh, lbpb0 = (c32 - 4 * hh - 1) * 4;
+    int ltid = tid, lhh = hh, lc32 = c32, ljk = jk;
     // query tiles i0 = j0 + 32 t (causal: i >= j0; block 0 also the metadata rows)
     const int it0 = j0;
     const int nqt = (S - it0 + QT - 1) / QT;
@@ -210,8 +247,18 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
     const __amdgpu_buffer_rsrc_t rm =
         make_rsrc(DROP ? (const void*)(a.colmask + (int64_t)(b * H + h) * (mask_bh_bytes(mld) / 4)) : (const void*)a.R,
                   DROP ? (uint32_t)mask_bh_bytes(mld) : 0u);
+    // the row-constant / keep-word piece: its descriptor and lane part (the
+    // keep word of key j against queries c.. is mask_word(mld, j, c) = lane
+    // part (key) + query part (c), computed per tile in scalars)
+    const __amdgpu_buffer_rsrc_t rpc = w == 0 ? rl : (w == 1 ? rd : rm);
+    const uint32_t pc_lane = [&] {
+        const int ln = lane;
+        if (w < 2) return (uint32_t)(ln * 4);
+        const int64_t key = j0 + 64 * (w - 2) + ln;
+        return (uint32_t)((((key >> 6) * (mld >> 1)) * 128 + (key & 63) * 2) * 4);
+    }();
     // staging piece p (0..6) of query tile T (R chunk T + 4): Q 0-1, dO 2-3,
-    // row constants 4 (lse / D on waves 0-1, keep words colmask[b,h,j][i0/32]
+    // row constants 4 (nls / ndk on waves 0-1, keep words colmask[b,h,j][i0/32]
     // of the block's keys on waves 2-3, a zero-filling dummy without dropout),
     // R 5-6. Every piece is issued by every wave (out-of-range rows: dropped
     // offset), so the per-iteration vmcnt arithmetic is exact.
@@ -225,14 +272,12 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
             if (p < 2) dma16(rq, smem + O_Q + buf * TILE + w * 2048 + k * 1024, offQ[k] + (uint32_t)i0 * (uint32_t)(ldq * 2));
             else dma16(ro, smem + O_O + buf * TILE + w * 2048 + k * 1024, offO[k] + (uint32_t)i0 * (uint32_t)(ldo * 2));
         } else if (p == 4) {
-            const int ln = ltid & 63;
-            if (w < 2) {
-                dma4(w == 0 ? rl : rd, smem + O_L + (buf * 2 + w) * 256, (uint32_t)((i0 + ln) * 4));
-            } else {
-                const int key = j0 + 64 * (w - 2) + ln;
-                dma4(rm, smem + O_D + buf * KB * 4 + (w - 2) * 256,
-                     DROP && i0 < S ? (uint32_t)(mask_word(mld, key, i0) * 4) : OOB);
-            }
+            // one dword per lane, branch-free: waves 0 / 1 the row constants of
+            // rows i0 + lane, waves 2 / 3 the keep words of keys j0 + 64 (w-2) + lane
+            const uint32_t sc = w < 2 ? (uint32_t)(i0 * 4) : (uint32_t)(((i0 >> 6) * 128 + ((i0 >> 5) & 1)) * 4);
+            const bool ok = w < 2 || (DROP && i0 < S);
+            dma4(rpc, smem + (w < 2 ? O_L + (buf * 2 + w) * 256 : O_D + buf * KB * 4 + (w - 2) * 256),
+                 ok ? pc_lane + sc : OOB);
         } else {
             const int k = p - 5, c = T + 4, r0 = rw0 + 128 - 32 * c;
             dma16(rr, sR + (c % NCH) * TILE + w * 2048 + k * 1024, offR[k] + (uint32_t)(r0 * HS * 2));
@@ -265,84 +310,113 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
     // wave issues exactly NST stores per iteration.
     const uint32_t ds_bytes = (uint32_t)min<int64_t>((int64_t)S * ldr * 2, OOB - 1);
     const int ldr2 = (int)(ldr * 2);
-    auto store_piece = [&](int k, int ip, int sbuf, bool valid) {
+    // per-lane parts of the two pieces' offsets (row = t/16 + 16 k, 8 keys
+    // from j0 + 8 (t & 15)); i = ip + row adds ip (ldr2 - 2) resp. ip ldr2
+    uint32_t st_r[2], st_j[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int row = (tid >> 4) + 16 * k, j = j0 + 8 * (tid & 15);
+        st_r[k] = (uint32_t)(row * (ldr2 - 2) + 2 * (S - 1 + j));
+        st_j[k] = (uint32_t)(row * ldr2 + 2 * j);
+    }
+    auto store_read = [&](int k, int sbuf) {
+        const int row = (ltid >> 4) + 16 * k, ch = ltid & 15;
+        return *(const u32x4*)(smem + O_T + sbuf * T_BYTES + row * T_PITCH + ch * 16);
+    };
+    auto store_piece = [&](int k, const u32x4& v, int ip, bool valid) {
         // descriptors rebuilt per use from readfirstlane'd halves (kept live
         // across the loop they would sit in VGPRs: a waterfall loop per store)
-        const int row = (ltid >> 4) + 16 * k, ch = ltid & 15;
-        const u32x4 v = *(const u32x4*)(smem + O_T + sbuf * T_BYTES + row * T_PITCH + ch * 16);
-        const int i = ip + row, j = j0 + 8 * ch;
-        const bool in = valid;  // rows past the sequence end: past num_records
-        // 32-bit offsets (S * ldr * 2 < 4 GB, checked at launch)
-        const uint32_t rowb = (uint32_t)i * (uint32_t)ldr2;
+        // 32-bit offsets (S * ldr * 2 < 4 GB, checked at launch); rows past the
+        // sequence end fall past num_records
         const __amdgpu_buffer_rsrc_t rqr = make_rsrc(qr_rows, ds_bytes);
-        __builtin_amdgcn_raw_buffer_store_b128(v, rqr, in ? rowb + (uint32_t)(S - 1 - i + j) * 2u : OOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rqr, valid ? st_r[k] + (uint32_t)ip * (uint32_t)(ldr2 - 2) : OOB, 0, 0);
         const __amdgpu_buffer_rsrc_t rsj = make_rsrc(sj_rows, ds_bytes);
-        __builtin_amdgcn_raw_buffer_store_b128(v, rsj, in ? rowb + (uint32_t)j * 2u : OOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rsj, valid ? st_j[k] + (uint32_t)ip * (uint32_t)ldr2 : OOB, 0, 0);
     };
 
     // skew: register e of lane c32 takes the window value from lane
     // (c32 - row(e) - 1) mod 32 of the same half; the source selects block 0
-    // when c32 + row(e) >= 31 (z = c32 + 4 hh against 31 - (e&3) - 8 (e>>2))
+    // when c32 + row(e) >= 31 (z = c32 + 4 hh against 31 - (e&3) - 8 (e>>2)).
+    // Both are lane constants per e: the select mask and the bpermute address
+    // are computed once (32 VGPRs; per tile they cost 3 VALU per register)
+    uint32_t skm[16];
+    int ska[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int k = (e & 3) + 8 * (e >> 2);
+        skm[e] = (c32 + 4 * hh >= 31 - k) ? 0xffffffffu : 0u;
+        ska[e] = ((((c32 - 4 * hh - 1) * 4) - 4 * k) & 124) | (hh << 7);
+        // opaque: known 0 / -1 lane masks the compiler keeps as 16 SGPR pairs
+        // for v_cndmask, and the SGPR file then spills into VGPR lanes
+        pin(skm[e]);
+    }
 
     // pipeline state carried between iterations: one set of accumulators
     // (VGPRs; the AGPRs hold dK^T / dV^T and K / V) and the skewed relative
     // term bp of the tile the next iteration's softmax reads
     Acc acc;
-    float bp[16];            // raw window values (the mask applies in stage a)
-    f32x4 Lr[4], Dr[4];      // row constants of the carried tile: lse log2(e), D scale
-    uint32_t vm = 0u, mk = 0u;  // its causal / sequence-end mask and dropout keep word
+    float bp[16];               // raw window values (the causal mask applies in stage a)
+    f32x4 Dr[4];                // -D/ks of the carried tile's rows (the dropped entries' dP')
+    uint32_t vm = 0u, mk = 0u;  // its causal mask (tiles 0..3) and dropout keep word
 
-    // ---- skew of tile T (its q0 / q1 final, >= 16 MFMAs old) into bp, and
-    // the tile's row constants and masks, all for the NEXT iteration's
-    // softmax: nothing here is read before that iteration's barrier, whose
-    // lgkmcnt(0) retires these LDS reads (the bpermute is an asm statement so
-    // the compiler places no wait behind it; its float-typed result also keeps
-    // the carried value out of an i32 loop phi, which made the allocator move
-    // ~100 values into the AGPR file and spill)
-    int sk_z = 0, sk_bpb = 0;
+    // ---- per-tile constants of tile T for the NEXT iteration's softmax
+    // (nothing here is read before that iteration's barrier, whose lgkmcnt(0)
+    // retires these LDS reads; the bpermute is an asm statement so the
+    // compiler places no wait behind it)
     auto skew_setup = [&](int T) {
         const int i0 = it0 + QT * T, buf = T % NB;
-        // per-tile lane constants made opaque (hoisted, the 16 masks and 16
-        // addresses would pin registers for the whole kernel)
-        sk_z = lz0;
-        sk_bpb = lbpb0;
-        asm volatile("" : "+v"(sk_z), "+v"(sk_bpb));
-        // rows k + 4hh valid: jk <= i0 + k + 4hh <= S - 1 (all ones in full
-        // tiles); the metadata tile's j > i entries are left to
-        // flash_bwd_meta5_kernel
-        const int lo = ljk - i0 - 4 * lhh, hi = S - 1 - i0 - 4 * lhh;
-        const uint32_t up = hi >= 31 ? 0xffffffffu : (hi < 0 ? 0u : (2u << hi) - 1u);
-        const uint32_t dn = lo <= 0 ? 0xffffffffu : (lo >= 32 ? 0u : (0xffffffffu << lo));
-        vm = up & dn;
-        const float* cL = (const float*)(smem + O_L + buf * 512);
+        // rows k + 4hh valid: jk <= i0 + k + 4hh. Only the first four tiles
+        // meet the diagonal (t >= 4: every key of the block is below i0); rows
+        // past the sequence end need no mask (their Q, dO and row constants read
+        // as zeros, so P ks scale = ks scale and dP' = 0: no dV, dK or dS);
+        // the metadata tile's j > i entries are left to flash_bwd_meta5_kernel
+        const int lo = ljk - i0 - 4 * lhh;
+        vm = lo <= 0 ? 0xffffffffu : (lo >= 32 ? 0u : (0xffffffffu << lo));
+        if (DROP) {
+            const float* cL = (const float*)(smem + O_L + buf * 512);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            Lr[g] = *(const f32x4*)(cL + 8 * g + 4 * lhh);
-            Dr[g] = *(const f32x4*)(cL + 64 + 8 * g + 4 * lhh);
+            for (int g = 0; g < 4; ++g) Dr[g] = *(const f32x4*)(cL + 64 + 8 * g + 4 * lhh);
+            // keep word of this lane's key over the tile's 32 queries; bit k of
+            // mk = query row k + 4 hh
+            mk = ((const uint32_t*)(smem + O_D + buf * KB * 4))[32 * w + lc32] >> (4 * lhh);
         }
-        // keep word of this lane's key over the tile's 32 queries; bit k of
-        // mk = query row k + 4 hh
-        if (DROP) mk = ((const uint32_t*)(smem + O_D + buf * KB * 4))[32 * w + lc32] >> (4 * lhh);
     };
     auto skew = [&](auto E) {
-        constexpr int e = decltype(E)::value, k = (e & 3) + 8 * (e >> 2);
-        const float sel = (sk_z >= 31 - k) ? acc.q0[e] : acc.q1[e];
-        const int adr = ((sk_bpb - 4 * k) & 124) | lhh7;
+        constexpr int e = decltype(E)::value;
+        float x0 = acc.q0[e], x1 = acc.q1[e];
+        pin(x0);
+        pin(x1);
+        const float sel = __uint_as_float((__float_as_uint(x0) & skm[e]) | (__float_as_uint(x1) & ~skm[e]));
         float r;
-        asm volatile("ds_bpermute_b32 %0, %1, %2" : "=v"(r) : "v"(adr), "v"(sel));
+#ifndef KV_ABL_NOSKEW
+        asm volatile("ds_bpermute_b32 %0, %1, %2" : "=v"(r) : "v"(ska[e]), "v"(sel));
+#else
+        r = sel;
+#endif
         bp[e] = r;
     };
+    // row constants of tile T as the initial accumulators (register e = row
+    // acc_row(e, hh))
+    auto row_consts = [&](int T, int which) {
+        const float* cL = (const float*)(smem + O_L + (T % NB) * 512) + 64 * which;
+        f32x4 v[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) v[g] = *(const f32x4*)(cL + 8 * g + 4 * lhh);
+        return cat16(v);
+    };
 
-    // ---- one iteration (t): with DO_A, A(t+1) runs beside it.
+    // ---- one iteration (t): with DO_A, A(t+1) runs beside it; MASK: tile t
+    // is one of the first four (the causal diagonal crosses it).
     //  phase 1 (16 MFMAs: QR window of t+1 into q0 / q1) | softmax stage a of
-    //           tile t (p from s + bp), the staging DMA of tile t+1+DEPTH,
-    //           the dS(t-1) row stores
-    //  phase 2 (16 MFMAs: S of t+1, then dP of t+1, into the registers tile
-    //           t's s / dp just left) | softmax stage b (dS from dp), dS(t)
-    //           staging writes
+    //           tile t (p from s' + bp), the staging DMA of tile t+1+DEPTH,
+    //           the dS(t-1) row stores, tile t+1's -lse/scale
+    //  phase 2 (16 MFMAs: S' of t+1 from -lse/scale, then dP' of t+1 from
+    //           -D/ks, into the registers tile t's s / dp just left) | softmax
+    //           stage b (dS from dp'), dS(t) staging writes
     //  phase 3 (16 MFMAs: C(t) = dV / dK of tile t) | skew of tile t+1
-    auto iter = [&](auto DOA, int t) {
+    auto iter = [&](auto DOA, auto MSK, int t) {
         constexpr bool DO_A = decltype(DOA)::value;
+        constexpr bool MASK = decltype(MSK)::value;
         const int i0 = it0 + QT * t, buf = t % NB, sb = t & 1, T = t + 1;
         // the lane constants are re-declared opaque every iteration: the
         // unrolled gaps derive dozens of per-lane addresses from them, and
@@ -351,28 +425,60 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
                      "+v"(offR[0]), "+v"(offR[1]));
         asm volatile("" : "+v"(rof[0]), "+v"(rof[1]), "+v"(tb[0]), "+v"(tb[1]), "+v"(ltid), "+v"(ljk), "+v"(lhh),
                      "+v"(lc32));
-        asm volatile("" : "+v"(lhh7), "+v"(lz0), "+v"(lbpb0));
         // tile t+1's data: issued DEPTH iterations ago
+#ifndef KV_ABL_NODMA
         if (t >= DEPTH) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST + (NDMA + NST) * (DEPTH - 1)) : "memory");
+#endif
+#ifndef KV_ABL_NOBAR
         bar();  // tile t+1 landed everywhere; tile t-1's buffers and dS(t-1) staging published
-        float pv[16];
-        bf16x8 pa[2], da[2];
-        // stage a: p = exp2((s + bp) c2 - lse log2e), bp = -inf where masked
-        // (v_bfi); the dropped P for dV
+#else
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+        float pv[16], dsv[16];
+        uint32_t pw[8], dw[8];  // bf16 pairs (rows e, e+1 of the lane's key) of P and dS
+        // stage a: P ks scale = exp2(c2 (s' + bp) + lks), -inf where masked;
+        // the dropped P for dV in bf16 pairs
         auto stage_a = [&](auto E) {
             constexpr int e = decltype(E)::value, k = (e & 3) + 8 * (e >> 2);
-            const int m = __builtin_amdgcn_sbfe((int)vm, k, 1);
-            const float b = __int_as_float((__float_as_int(bp[e]) & m) | ((int)0xff800000 & ~m));
-            const float p = __builtin_amdgcn_exp2f(fmaf(acc.s[e] + b, c2, -Lr[e >> 2][e & 3]));
+            float sv = acc.s[e], bv = bp[e];
+            pin(sv);
+            pin(bv);
+            float x = sv + bv;
+            if (MASK) {
+                const int m = __builtin_amdgcn_sbfe((int)vm, k, 1);
+                x = __int_as_float((__float_as_int(x) & m) | ((int)0xff800000 & ~m));
+            }
+            float p = __builtin_amdgcn_exp2f(fmaf(x, c2, lks));
+            pin(p);
             pv[e] = p;
-            pa[e >> 3][e & 7] = (bf16)(DROP ? and_f(p, __builtin_amdgcn_sbfe((int)mk, k, 1)) : p);
+            if constexpr ((e & 1) == 1) {
+                float p0 = pv[e - 1], p1 = p;
+                if (DROP) {
+                    p0 = and_f(p0, __builtin_amdgcn_sbfe((int)mk, k - 1, 1));
+                    p1 = and_f(p1, __builtin_amdgcn_sbfe((int)mk, k, 1));
+                }
+                uint32_t wv = pack2(p0, p1);
+                pin(wv);
+                pw[e >> 1] = wv;
+            }
         };
-        // stage b: dS = p fma(dP m, ks scale, -D scale)
+        // stage b: dS = (P ks scale) (m ? dP' : -D/ks), bf16 pairs
         auto stage_b = [&](auto E) {
             constexpr int e = decltype(E)::value, k = (e & 3) + 8 * (e >> 2);
             float dpv = acc.dp[e];
-            if (DROP) dpv = and_f(dpv, __builtin_amdgcn_sbfe((int)mk, k, 1));
-            da[e >> 3][e & 7] = (bf16)(pv[e] * fmaf(dpv, ks_scale, -Dr[e >> 2][e & 3]));
+            pin(dpv);
+            if (DROP) {
+                const int m = __builtin_amdgcn_sbfe((int)mk, k, 1);
+                dpv = __int_as_float((__float_as_int(dpv) & m) | (__float_as_int(Dr[e >> 2][e & 3]) & ~m));
+            }
+            float ds = pv[e] * dpv;
+            pin(ds);
+            dsv[e] = ds;
+            if constexpr ((e & 1) == 1) {
+                uint32_t wv = pack2(dsv[e - 1], ds);
+                pin(wv);
+                dw[e >> 1] = wv;
+            }
         };
         const char* cQn = smem + O_Q + (T % NB) * TILE;
         const char* cOn = smem + O_O + (T % NB) * TILE;
@@ -385,6 +491,14 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
             fx[n] = *(const bf16x8*)(rb0 + off);
             fy[n] = *(const bf16x8*)(rb1 + off);
         };
+        // phase 2's fragments, three ahead (the first three from phase 1's end)
+        bf16x8 fa[4];
+        auto lds1 = [&](int g) {
+            const int ks = g & 7, off = rof[ks & 1] + 1024 * ks;
+            fa[g & 3] = *(const bf16x8*)((g < 8 ? cQn : cOn) + off);
+        };
+        f32x16 Lrow, Drow;
+        u32x4 stv[2];  // dS(t-1) staging rows for the row stores
         // ---- phase 1
         if (DO_A) ldqr(0, 0);
         static_for<16>([&](auto G) {
@@ -398,51 +512,54 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
                     if (ks == 0) mfma_first_vv(acc.q1, fq[c], fy[c]);
                     else mfma_acc_vv(acc.q1, fq[c], fy[c]);
                 }
+                if constexpr (g == 11) Lrow = row_consts(T, 0);
+                if constexpr (g >= 13) lds1(g - 13);
             }
+#ifndef KV_ABL_NODMA
             if constexpr (g < NDMA) dma_piece(g, t + 1 + DEPTH);
-            if constexpr (g == NDMA || g == NDMA + 1) store_piece(g - NDMA, i0 - QT, sb ^ 1, t >= 1);
+#endif
+#ifndef KV_ABL_NOSTORE
+            if constexpr (g == 1 || g == 2) stv[g - 1] = store_read(g - 1, sb ^ 1);
+            if constexpr (g == NDMA || g == NDMA + 1) store_piece(g - NDMA, stv[g - NDMA], i0 - QT, t >= 1);
+#endif
             if constexpr (g >= 2) stage_a(std::integral_constant<int, g - 2>{});
             if constexpr (g >= 14) stage_a(std::integral_constant<int, g>{});
             if constexpr (g >= 6) stage_b(std::integral_constant<int, g - 6>{});
             SB();
         });
-        // ---- phase 2: S chain (tile t's s is dead), then dP chain (its dp
-        // dies at the stage b of gap 7)
-        bf16x8 fa[2];
-        auto lds1 = [&](int ks, int n, bool q) {
-            const int off = rof[ks & 1] + 1024 * ks;
-            fa[n] = *(const bf16x8*)((q ? cQn : cOn) + off);
-        };
+        // ---- phase 2: S' chain (tile t's s is dead), then dP' chain (its dp
+        // dies at the stage b of gap 5)
         char* st = smem + O_T + sb * T_BYTES + 4 * lhh * T_PITCH + (32 * w + lc32) * 2;
-        if (DO_A) lds1(0, 0, true);
+        const char* cQ = smem + O_Q + buf * TILE;
+        const char* cO = smem + O_O + buf * TILE;
+        bf16x8 fo[2], fqq[2];
         static_for<16>([&](auto G) {
-            constexpr int g = decltype(G)::value, ks = g & 7, c = g & 1;
+            constexpr int g = decltype(G)::value, ks = g & 7;
             if (DO_A) {
-                if (g + 1 < 16) lds1((g + 1) & 7, c ^ 1, g + 1 < 8);
-                if (g < 8) {
-                    if (ks == 0) mfma_first_va(acc.s, fa[c], kf[ks]);
-                    else mfma_acc_va(acc.s, fa[c], kf[ks]);
-                } else {
-                    if (ks == 0) mfma_first_va(acc.dp, fa[c], vf[ks]);
-                    else mfma_acc_va(acc.dp, fa[c], vf[ks]);
-                }
+                if constexpr (g + 3 < 16) lds1(g + 3);
+                if constexpr (g == 2) Drow = row_consts(T, 1);
+                if constexpr (g == 0) mfma_init_va(acc.s, fa[g & 3], kf[ks], Lrow);
+                else if constexpr (g < 8) mfma_acc_va(acc.s, fa[g & 3], kf[ks]);
+                else if constexpr (g == 8) mfma_init_va(acc.dp, fa[g & 3], vf[ks], Drow);
+                else mfma_acc_va(acc.dp, fa[g & 3], vf[ks]);
             }
             if constexpr (g < 6) stage_b(std::integral_constant<int, 10 + g>{});
             if constexpr (g >= 8) {  // dS(t) staging for the next iteration's row stores
-                constexpr int e0 = 2 * (g - 8);
-                *(bf16*)(st + acc_row(e0, 0) * T_PITCH) = da[e0 >> 3][e0 & 7];
-                *(bf16*)(st + acc_row(e0 + 1, 0) * T_PITCH) = da[(e0 + 1) >> 3][(e0 + 1) & 7];
+                constexpr int u = g - 8, e0 = 2 * u;
+                *(uint16_t*)(st + acc_row(e0, 0) * T_PITCH) = (uint16_t)(dw[u] & 0xffffu);
+                *(uint16_t*)(st + acc_row(e0 + 1, 0) * T_PITCH) = (uint16_t)(dw[u] >> 16);
+            }
+            if constexpr (g == 14) {
+                fo[0] = tr_frag(cO, 0, 0);
+                fqq[0] = tr_frag(cQ, 0, 0);
             }
             SB();
         });
         // ---- phase 3: C(t): dV^T[d][j] += dO^T[d][i] P[i][j], dK^T[d][j] +=
         // Q^T[d][i] dS[i][j] (16 MFMAs) | skew of tile t+1
-        const char* cQ = smem + O_Q + buf * TILE;
-        const char* cO = smem + O_O + buf * TILE;
-        bf16x8 fo[2], fqq[2];
-        fo[0] = tr_frag(cO, 0, 0);
-        fqq[0] = tr_frag(cQ, 0, 0);
         if (DO_A) skew_setup(T);
+        const bf16x8 pa[2] = {words8(pw[0], pw[1], pw[2], pw[3]), words8(pw[4], pw[5], pw[6], pw[7])};
+        const bf16x8 da[2] = {words8(dw[0], dw[1], dw[2], dw[3]), words8(dw[4], dw[5], dw[6], dw[7])};
         static_for<16>([&](auto G) {
             constexpr int g = decltype(G)::value, n = g >> 1, c = n & 1, db = n >> 1, s2 = n & 1;
             if ((g & 1) == 0) {
@@ -481,6 +598,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
         const char* cO = smem + O_O;
         const char* rb0 = sR + ((4 - w) % NCH) * TILE;
         const char* rb1 = sR + ((3 - w) % NCH) * TILE;
+        const f32x16 L0 = row_consts(0, 0), D0 = row_consts(0, 1);
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) {
             const int off = rof[ks & 1] + 1024 * ks;
@@ -489,8 +607,8 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
             if (ks == 0) {
                 mfma_first_vv(acc.q0, fq, fx);
                 mfma_first_vv(acc.q1, fq, fy);
-                mfma_first_va(acc.s, fq, kf[0]);
-                mfma_first_va(acc.dp, fo, vf[0]);
+                mfma_init_va(acc.s, fq, kf[0], L0);
+                mfma_init_va(acc.dp, fo, vf[0], D0);
             } else {
                 mfma_acc_vv(acc.q0, fq, fx);
                 mfma_acc_vv(acc.q1, fq, fy);
@@ -505,20 +623,25 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
         skew_setup(0);
         static_for<16>([&](auto E) { skew(E); });
     }
-    for (int t = 0; t + 1 < nqt; ++t) iter(std::true_type{}, t);
-    iter(std::false_type{}, nqt - 1);
+    // tiles 0..3 cross the causal diagonal (masked softmax), the rest do not
+    int t = 0;
+    for (; t + 1 < nqt && t < 4; ++t) iter(std::true_type{}, std::true_type{}, t);
+    for (; t + 1 < nqt; ++t) iter(std::true_type{}, std::false_type{}, t);
+    if (nqt - 1 < 4) iter(std::false_type{}, std::true_type{}, nqt - 1);
+    else iter(std::false_type{}, std::false_type{}, nqt - 1);
     // the last tile's dS rows
     bar();
 #pragma unroll
-    for (int k = 0; k < 2; ++k) store_piece(k, it0 + QT * (nqt - 1), (nqt - 1) & 1, true);
+    for (int k = 0; k < 2; ++k) store_piece(k, store_read(k, (nqt - 1) & 1), it0 + QT * (nqt - 1), true);
     // the staging DMA issued for tiles past the end (zero-filled) lands before
     // the workgroup gives its LDS back
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    // lane holds dK^T / dV^T [d = 32 db + acc_row(e)][key c32]
+    // lane holds dK^T / dV^T [d = 32 db + acc_row(e)][key c32]; dV was
+    // accumulated from P ks scale: dV = acc / scale
     drain_a(dk, dv);
     if (jk < S) {
-        const float vs = DROP ? a.keep_scale : 1.f;
+        const float vs = 1.f / a.scale;
         bf16* dkp = dqkv + ((int64_t)b * S + jk) * ldd + (H + h) * HS;
         bf16* dvp = dkp + H * HS;
 #pragma unroll
@@ -535,7 +658,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
 
 }  // namespace
 
-int flash_bwd_kv5(const AttnArgs& a, const float* lse, const float* Dv, const bf16* dout, int64_t ldo, bf16* dqkv,
+int flash_bwd_kv5(const AttnArgs& a, const float* nls, const float* ndk, const bf16* dout, int64_t ldo, bf16* dqkv,
                   int64_t ldd, bf16* dqr, bf16* dsj, int64_t ldr, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
@@ -552,10 +675,10 @@ int flash_bwd_kv5(const AttnArgs& a, const float* lse, const float* Dv, const bf
     if (ldr < a.S + 128 || !dsj) return -1;
     const dim3 grid((unsigned)((a.S + KB - 1) / KB), (unsigned)a.H, (unsigned)a.B);
     if (a.colmask)
-        hipLaunchKernelGGL((flash_bwd_kv5_kernel<true>), grid, dim3(NT), LDS_BYTES, s, a, lse, Dv, dout, ldo, dqkv, ldd,
+        hipLaunchKernelGGL((flash_bwd_kv5_kernel<true>), grid, dim3(NT), LDS_BYTES, s, a, nls, ndk, dout, ldo, dqkv, ldd,
                            dqr, dsj, ldr);
     else
-        hipLaunchKernelGGL((flash_bwd_kv5_kernel<false>), grid, dim3(NT), LDS_BYTES, s, a, lse, Dv, dout, ldo, dqkv,
+        hipLaunchKernelGGL((flash_bwd_kv5_kernel<false>), grid, dim3(NT), LDS_BYTES, s, a, nls, ndk, dout, ldo, dqkv,
                            ldd, dqr, dsj, ldr);
     return 0;
 }

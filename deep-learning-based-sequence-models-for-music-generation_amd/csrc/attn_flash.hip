@@ -1,7 +1,8 @@
 // Relative-position flash attention backward, bf16 MFMA path (hs = 128):
 // the host side of the pass sequence and its small kernels
 // (model_transformer.py:54-90 differentiated):
-//   pre : D_i = sum_d dO.O (and the v5 row constants lse log2(e), D scale)
+//   pre : D_i = sum_d dO.O (and the key/value pass's row constants -lse/scale,
+//         -D/ks: the initial accumulators of its S and dP chains)
 //   kv  : per 128-key block (attn_bwd5.hip): recompute S, P; dP = dO.V^T;
 //         dS = P (dP - D) scale; dK, dV accumulated in registers; dS written
 //         once, r-indexed: dQR[h][b][i][r = S-1-i+j];
@@ -22,13 +23,15 @@ constexpr int NT = 256;
 // ------------------------------------------------------------ backward: pre
 // D[b,h,i] = sum_d dO[i,d] O[i,d]
 // same, 16 lanes x 8 elements (one 16-B load of dO and of O each) per
-// (row, head): 4 head-rows per wave; also the key/value pass v5's row
-// constants l2 = lse * log2(e) and dsc = D * scale
+// (row, head): 4 head-rows per wave; also the key/value pass's row
+// constants nls = -lse / scale and ndk = -D / ks (ks = 1/(1-p) with dropout,
+// else 1): the initial values of its S and dP accumulators, so that
+// P = exp2(scale log2(e) (S + R term)) and dS = P ks scale (dP - D/ks)
 __global__ __launch_bounds__(256) void flash_bwd_pre_vec_kernel(AttnArgs a, const bf16* __restrict__ dout,
                                                                 int64_t ldo, const bf16* __restrict__ out,
                                                                 const float* __restrict__ lse,
-                                                                float* __restrict__ Dv, float* __restrict__ l2,
-                                                                float* __restrict__ dsc) {
+                                                                float* __restrict__ Dv, float* __restrict__ nls,
+                                                                float* __restrict__ ndk) {
     const int64_t row = blockIdx.x * 16LL + (threadIdx.x >> 4);  // over B*S*H
     const int l = threadIdx.x & 15;
     const bool ok = row < a.B * a.S * a.H;
@@ -44,8 +47,8 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_vec_kernel(AttnArgs a, cons
     if (ok && l == 0) {
         const int64_t b = bi / a.S, i = bi % a.S, k = (b * a.H + h) * a.S + i;
         Dv[k] = s;
-        dsc[k] = s * a.scale;
-        l2[k] = lse[k] * LOG2E;
+        ndk[k] = -s / (a.colmask ? a.keep_scale : 1.f);
+        nls[k] = -lse[k] / a.scale;
     }
 }
 
@@ -181,7 +184,7 @@ int64_t flash_dqr_ld(int64_t S) { return (S + 200 + 7) / 8 * 8; }
 
 // workspace: dQR bf16 [H][B][S][ldr] | dSj bf16 [H][B][S][ldr] | D f32 [B][H][S]
 //            | dR split-K partials f32 [ksplit][H][S][HS]
-//            | l2 f32 [B][H][S] | dsc f32 [B][H][S] | mdr f32 [B][H][8][HS]
+//            | nls f32 [B][H][S] | ndk f32 [B][H][S] | mdr f32 [B][H][8][HS]
 static size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 static size_t dr_ws_bytes(int64_t B, int64_t S, int64_t H) {
     return splitk_ws_bytes(S, HS, H, gemm_bf16_tri_ksplit(2, S, HS, B * S, S, H));
@@ -206,9 +209,9 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     p += align256((size_t)B * H * S * 4);
     float* dr_ws = (float*)p;
     p += align256(dr_ws_bytes(B, S, H));
-    float* l2 = (float*)p;
+    float* nls = (float*)p;
     p += align256((size_t)B * H * S * 4);
-    float* dsc = (float*)p;
+    float* ndk = (float*)p;
     p += align256((size_t)B * H * S * 4);
     float* mdr = (float*)p;  // the metadata block's dR rows per (b, h)
 
@@ -221,10 +224,10 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     if (ldo % 8 || ((uintptr_t)dout % 16) || ((uintptr_t)out % 16))
         return msq_set_error(MSQ_ERR_ARG, "flash_bwd: dout / out need 16-B aligned rows");
     hipLaunchKernelGGL(flash_bwd_pre_vec_kernel, dim3((unsigned)((B * S * H + 15) / 16)), dim3(256), 0, s, a, dout, ldo,
-                       out, lse, Dv, l2, dsc);
+                       out, lse, Dv, nls, ndk);
     // key/value pass v5: dK, dV, and dS in both layouts (dQR r-indexed, dSj
     // j-indexed; storing it once measured slower overall)
-    if (flash_bwd_kv5(a, l2, dsc, dout, ldo, dqkv, ldd, dqr, dsj, ldr, s))
+    if (flash_bwd_kv5(a, nls, ndk, dout, ldo, dqkv, ldd, dqr, dsj, ldr, s))
         return msq_set_error(MSQ_ERR_UNSUPPORTED, "flash_bwd: shape outside the key/value pass (n_meta > 8 or > 4 GB)");
     // dq (bf16, q columns of dqkv) = dSj . K + dQR . R
     flash_bwd_dq(a, dsj, dqr, ldr, dqkv, ldd, s);
