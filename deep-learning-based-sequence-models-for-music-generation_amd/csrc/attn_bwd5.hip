@@ -58,6 +58,12 @@ constexpr int LDS_BYTES = O_T + 2 * T_BYTES;
 // R 2), then the dS row stores (2, or 4 with the j-indexed copy)
 constexpr int NDMA = 7;
 constexpr uint32_t OOB = 0xFFFF0000u;
+#ifndef KV_STORE_AUX
+// cache policy of the dS row stores: nt (2.16 GB per layer streamed through
+// L2 evicted the staging reads' lines): kv 1578 -> 1498 us, and the dq pass
+// that reads them back 795 -> 763 us (same box)
+#define KV_STORE_AUX 2
+#endif
 static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 
 template <typename F, int... I>
@@ -329,9 +335,15 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
         // 32-bit offsets (S * ldr * 2 < 4 GB, checked at launch); rows past the
         // sequence end fall past num_records
         const __amdgpu_buffer_rsrc_t rqr = make_rsrc(qr_rows, ds_bytes);
-        __builtin_amdgcn_raw_buffer_store_b128(v, rqr, valid ? st_r[k] + (uint32_t)ip * (uint32_t)(ldr2 - 2) : OOB, 0, 0);
+#if defined(KV_ABL_ALIGNR)
+        __builtin_amdgcn_raw_buffer_store_b128(v, rqr, valid ? st_j[k] + (uint32_t)ip * (uint32_t)ldr2 : OOB, 0, 0);
+#elif !defined(KV_ABL_NOSTORE_R)
+        __builtin_amdgcn_raw_buffer_store_b128(v, rqr, valid ? st_r[k] + (uint32_t)ip * (uint32_t)(ldr2 - 2) : OOB, 0,
+                                               KV_STORE_AUX);
+#endif
         const __amdgpu_buffer_rsrc_t rsj = make_rsrc(sj_rows, ds_bytes);
-        __builtin_amdgcn_raw_buffer_store_b128(v, rsj, valid ? st_j[k] + (uint32_t)ip * (uint32_t)ldr2 : OOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rsj, valid ? st_j[k] + (uint32_t)ip * (uint32_t)ldr2 : OOB, 0,
+                                               KV_STORE_AUX);
     };
 
     // skew: register e of lane c32 takes the window value from lane
@@ -484,7 +496,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
         const char* cOn = smem + O_O + (T % NB) * TILE;
         const char* rb0 = sR + ((T + 4 - w) % NCH) * TILE;
         const char* rb1 = sR + ((T + 3 - w) % NCH) * TILE;
-        bf16x8 fq[2], fx[2], fy[2];
+        bf16x8 fq[3], fx[3], fy[3];  // two k-steps ahead
         auto ldqr = [&](int ks, int n) {
             const int off = rof[ks & 1] + 1024 * ks;
             fq[n] = *(const bf16x8*)(cQn + off);
@@ -500,12 +512,15 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
         f32x16 Lrow, Drow;
         u32x4 stv[2];  // dS(t-1) staging rows for the row stores
         // ---- phase 1
-        if (DO_A) ldqr(0, 0);
+        if (DO_A) {
+            ldqr(0, 0);
+            ldqr(1, 1);
+        }
         static_for<16>([&](auto G) {
-            constexpr int g = decltype(G)::value, ks = g >> 1, c = ks & 1;
+            constexpr int g = decltype(G)::value, ks = g >> 1, c = ks % 3;
             if (DO_A) {
                 if ((g & 1) == 0) {
-                    if (ks + 1 < 8) ldqr(ks + 1, c ^ 1);
+                    if (ks + 2 < 8) ldqr(ks + 2, (ks + 2) % 3);
                     if (ks == 0) mfma_first_vv(acc.q0, fq[c], fx[c]);
                     else mfma_acc_vv(acc.q0, fq[c], fx[c]);
                 } else {
@@ -532,7 +547,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
         char* st = smem + O_T + sb * T_BYTES + 4 * lhh * T_PITCH + (32 * w + lc32) * 2;
         const char* cQ = smem + O_Q + buf * TILE;
         const char* cO = smem + O_O + buf * TILE;
-        bf16x8 fo[2], fqq[2];
+        bf16x8 fo[3], fqq[3];  // two MFMA pairs ahead
         static_for<16>([&](auto G) {
             constexpr int g = decltype(G)::value, ks = g & 7;
             if (DO_A) {
@@ -553,6 +568,10 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
                 fo[0] = tr_frag(cO, 0, 0);
                 fqq[0] = tr_frag(cQ, 0, 0);
             }
+            if constexpr (g == 15) {
+                fo[1] = tr_frag(cO, 1, 0);
+                fqq[1] = tr_frag(cQ, 1, 0);
+            }
             SB();
         });
         // ---- phase 3: C(t): dV^T[d][j] += dO^T[d][i] P[i][j], dK^T[d][j] +=
@@ -561,11 +580,11 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
         const bf16x8 pa[2] = {words8(pw[0], pw[1], pw[2], pw[3]), words8(pw[4], pw[5], pw[6], pw[7])};
         const bf16x8 da[2] = {words8(dw[0], dw[1], dw[2], dw[3]), words8(dw[4], dw[5], dw[6], dw[7])};
         static_for<16>([&](auto G) {
-            constexpr int g = decltype(G)::value, n = g >> 1, c = n & 1, db = n >> 1, s2 = n & 1;
+            constexpr int g = decltype(G)::value, n = g >> 1, c = n % 3, db = n >> 1, s2 = n & 1;
             if ((g & 1) == 0) {
-                if (n + 1 < 8) {
-                    fo[c ^ 1] = tr_frag(cO, (n + 1) & 1, (n + 1) >> 1);
-                    fqq[c ^ 1] = tr_frag(cQ, (n + 1) & 1, (n + 1) >> 1);
+                if (n + 2 < 8) {
+                    fo[(n + 2) % 3] = tr_frag(cO, (n + 2) & 1, (n + 2) >> 1);
+                    fqq[(n + 2) % 3] = tr_frag(cQ, (n + 2) & 1, (n + 2) >> 1);
                 }
                 mfma_acc_a(dv[db], fo[c], pa[s2]);
             } else {
