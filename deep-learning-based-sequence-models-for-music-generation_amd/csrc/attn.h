@@ -44,13 +44,12 @@ int exact_bwd(const AttnArgs& a, const float* lse, const float* dout, int64_t ld
 // bf16 flash path (attn_flash.hip), hs == 128
 int64_t flash_dqr_ld(int64_t S);
 size_t flash_bwd_workspace(int64_t B, int64_t S, int64_t H);
-// v5 key/value pass (attn_bwd5.hip): dS to dqr (r-indexed) and dsj
-// (j-indexed), both [H][B][S][ldr]; -1 if unsupported
-int flash_bwd_kv5(const AttnArgs& a, const float* lse, const float* Dv, const bf16* dout, int64_t ldo, bf16* dqkv,
-                  int64_t ldd, bf16* dqr, bf16* dsj, int64_t ldr, hipStream_t s);
-// dq = dSj.K + dQR.R into the q columns of dqkv (attn_dq.hip)
-void flash_bwd_dq(const AttnArgs& a, const bf16* dsj, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd,
-                  hipStream_t s);
+// v5 key/value pass (attn_bwd5.hip): dS once, r-indexed, into dqr
+// [H][B][S][ldr] (its j-view: row pitch ldr - 1 from element S - 1); -1 if unsupported
+int flash_bwd_kv5(const AttnArgs& a, const float* nls, const float* ndk, const bf16* dout, int64_t ldo, bf16* dqkv,
+                  int64_t ldd, bf16* dqr, int64_t ldr, hipStream_t s);
+// dq = dS.K (dQR's j-view) + dQR.R into the q columns of dqkv (attn_dq.hip)
+void flash_bwd_dq(const AttnArgs& a, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd, hipStream_t s);
 // v3 forward (attn_fwd3.hip): 8 waves x 32 queries, 32-key tiles; -1 if unsupported
 int flash_fwd3(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s);
 int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo, const bf16* out, bf16* dqkv,

@@ -173,10 +173,9 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
                                                               const float* __restrict__ ndk,
                                                               const bf16* __restrict__ dout, int64_t ldo,
                                                               bf16* __restrict__ dqkv, int64_t ldd,
-                                                              bf16* __restrict__ dqr, bf16* __restrict__ dsj,
-                                                              int64_t ldr) {
+                                                              bf16* __restrict__ dqr, int64_t ldr) {
 #ifndef KV_ABL_NOSTORE
-    constexpr int NST = 4;  // dS row stores per wave and iteration (2 r-indexed, 2 j-indexed)
+    constexpr int NST = 2;  // dS row stores per wave and iteration (r-indexed; the dq pass reads the j-view)
 #else
     constexpr int NST = 0;  // (ablation build: no dS stores)
 #endif
@@ -200,7 +199,6 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
     const __amdgpu_buffer_rsrc_t rl = make_rsrc(Lp, (uint32_t)(S * 4));
     const __amdgpu_buffer_rsrc_t rd = make_rsrc(Dp, (uint32_t)(S * 4));
     bf16* qr_rows = dqr + ((int64_t)h * a.B + b) * S * ldr;
-    bf16* sj_rows = dsj + ((int64_t)h * a.B + b) * S * ldr;
     const float c2 = a.scale * LOG2E;
     // P ks scale = exp2(c2 x + lks): the dS factor ks scale rides in P
     const float ks_scale = (DROP ? a.keep_scale : 1.f) * a.scale;
@@ -316,33 +314,26 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
     // wave issues exactly NST stores per iteration.
     const uint32_t ds_bytes = (uint32_t)min<int64_t>((int64_t)S * ldr * 2, OOB - 1);
     const int ldr2 = (int)(ldr * 2);
-    // per-lane parts of the two pieces' offsets (row = t/16 + 16 k, 8 keys
-    // from j0 + 8 (t & 15)); i = ip + row adds ip (ldr2 - 2) resp. ip ldr2
-    uint32_t st_r[2], st_j[2];
+    // per-lane part of the two pieces' offsets (row = t/16 + 16 k, 8 keys
+    // from j0 + 8 (t & 15)); i = ip + row adds ip (ldr2 - 2)
+    uint32_t st_r[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const int row = (tid >> 4) + 16 * k, j = j0 + 8 * (tid & 15);
         st_r[k] = (uint32_t)(row * (ldr2 - 2) + 2 * (S - 1 + j));
-        st_j[k] = (uint32_t)(row * ldr2 + 2 * j);
     }
     auto store_read = [&](int k, int sbuf) {
         const int row = (ltid >> 4) + 16 * k, ch = ltid & 15;
         return *(const u32x4*)(smem + O_T + sbuf * T_BYTES + row * T_PITCH + ch * 16);
     };
     auto store_piece = [&](int k, const u32x4& v, int ip, bool valid) {
-        // descriptors rebuilt per use from readfirstlane'd halves (kept live
-        // across the loop they would sit in VGPRs: a waterfall loop per store)
+        // descriptor rebuilt per use from readfirstlane'd halves (kept live
+        // across the loop it would sit in VGPRs: a waterfall loop per store)
         // 32-bit offsets (S * ldr * 2 < 4 GB, checked at launch); rows past the
-        // sequence end fall past num_records
+        // sequence end fall past num_records. Unaligned 16-B stores: row i's
+        // keys j0.. start at r = S-1-i+j0
         const __amdgpu_buffer_rsrc_t rqr = make_rsrc(qr_rows, ds_bytes);
-#if defined(KV_ABL_ALIGNR)
-        __builtin_amdgcn_raw_buffer_store_b128(v, rqr, valid ? st_j[k] + (uint32_t)ip * (uint32_t)ldr2 : OOB, 0, 0);
-#elif !defined(KV_ABL_NOSTORE_R)
         __builtin_amdgcn_raw_buffer_store_b128(v, rqr, valid ? st_r[k] + (uint32_t)ip * (uint32_t)(ldr2 - 2) : OOB, 0,
-                                               KV_STORE_AUX);
-#endif
-        const __amdgpu_buffer_rsrc_t rsj = make_rsrc(sj_rows, ds_bytes);
-        __builtin_amdgcn_raw_buffer_store_b128(v, rsj, valid ? st_j[k] + (uint32_t)ip * (uint32_t)ldr2 : OOB, 0,
                                                KV_STORE_AUX);
     };
 
@@ -678,7 +669,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
 }  // namespace
 
 int flash_bwd_kv5(const AttnArgs& a, const float* nls, const float* ndk, const bf16* dout, int64_t ldo, bf16* dqkv,
-                  int64_t ldd, bf16* dqr, bf16* dsj, int64_t ldr, hipStream_t s) {
+                  int64_t ldd, bf16* dqr, int64_t ldr, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)flash_bwd_kv5_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -691,13 +682,13 @@ int flash_bwd_kv5(const AttnArgs& a, const float* nls, const float* ndk, const b
     if ((a.S + 128) * a.ldq * 2 >= (int64_t)OOB || (a.S + 128) * ldo * 2 >= (int64_t)OOB || a.n_meta > 8) return -1;
     if ((a.S + 128) * ldr * 2 >= (int64_t)OOB) return -1;
     if (a.colmask && mask_bh_bytes(a.mask_ld) >= (int64_t)OOB) return -1;
-    if (ldr < a.S + 128 || !dsj) return -1;
+    if (ldr < a.S + 128) return -1;
     const dim3 grid((unsigned)((a.S + KB - 1) / KB), (unsigned)a.H, (unsigned)a.B);
     if (a.colmask)
         hipLaunchKernelGGL((flash_bwd_kv5_kernel<true>), grid, dim3(NT), LDS_BYTES, s, a, nls, ndk, dout, ldo, dqkv, ldd,
-                           dqr, dsj, ldr);
+                           dqr, ldr);
     else
         hipLaunchKernelGGL((flash_bwd_kv5_kernel<false>), grid, dim3(NT), LDS_BYTES, s, a, nls, ndk, dout, ldo, dqkv,
-                           ldd, dqr, dsj, ldr);
+                           ldd, dqr, ldr);
     return 0;
 }

@@ -1,9 +1,11 @@
 // Relative-position attention backward, query gradient (model_transformer.py:72-80
 // differentiated w.r.t. q):
 //   dq_i = sum_j dS_ij k_j  +  sum_j dS_ij R[S-1-i+j]
-//        = sum_j dSj[i][j] K[j]  +  sum_r dQR[i][r] R[r]          (r = S-1-i+j)
-// The key/value pass (attn_bwd5.hip) writes dS twice: j-indexed (dSj, zero for
-// j > i inside the tiles it visits) and r-indexed (dQR). Both products are plain
+//        = sum_j dQR[i][S-1-i+j] K[j]  +  sum_r dQR[i][r] R[r]     (r = S-1-i+j)
+// The key/value pass (attn_bwd5.hip) writes dS once, r-indexed (dQR, zero for
+// j > i inside the tiles it visits); the K term reads its j-view, i.e. the same
+// memory with row pitch ldr - 1 from element S - 1 (unaligned 16-B loads: row i
+// starts S-1-i elements into its r-row). Both products are plain
 // contractions over one K axis, so one kernel runs them back to back into the
 // same accumulators: a 128-query x 128-dim output tile per (b, h), K range
 // j in [0, i0+128) then r in [S-1-i_last rounded down to 64, S) (rows below
@@ -66,8 +68,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t dq_rsrc(const void* base, uint
 }
 
 // 64 KB of LDS, two workgroups per CU.
-__global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const bf16* __restrict__ dsj,
-                                                             const bf16* __restrict__ dqr, int64_t ldr,
+__global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const bf16* __restrict__ dqr, int64_t ldr,
                                                              bf16* __restrict__ dqkv, int64_t ldd) {
     constexpr int BK = 64;
     constexpr int A_BYTES = BM * BK * 2, B_BYTES = BK * HSZ * 2, STAGE = A_BYTES + B_BYTES;
@@ -83,7 +84,6 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
     const int64_t rows = ((h * a.B + b) * S) * ldr;
     const uint32_t slab = (uint32_t)(S * ldr * 2);
     const __amdgpu_buffer_rsrc_t rR = dq_rsrc(dqr + rows, slab);
-    const __amdgpu_buffer_rsrc_t rJ = dq_rsrc(dsj + rows, slab);
     const bf16* B0 = (const bf16*)a.qkv + b * S * ldq + (H + h) * HSZ;
     const bf16* B1 = (const bf16*)a.R + h * a.S_max * HSZ;
     const int64_t ke0 = min<int64_t>(S, i0 + BM);        // j range [0, ke0)
@@ -109,8 +109,10 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
         for (int u = 0; u < NU; ++u) {
             {  // A [128 rows][BK k]
                 const int64_t gi = i0 + arow[u];
-                const uint32_t off = gi < S ? (uint32_t)((gi * ldr + k0 + 8 * ch8) * 2) : 0xFFFF0000u;
-                ra[u] = __builtin_amdgcn_raw_buffer_load_b128(s1 ? rR : rJ, off, 0, 0);
+                // K term: element j of row gi's j-view = r = S-1-gi+j of its r-row
+                const int64_t c0 = s1 ? k0 : S - 1 - gi + k0;
+                const uint32_t off = gi < S ? (uint32_t)((gi * ldr + c0 + 8 * ch8) * 2) : 0xFFFF0000u;
+                ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rR, off, 0, 0);
             }
             {  // B [BK k][128 d]
                 const int c = tid + NT * u;
@@ -179,8 +181,7 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
 
 }  // namespace
 
-void flash_bwd_dq(const AttnArgs& a, const bf16* dsj, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd,
-                  hipStream_t s) {
+void flash_bwd_dq(const AttnArgs& a, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd, hipStream_t s) {
     const dim3 grid((unsigned)((a.S + BM - 1) / BM), (unsigned)a.H, (unsigned)a.B);
-    hipLaunchKernelGGL(flash_bwd_dq_kernel, grid, dim3(NT), 0, s, a, dsj, dqr, ldr, dqkv, ldd);
+    hipLaunchKernelGGL(flash_bwd_dq_kernel, grid, dim3(NT), 0, s, a, dqr, ldr, dqkv, ldd);
 }

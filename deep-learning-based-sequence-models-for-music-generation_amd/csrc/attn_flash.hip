@@ -6,7 +6,7 @@
 //   kv  : per 128-key block (attn_bwd5.hip): recompute S, P; dP = dO.V^T;
 //         dS = P (dP - D) scale; dK, dV accumulated in registers; dS written
 //         once, r-indexed: dQR[h][b][i][r = S-1-i+j];
-//   dq  : dq = dS . K (the j-view of dQR) + dQR . R (attn_dq.hip);
+//   dq  : dq = dS . K (the j-view of dQR: pitch ldr - 1) + dQR . R (attn_dq.hip);
 //   GEMM: dR += dQR^T . Q (batched over heads, split-K partials);
 //   meta: the metadata-prefix entries j > i (flash_bwd_meta5_kernel).
 // The forward is attn_fwd3.hip.
@@ -148,8 +148,8 @@ __global__ __launch_bounds__(HS) void flash_bwd_meta_dr_kernel(AttnArgs a, const
 namespace {
 // zero the part of dQR[h][b][i][r] that the consumers read but the key/value
 // pass does not write: r in [S-1-i-DQR_BAND, S-1-i) (below the written band)
-// and the row pad [S, ldr); and the row pad of dSj. The dq kernel and the dR
-// product never read further below the band.
+// and the row pad [S, ldr). The dq kernel and the dR product never read
+// further below the band.
 constexpr int DQR_BAND = 256;
 // one wave per row; ldr % 8 == 0 (flash_dqr_ld), so the row starts are 16-B
 // aligned: ragged ends with 2-B stores, the body with 16-B stores
@@ -162,8 +162,7 @@ __device__ __forceinline__ void zero_span(bf16* __restrict__ p, int64_t lo, int6
     for (int64_t r = a + 8 * lane; r < e; r += 512) *(u32x4*)(p + r) = z;
 }
 
-__global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, bf16* __restrict__ dsj, int64_t ldr, int64_t S,
-                                     int64_t rows) {
+__global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, int64_t ldr, int64_t S, int64_t rows) {
     const int64_t row = blockIdx.x * 4LL + (threadIdx.x >> 6);  // (h, b, i) flattened
     if (row >= rows) return;
     const int lane = threadIdx.x & 63;
@@ -171,7 +170,6 @@ __global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, bf16* __restrict__ 
     bf16* p = dqr + row * ldr;
     zero_span(p, max<int64_t>(0, S - 1 - i - DQR_BAND), S - 1 - i, lane);
     zero_span(p, S, ldr, lane);
-    zero_span(dsj + row * ldr, S, ldr, lane);
 }
 }  // namespace
 
@@ -182,7 +180,7 @@ __global__ void dqr_band_zero_kernel(bf16* __restrict__ dqr, bf16* __restrict__ 
 // the funnel shift's second chunk): padding, zeroed once per workspace
 int64_t flash_dqr_ld(int64_t S) { return (S + 200 + 7) / 8 * 8; }
 
-// workspace: dQR bf16 [H][B][S][ldr] | dSj bf16 [H][B][S][ldr] | D f32 [B][H][S]
+// workspace: dQR bf16 [H][B][S][ldr] | D f32 [B][H][S]
 //            | dR split-K partials f32 [ksplit][H][S][HS]
 //            | nls f32 [B][H][S] | ndk f32 [B][H][S] | mdr f32 [B][H][8][HS]
 static size_t align256(size_t x) { return (x + 255) / 256 * 256; }
@@ -192,7 +190,7 @@ static size_t dr_ws_bytes(int64_t B, int64_t S, int64_t H) {
 
 size_t flash_bwd_workspace(int64_t B, int64_t S, int64_t H) {
     const int64_t ldr = flash_dqr_ld(S);
-    return 2 * align256((size_t)H * B * S * ldr * 2) + 3 * align256((size_t)B * H * S * 4) +
+    return align256((size_t)H * B * S * ldr * 2) + 3 * align256((size_t)B * H * S * 4) +
            align256((size_t)B * H * 8 * HS * 4) +
            align256(dr_ws_bytes(B, S, H));
 }
@@ -202,8 +200,6 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     const int64_t B = a.B, S = a.S, H = a.H, ldr = flash_dqr_ld(S);
     char* p = (char*)ws;
     bf16* dqr = (bf16*)p;
-    p += align256((size_t)H * B * S * ldr * 2);
-    bf16* dsj = (bf16*)p;
     p += align256((size_t)H * B * S * ldr * 2);
     float* Dv = (float*)p;
     p += align256((size_t)B * H * S * 4);
@@ -219,18 +215,18 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     // (their dS entries there are 0 by the mask), so a workspace that already
     // served this (B, S, H) keeps them (ws_ready)
     if (!ws_ready)
-        hipLaunchKernelGGL(dqr_band_zero_kernel, dim3((unsigned)((H * B * S + 3) / 4)), dim3(256), 0, s, dqr, dsj, ldr,
-                           S, H * B * S);
+        hipLaunchKernelGGL(dqr_band_zero_kernel, dim3((unsigned)((H * B * S + 3) / 4)), dim3(256), 0, s, dqr, ldr, S,
+                           H * B * S);
     if (ldo % 8 || ((uintptr_t)dout % 16) || ((uintptr_t)out % 16))
         return msq_set_error(MSQ_ERR_ARG, "flash_bwd: dout / out need 16-B aligned rows");
     hipLaunchKernelGGL(flash_bwd_pre_vec_kernel, dim3((unsigned)((B * S * H + 15) / 16)), dim3(256), 0, s, a, dout, ldo,
                        out, lse, Dv, nls, ndk);
-    // key/value pass v5: dK, dV, and dS in both layouts (dQR r-indexed, dSj
-    // j-indexed; storing it once measured slower overall)
-    if (flash_bwd_kv5(a, nls, ndk, dout, ldo, dqkv, ldd, dqr, dsj, ldr, s))
+    // key/value pass v5: dK, dV, and dS once (dQR, r-indexed; its second,
+    // j-indexed copy cost the pass a quarter of its time: DESIGN.md §10)
+    if (flash_bwd_kv5(a, nls, ndk, dout, ldo, dqkv, ldd, dqr, ldr, s))
         return msq_set_error(MSQ_ERR_UNSUPPORTED, "flash_bwd: shape outside the key/value pass (n_meta > 8 or > 4 GB)");
-    // dq (bf16, q columns of dqkv) = dSj . K + dQR . R
-    flash_bwd_dq(a, dsj, dqr, ldr, dqkv, ldd, s);
+    // dq (bf16, q columns of dqkv) = dS . K (dQR's j-view) + dQR . R
+    flash_bwd_dq(a, dqr, ldr, dqkv, ldd, s);
     // dR[h][r] += sum_{b,i} dQR[h][b,i][r] q_{b,i}   (batched over heads; per batch
     // segment only i >= S-1-r contributes: tri 2, split over segments)
     // (a strided-batched hipBLASLt product over the whole K range, 2x the

@@ -34,6 +34,10 @@ constexpr uint32_t OOB = 0xFFFF0000u;
 #ifndef FWD3_REGSTAGE
 #define FWD3_REGSTAGE 0
 #endif
+// ablation builds (tools/build_var.sh -DFWD3_LAB=n): the LAB mask of the launched kernel
+#ifndef FWD3_LAB
+#define FWD3_LAB 0
+#endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
     const uint64_t a = (uint64_t)base;
@@ -368,16 +372,17 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
 int flash_fwd3(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)flash_fwd3_kernel<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)flash_fwd3_kernel<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)flash_fwd3_kernel<FWD3_LAB, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)flash_fwd3_kernel<FWD3_LAB, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
         attr = true;
     }
     if (a.rowmask && mask_bh_bytes(a.mask_ld) >= (int64_t)OOB) return -1;
     if (a.S * a.ldq * 2 >= (int64_t)OOB || a.S * HS * 2 >= (int64_t)OOB || a.n_meta > 8) return -1;
     const dim3 grid((unsigned)((a.S + QB - 1) / QB), (unsigned)a.H, (unsigned)a.B);
-    if (a.rowmask) hipLaunchKernelGGL((flash_fwd3_kernel<0, true>), grid, dim3(NT), LDS_BYTES, s, a, out, ldo, lse);
-    else hipLaunchKernelGGL((flash_fwd3_kernel<0, false>), grid, dim3(NT), LDS_BYTES, s, a, out, ldo, lse);
+    if (a.rowmask)
+        hipLaunchKernelGGL((flash_fwd3_kernel<FWD3_LAB, true>), grid, dim3(NT), LDS_BYTES, s, a, out, ldo, lse);
+    else hipLaunchKernelGGL((flash_fwd3_kernel<FWD3_LAB, false>), grid, dim3(NT), LDS_BYTES, s, a, out, ldo, lse);
     return 0;
 }
