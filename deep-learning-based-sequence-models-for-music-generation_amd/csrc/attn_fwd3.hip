@@ -28,6 +28,11 @@ constexpr int O_M = O_S + 8 * 16 * SCR * 4;
 constexpr int O_D = O_M + 64 * 4;  // dropout keep words of the block's 256 queries, 2 tiles
 constexpr int LDS_BYTES = O_D + 2 * QB * 4;
 constexpr uint32_t OOB = 0xFFFF0000u;
+// lazy-rescale threshold of the running row maximum, log2 units (P <= 2^RESCALE)
+#ifndef FWD3_RESCALE
+#define FWD3_RESCALE 8.f
+#endif
+constexpr float RESCALE = FWD3_RESCALE;
 // 1: the next K / V / R tile is staged through registers (loads after the
 // barrier, ds_write at the end of the tile) instead of in-loop LDS-DMA.
 // Measured 1-2 % slower at cfg 2 (0.908 vs 0.892 ms per launch, same box), so off.
@@ -74,7 +79,8 @@ __device__ __forceinline__ void bar() {
 }
 
 // LAB: ablation switches for tools/lab (0 in the library):
-// 1 no K.Q^T MFMA, 2 no QR MFMA, 4 no skew / softmax, 8 no PV MFMA, 16 no DMA in the loop
+// 1 no K.Q^T MFMA, 2 no QR MFMA, 4 no skew / softmax, 8 no PV MFMA, 16 no DMA in the loop,
+// 32 no skew scratch round trip, 64 no rescale, 128 no row max
 // DROP: attention-probability dropout (model_transformer.py:80): the keep word
 // of (query, key tile) is staged by LDS-DMA with the tile; P.V uses p * keep,
 // the softmax normaliser the undropped p, the output is scaled by 1/(1-p)
@@ -270,10 +276,15 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
                     continue;
                 }
                 const int iq = iw + 16 * q2 + il;
+                // (a wave's LDS operations execute in issue order, so the skewed
+                // reads below see these writes, and the next group's writes
+                // follow this group's reads, without an lgkmcnt(0) between:
+                // the compiler waits only where a read's value is used)
+                if (!(LAB & 32)) {
 #pragma unroll
-                for (int t = 0; t < 3; ++t) *(f32x4*)(scw + il * SCR + t * 16 + 4 * g) = qacc[q2][t];
-                __builtin_amdgcn_s_waitcnt(0xc07f);
-                __builtin_amdgcn_wave_barrier();
+                    for (int t = 0; t < 3; ++t) *(f32x4*)(scw + il * SCR + t * 16 + 4 * g) = qacc[q2][t];
+                    __builtin_amdgcn_wave_barrier();
+                }
                 float sv[2][4];
                 float mx = -INFINITY;
                 // masking only where a key may follow a query of the group or
@@ -285,7 +296,7 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int jl = nt * 16 + 4 * g + r;
-                            const float x = sacc[q2][nt][r] + scw[il * SCR + jl - il + 15];
+                            const float x = sacc[q2][nt][r] + ((LAB & 32) ? qacc[q2][nt][r] : scw[il * SCR + jl - il + 15]);
                             sv[nt][r] = x;
                             mx = fmaxf(mx, x);
                         }
@@ -304,11 +315,14 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
                             mx = fmaxf(mx, x);
                         }
                 }
-                __builtin_amdgcn_s_waitcnt(0xc07f);
-                __builtin_amdgcn_wave_barrier();  // scratch reads done before the next group's writes
-                mx = max_rows(mx);
-                const float m_new = fmaxf(m_run[q2], mx * c2);
-                if (__any(m_new > m_run[q2])) {  // rescale only when a running max moved (T13)
+                if (!(LAB & 32)) __builtin_amdgcn_wave_barrier();  // (code motion only)
+                if (!(LAB & 128)) mx = max_rows(mx);
+                // lazy rescale (T13): the running max moves only when some row's
+                // new maximum passes it by more than RESCALE (log2 units), so
+                // p = exp2(raw c2 - m) <= 2^RESCALE; l and O always see the same m
+                float m_new = m_run[q2];
+                if (!(LAB & 64) && __any(mx * c2 > m_run[q2] + RESCALE)) {
+                    m_new = (LAB & 128) ? 8.f : fmaxf(m_run[q2], mx * c2);
                     const float alpha = __builtin_amdgcn_exp2f(m_run[q2] - m_new);
                     l_part[q2] *= alpha;
 #pragma unroll
