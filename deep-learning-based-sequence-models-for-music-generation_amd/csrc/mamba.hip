@@ -1013,6 +1013,12 @@ __device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
     for (int k = 0; k < 8; ++k) r.e[k] = (bf16)v[k];
     return r.u;
 }
+__device__ __forceinline__ uint64_t pack4(f32x4 v) {
+    union { uint64_t u; bf16 e[4]; } r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r.e[k] = (bf16)v[k];
+    return r.u;
+}
 __device__ __forceinline__ void unpack8(u32x4 u, float (&v)[8]) {
     union { u32x4 u; bf16 e[8]; } r;
     r.u = u;
@@ -1135,10 +1141,22 @@ __global__ __launch_bounds__(256) void pass_kernel(float* __restrict__ states, c
 // One workgroup per (b, chunk, group of hg heads): the chunk's B / C rows and
 // C B^T (head-independent: only the decay mask L is per head) are staged /
 // computed once and serve the group's heads in turn.
+// 8 consecutive state values as bf16 (fp32 storage: rounded here; optionally unpacked)
+template <bool SB>
+__device__ __forceinline__ u32x4 ld_state(const void* base, int64_t e) {
+    if constexpr (SB) return *(const u32x4*)((const bf16*)base + e);
+    const float* f = (const float*)base + e;
+    const f32x4 h0 = *(const f32x4*)f, h1 = *(const f32x4*)(f + 4);
+    const float hv[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+    return pack8(hv);
+}
+// SB: the entry states are bf16 (the fused scan's form) or fp32 (the three-kernel
+// path's); either way the product reads them as bf16 (the same RNE rounding)
+template <bool SB>
 __global__ __launch_bounds__(512) void out_kernel(MambaArgs a, const bf16* __restrict__ xc,
                                                   const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
                                                   const float* __restrict__ A_log, const float* __restrict__ Dp,
-                                                  bf16* __restrict__ y, int64_t ldy, const float* __restrict__ states,
+                                                  bf16* __restrict__ y, int64_t ldy, const void* __restrict__ states,
                                                   int nch, float* __restrict__ clast, int hg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sCB = smem;           // half 0: C [t][n];     half 1: B [s][n]
@@ -1165,13 +1183,11 @@ __global__ __launch_bounds__(512) void out_kernel(MambaArgs a, const bf16* __res
         k.h = kg.h + hh;
         const float A = -expf(A_log[k.h]), Dh = Dp[k.h];
         u32x4 xr;
-        const float* st = states + ((k.b * a.nheads + k.h) * nch + k.c) * (int64_t)(P * N);
+        const int64_t slot = ((k.b * a.nheads + k.h) * nch + k.c) * (int64_t)(P * N);
         {
             const int row = tid >> 3, ch = tid & 7;
             xr = ld_chunk(a, k, xc, k.h * P, tid);
-            const f32x4 h0 = *(const f32x4*)(st + row * N + ch * 8), h1 = *(const f32x4*)(st + row * N + ch * 8 + 4);
-            const float hv[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-            *(u32x4*)(sXH + offd(row, 8 + ch)) = pack8(hv);
+            *(u32x4*)(sXH + offd(row, 8 + ch)) = ld_state<SB>(states, slot + row * N + ch * 8);
         }
         dt_cum(a, k, zx, dt_bias, A, sdt, scum, tid);
         __syncthreads();
@@ -1344,7 +1360,7 @@ __device__ __forceinline__ void dt_cum_raw(const Chunk& k, unsigned raw, float b
 constexpr size_t SCAN_LDS = 2 * (IMG + 512);
 __global__ __launch_bounds__(512) void scan_fwd_kernel(MambaArgs a, const bf16* __restrict__ xc,
                                                        const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
-                                                       const float* __restrict__ A_log, float* __restrict__ states,
+                                                       const float* __restrict__ A_log, bf16* __restrict__ states,
                                                        float* __restrict__ clast, int nch, float* __restrict__ fin) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1357,7 +1373,14 @@ __global__ __launch_bounds__(512) void scan_fwd_kernel(MambaArgs a, const bf16* 
     H[0][0] = H[1][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
     u32x4 x0[1], b0[1], x1[1], b1[1];
     unsigned r0 = 0u, r1 = 0u;
-    auto store_state = [&](float* st) {
+    // entry states in bf16 (what out / grad multiply with); the final state in fp32
+    auto store_state = [&](bf16* st) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            *(uint64_t*)(st + (rb + 16 * i + (lane & 15)) * N + cb + 4 * (lane >> 4)) = pack4(H[i][0]);
+        }
+    };
+    auto store_fin = [&](float* st) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
             *(f32x4*)(st + (rb + 16 * i + (lane & 15)) * N + cb + 4 * (lane >> 4)) = H[i][0];
@@ -1404,7 +1427,8 @@ __global__ __launch_bounds__(512) void scan_fwd_kernel(MambaArgs a, const bf16* 
         // the entry state of chunk c + 1 (or the final state) is stored right after
         // the update: H is next overwritten one chunk later, so the wait the store's
         // source registers need does not also wait for the next loads
-        store_state(c + 1 < nch ? states + (bh * nch + c + 1) * (int64_t)(P * N) : fin + bh * (int64_t)(P * N));
+        if (c + 1 < nch) store_state(states + (bh * nch + c + 1) * (int64_t)(P * N));
+        else store_fin(fin + bh * (int64_t)(P * N));
         // no trailing barrier: chunk c + 1 writes the other buffer, and chunk c + 2
         // writes this one only after every wave has passed chunk c + 1's first barrier
     };
@@ -1421,8 +1445,8 @@ __global__ __launch_bounds__(512) void scan_fwd_kernel(MambaArgs a, const bf16* 
 __global__ __launch_bounds__(256) void scan_bwd_kernel(MambaArgs a, const bf16* __restrict__ xc,
                                                        const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
                                                        const float* __restrict__ A_log, const bf16* __restrict__ dY,
-                                                       int64_t ldy, float* __restrict__ U, int nch,
-                                                       float* __restrict__ dh0) {
+                                                       int64_t ldy, bf16* __restrict__ U, int nch,
+                                                       bf16* __restrict__ dh0) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t bh = blockIdx.x;
@@ -1434,12 +1458,12 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(MambaArgs a, const bf16* 
     u32x4 c0[2], c1[2];
     u32x4 y0[2], y1[2];  // raw bf16 dY rows
     unsigned r0 = 0u, r1 = 0u;
-    auto store_d = [&](float* dst) {
+    auto store_d = [&](bf16* dst) {  // bf16, as grad multiplies with it
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-                *(f32x4*)(dst + (rb + 16 * i + (lane & 15)) * N + cb + 16 * j + 4 * (lane >> 4)) = D[i][j];
+                *(uint64_t*)(dst + (rb + 16 * i + (lane & 15)) * N + cb + 16 * j + 4 * (lane >> 4)) = pack4(D[i][j]);
     };
     auto load = [&](int c, u32x4 (&cr)[2], u32x4 (&yr)[2], unsigned& raw) {
         const Chunk k = chunk_at(a, bh, c);
@@ -1502,12 +1526,12 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(MambaArgs a, const bf16* 
     }
 }
 
-template <typename TD>
+template <typename TD, bool SB>
 __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* __restrict__ xc,
                                                       const bf16* __restrict__ zx, const float* __restrict__ dt_bias,
                                                       const float* __restrict__ A_log, const float* __restrict__ Dp,
                                                       const bf16* __restrict__ dY, int64_t ldy,
-                                                      const float* __restrict__ states, const float* __restrict__ dHx,
+                                                      const void* __restrict__ states, const void* __restrict__ dHx,
                                                       float* __restrict__ dxc, float* __restrict__ dbc,
                                                       TD* __restrict__ dzx,
                                                       float* __restrict__ gA_log, float* __restrict__ gD,
@@ -1544,25 +1568,23 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
     k.h = kg.h + hh;
     const float A = -expf(A_log[k.h]), Dh = Dp[k.h];
     const int64_t slot = ((k.b * a.nheads + k.h) * nch + k.c) * (int64_t)(P * N);
-    const float* Hs = states + slot;
-    const float* dHs = dHx + slot;
     u32x4 xr[2];
     float hdh = 0.f;  // sum dH o H (the cum_last term)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
         xr[u] = ld_chunk(a, k, xc, k.h * P, e);
-        float hv[8], dv[8];
+        // H / dH as bf16 (the MFMA operands); the cum_last term from the same values
+        const u32x4 hb = ld_state<SB>(states, slot + row * N + ch * 8), db = ld_state<SB>(dHx, slot + row * N + ch * 8);
         {
-            const f32x4 h0 = *(const f32x4*)(Hs + row * N + ch * 8), h1 = *(const f32x4*)(Hs + row * N + ch * 8 + 4);
-            const f32x4 d0 = *(const f32x4*)(dHs + row * N + ch * 8), d1 = *(const f32x4*)(dHs + row * N + ch * 8 + 4);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) hv[q] = h0[q], hv[4 + q] = h1[q], dv[q] = d0[q], dv[4 + q] = d1[q];
+            float hv[8], dv[8];
+            unpack8(hb, hv);
+            unpack8(db, dv);
 #pragma unroll
             for (int q = 0; q < 8; ++q) hdh += hv[q] * dv[q];
         }
-        *(u32x4*)(sHD + offd(row, ch)) = pack8(hv);
-        *(u32x4*)(sHD + offd(row, 8 + ch)) = pack8(dv);
+        *(u32x4*)(sHD + offd(row, ch)) = hb;
+        *(u32x4*)(sHD + offd(row, 8 + ch)) = db;
         // dY rows are bf16 already: copied into the image as they are (zero past nval)
         *(u32x4*)(sXY + offd(row, 8 + ch)) =
             row < k.nval ? *(const u32x4*)(dY + (k.b * a.L + k.t0 + row) * ldy + k.h * P + ch * 8)
@@ -1820,8 +1842,10 @@ extern "C" int msq_mamba_ssd_fwd_state(void* y, int64_t ldy, float* states, floa
     if (dtype == MSQ_BF16) {
         float* clast = states + B * nheads * nch * (int64_t)(P * N);
         const dim3 gch((unsigned)(B * nheads * nch));
-        allow_lds(ssd2::out_kernel, ssd2::OUT_LDS);
-        if (getenv("MSQ_MAMBA_SSD_3K")) {  // per-chunk state kernel + separate pass (round-2 form)
+        const bool k3 = getenv("MSQ_MAMBA_SSD_3K") != nullptr;
+        if (k3) allow_lds(ssd2::out_kernel<false>, ssd2::OUT_LDS);
+        else allow_lds(ssd2::out_kernel<true>, ssd2::OUT_LDS);
+        if (k3) {  // per-chunk state kernel + separate pass (round-2 form)
             allow_lds(ssd2::state_kernel, ssd2::STATE_LDS);
             hipLaunchKernelGGL(ssd2::state_kernel, gch, dim3(256), ssd2::STATE_LDS, s, a, (const bf16*)xc,
                                (const bf16*)zxbcdt, dt_bias, A_log, states, clast, nch);
@@ -1831,14 +1855,16 @@ extern "C" int msq_mamba_ssd_fwd_state(void* y, int64_t ldy, float* states, floa
             allow_lds(ssd2::scan_fwd_kernel, ssd2::SCAN_LDS);
             if (!final_state) final_state = clast + B * nheads * nch;  // scratch past cum_last
             hipLaunchKernelGGL(ssd2::scan_fwd_kernel, dim3((unsigned)(B * nheads)), dim3(512), ssd2::SCAN_LDS, s, a,
-                               (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, states, clast, nch,
+                               (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, (bf16*)states, clast, nch,
                                final_state);
         }
         // out: one workgroup per (b, chunk, group of hg heads), as grad
         const int hg = nheads % 4 == 0 ? 4 : nheads % 2 == 0 ? 2 : 1;
-        hipLaunchKernelGGL(ssd2::out_kernel, dim3((unsigned)(B * (nheads / hg) * nch)), dim3(512), ssd2::OUT_LDS, s, a,
-                           (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, D, (bf16*)y, ldy, states, nch, clast,
-                           hg);
+        const dim3 go((unsigned)(B * (nheads / hg) * nch));
+        if (k3) hipLaunchKernelGGL(ssd2::out_kernel<false>, go, dim3(512), ssd2::OUT_LDS, s, a, (const bf16*)xc,
+                                   (const bf16*)zxbcdt, dt_bias, A_log, D, (bf16*)y, ldy, states, nch, clast, hg);
+        else hipLaunchKernelGGL(ssd2::out_kernel<true>, go, dim3(512), ssd2::OUT_LDS, s, a, (const bf16*)xc,
+                                (const bf16*)zxbcdt, dt_bias, A_log, D, (bf16*)y, ldy, states, nch, clast, hg);
         MSQ_LAUNCH_CHECK();
         return MSQ_OK;
     }
@@ -1935,8 +1961,10 @@ extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, cons
         // grad: one workgroup per (b, chunk, group of hg heads); the group's B / C
         // tile is staged once and its dB / dC rows summed in registers
         const int hg = nheads % 4 == 0 ? 4 : nheads % 2 == 0 ? 2 : 1;
-        allow_lds(ssd2::grad_kernel<bf16>, ssd2::GRAD_LDS);
-        if (getenv("MSQ_MAMBA_SSD_3K")) {
+        const bool k3 = getenv("MSQ_MAMBA_SSD_3K") != nullptr;
+        if (k3) allow_lds(ssd2::grad_kernel<bf16, false>, ssd2::GRAD_LDS);
+        else allow_lds(ssd2::grad_kernel<bf16, true>, ssd2::GRAD_LDS);
+        if (k3) {
             allow_lds(ssd2::uterm_kernel, ssd2::UTERM_LDS);
             hipLaunchKernelGGL(ssd2::uterm_kernel, gch, dim3(256), ssd2::UTERM_LDS, s, a, (const bf16*)xc,
                                (const bf16*)zxbcdt, dt_bias, A_log, (const bf16*)dY, ldy, U, nch);
@@ -1945,12 +1973,16 @@ extern "C" int msq_mamba_ssd_bwd(float* dxc, int64_t ld_dxc, void* dzxbcdt, cons
         } else {
             allow_lds(ssd2::scan_bwd_kernel, ssd2::SCAN_LDS);
             hipLaunchKernelGGL(ssd2::scan_bwd_kernel, dim3((unsigned)(B * nheads)), dim3(256), ssd2::SCAN_LDS, s, a,
-                               (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, (const bf16*)dY, ldy, U, nch,
-                               dbc + B * L * nheads * 2 * N);
+                               (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, (const bf16*)dY, ldy, (bf16*)U,
+                               nch, (bf16*)(dbc + B * L * nheads * 2 * N));
         }
-        hipLaunchKernelGGL(ssd2::grad_kernel<bf16>, dim3((unsigned)(B * (nheads / hg) * nch)), dim3(256),
-                           ssd2::GRAD_LDS, s, a, (const bf16*)xc, (const bf16*)zxbcdt, dt_bias, A_log, D, (const bf16*)dY, ldy,
-                           states, U, dxc, dbc, (bf16*)dzxbcdt, gA_log, gD, gdt_bias, nch, hg);
+        const dim3 gg((unsigned)(B * (nheads / hg) * nch));
+        if (k3) hipLaunchKernelGGL((ssd2::grad_kernel<bf16, false>), gg, dim3(256), ssd2::GRAD_LDS, s, a, (const bf16*)xc,
+                                   (const bf16*)zxbcdt, dt_bias, A_log, D, (const bf16*)dY, ldy, states, U, dxc, dbc,
+                                   (bf16*)dzxbcdt, gA_log, gD, gdt_bias, nch, hg);
+        else hipLaunchKernelGGL((ssd2::grad_kernel<bf16, true>), gg, dim3(256), ssd2::GRAD_LDS, s, a, (const bf16*)xc,
+                                (const bf16*)zxbcdt, dt_bias, A_log, D, (const bf16*)dY, ldy, states, U, dxc, dbc,
+                                (bf16*)dzxbcdt, gA_log, gD, gdt_bias, nch, hg);
         hipLaunchKernelGGL(ssd2::dbc_reduce_kernel, dim3((unsigned)((B * L * (2 * N / 4) + 255) / 256)), dim3(256), 0,
                            s, dbc, dxc, B * L, nheads / hg, ldxc, d_inner);
         MSQ_LAUNCH_CHECK();
