@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # MSQ_LIB_PATH: an alternate build of the same library (same-box A/B tools only)
 LIB_PATH = os.environ.get("MSQ_LIB_PATH") or os.path.join(HERE, "libmidiseq.so")
 
-F32, BF16 = 0, 1
+F32, BF16, MASK1 = 0, 1, 2
 ROUTE_DEFAULT, ROUTE_TILE256, ROUTE_TILE128 = range(3)  # msq_gemm_set_route
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_RESID, EPI_RELU_MASK, EPI_ACCUM, EPI_BIAS_DROP_RESID = range(7)
 
@@ -161,4 +161,6 @@ def dt(t):
         return F32
     if t.dtype == torch.bfloat16:
         return BF16
+    if t.dtype == torch.int32:  # a GEMM aux bitmask (MSQ_MASK1)
+        return MASK1
     raise TypeError(f"unsupported dtype {t.dtype}")

@@ -78,6 +78,18 @@ __device__ __forceinline__ f32x4 epi_aux_load(const GemmArgs& g, const TX* X, in
     const int nv = g.vec ? (int)min<int64_t>(4, g.N - n) : -(int)min<int64_t>(4, g.N - n);
     return epi_load(X + m * g.ldx + n, nv);
 }
+// MSQ_MASK1 aux: one uint32 word per 32 columns (g.ldx in words); the mask
+// bits of C[m][n..n+3] (n % 4 == 0: one word) as 0 / 1
+struct mask1_t {
+    uint32_t w;
+};
+__device__ __forceinline__ f32x4 mask1_bits(uint32_t w, int64_t n) {
+    const uint32_t b = w >> (n & 31);
+    return (f32x4){(float)(b & 1u), (float)((b >> 1) & 1u), (float)((b >> 2) & 1u), (float)((b >> 3) & 1u)};
+}
+__device__ __forceinline__ f32x4 epi_aux_load(const GemmArgs& g, const mask1_t* X, int64_t m, int64_t n) {
+    return mask1_bits(X[m * g.ldx + (n >> 5)].w, n);
+}
 
 // Applies the epilogue to one lane's 4 consecutive outputs C[m][n..n+3]
 // (xpre: the aux vector, already loaded).
@@ -92,14 +104,14 @@ __device__ __forceinline__ f32x4 epi_apply(const GemmArgs& g, TC* C, const TX* X
     if ((EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID ||
          EPI == MSQ_EPI_BIAS_DROP_RESID) && g.bias)
         v += epi_load(g.bias + n, nv);
-    if (EPI == MSQ_EPI_BIAS_DROP_RESID) v = epi_drop(g, m, n, v) + (xpre ? *xpre : epi_load(X + m * g.ldx + n, nv));
+    if constexpr (EPI == MSQ_EPI_BIAS_DROP_RESID) v = epi_drop(g, m, n, v) + (xpre ? *xpre : epi_load(X + m * g.ldx + n, nv));
     if (EPI == MSQ_EPI_BIAS_RELU) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);
     }
-    if (EPI == MSQ_EPI_BIAS_RESID) v += xpre ? *xpre : epi_load(X + m * g.ldx + n, nv);
+    if constexpr (EPI == MSQ_EPI_BIAS_RESID) v += xpre ? *xpre : epi_load(X + m * g.ldx + n, nv);
     if (EPI == MSQ_EPI_RELU_MASK) {
-        const f32x4 x = xpre ? *xpre : epi_load(X + m * g.ldx + n, nv);
+        const f32x4 x = xpre ? *xpre : epi_aux_load(g, X, m, n);
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = x[t] > 0.f ? v[t] : 0.f;
     }

@@ -252,16 +252,16 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
             if ((EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID ||
                  EPI == MSQ_EPI_BIAS_DROP_RESID) && g.bias)
                 v += epi_load(g.bias + n, nv);
-            if (EPI == MSQ_EPI_BIAS_DROP_RESID) v = epi_drop(g, m, n, v) + epi_load(X + m * g.ldx + n, nv);
+            if constexpr (EPI == MSQ_EPI_BIAS_DROP_RESID) v = epi_drop(g, m, n, v) + epi_load(X + m * g.ldx + n, nv);
             if (EPI == MSQ_EPI_BIAS_RELU) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);
             }
-            if (EPI == MSQ_EPI_BIAS_RESID) {
+            if constexpr (EPI == MSQ_EPI_BIAS_RESID) {
                 v += epi_load(X + m * g.ldx + n, nv);
             }
             if (EPI == MSQ_EPI_RELU_MASK) {
-                const f32x4 x = epi_load(X + m * g.ldx + n, nv);
+                const f32x4 x = epi_aux_load(g, X, m, n);
 #pragma unroll
                 for (int t = 0; t < 4; ++t) v[t] = x[t] > 0.f ? v[t] : 0.f;
             }
@@ -376,6 +376,7 @@ int dispatch_epi(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hipS
         case MSQ_EPI_BIAS_RELU: return D(MSQ_EPI_BIAS_RELU, float);
         case MSQ_EPI_BIAS_RESID: return D(MSQ_EPI_BIAS_RESID, float);
         case MSQ_EPI_RELU_MASK:
+            if (aux_dtype == MSQ_MASK1) return BF ? dispatch_bf16_t<MSQ_EPI_RELU_MASK, TC, mask1_t>(g, ta, tb, s) : 1;
             return aux_dtype == MSQ_BF16 ? D(MSQ_EPI_RELU_MASK, bf16) : D(MSQ_EPI_RELU_MASK, float);
         case MSQ_EPI_ACCUM: return D(MSQ_EPI_ACCUM, float);
         case MSQ_EPI_BIAS_DROP_RESID: return D(MSQ_EPI_BIAS_DROP_RESID, float);
@@ -499,6 +500,21 @@ __global__ void tail_epi_kernel(GemmArgs t, const float* __restrict__ tmp) {
     }
 }
 
+// MSQ_MASK1 bits of a bf16 C (the FFN1 forward on routes whose epilogue does
+// not write them): word [m][w] bit c = (C[m][32 w + c] > 0)
+__global__ __launch_bounds__(256) void relu_bits_kernel(const bf16* __restrict__ C, int64_t ldc,
+                                                        uint32_t* __restrict__ X, int64_t ldx, int64_t M, int64_t N) {
+    const int64_t nw = (N + 31) / 32, e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= M * nw) return;
+    const int64_t m = e / nw, w = e - m * nw;
+    uint32_t bits = 0u;
+    for (int c = 0; c < 32; ++c) {
+        const int64_t n = w * 32 + c;
+        if (n < N && (float)C[m * ldc + n] > 0.f) bits |= 1u << c;
+    }
+    X[m * ldx + w] = bits;
+}
+
 template <typename TC>
 void tail_epi_launch(const GemmArgs& t, const float* tmp, int epi, int aux_dtype, hipStream_t s) {
     const unsigned nb = (unsigned)std::min<int64_t>((t.M * (t.N / 4) + 255) / 256, 4096);
@@ -509,7 +525,8 @@ void tail_epi_launch(const GemmArgs& t, const float* tmp, int epi, int aux_dtype
         case MSQ_EPI_BIAS_RESID: hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_BIAS_RESID, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp); break;
         case MSQ_EPI_BIAS_DROP_RESID: hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_BIAS_DROP_RESID, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp); break;
         case MSQ_EPI_RELU_MASK:
-            if (aux_dtype == MSQ_BF16) hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_RELU_MASK, TC, bf16>), dim3(nb), dim3(256), 0, s, t, tmp);
+            if (aux_dtype == MSQ_MASK1) hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_RELU_MASK, TC, mask1_t>), dim3(nb), dim3(256), 0, s, t, tmp);
+            else if (aux_dtype == MSQ_BF16) hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_RELU_MASK, TC, bf16>), dim3(nb), dim3(256), 0, s, t, tmp);
             else hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_RELU_MASK, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp);
             break;
     }
@@ -581,6 +598,11 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
     MSQ_CHECK_ARG(aux || (epilogue != MSQ_EPI_BIAS_RESID && epilogue != MSQ_EPI_RELU_MASK),
                   "msq_gemm: epilogue needs aux");
     MSQ_CHECK_ARG(lda >= (ta ? M : K) && ldb >= (tb ? N : K) && ldc >= N, "msq_gemm: leading dim too small");
+    MSQ_CHECK_ARG(aux_dtype != MSQ_MASK1 ||
+                      (dtype == MSQ_BF16 && c_dtype == MSQ_BF16 && batch == 1 && ld_aux >= (N + 31) / 32 &&
+                       ((uintptr_t)aux % 4) == 0 && (epilogue == MSQ_EPI_RELU_MASK || epilogue == MSQ_EPI_BIAS_RELU)),
+                  "msq_gemm: a MSQ_MASK1 aux needs bf16 operands and C, one batch, ld_aux >= ceil(N / 32) words, "
+                  "epilogue RELU_MASK or BIAS_RELU");
     if (dtype == MSQ_BF16) {
         MSQ_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && (strideA % 8) == 0 && (strideB % 8) == 0,
                       "msq_gemm: bf16 path needs lda/ldb (and batch strides) %% 8 == 0");
@@ -603,7 +625,8 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
         const int xsz = aux_dtype == MSQ_BF16 ? 2 : 4;
         bool vec = (ldc % 4 == 0) && (strideC % 4 == 0) && ((uintptr_t)C % (4 * esz) == 0);
         if (bias) vec = vec && ((uintptr_t)bias % 16 == 0);
-        if (aux) vec = vec && (ld_aux % 4 == 0) && (stride_aux % 4 == 0) && ((uintptr_t)aux % (4 * xsz) == 0);
+        if (aux && aux_dtype != MSQ_MASK1)
+            vec = vec && (ld_aux % 4 == 0) && (stride_aux % 4 == 0) && ((uintptr_t)aux % (4 * xsz) == 0);
         g.vec = vec ? 1 : 0;
     }
     MSQ_CHECK_ARG(ws_bytes >= 0 && (ws || ws_bytes == 0), "msq_gemm_ex: bad workspace");
@@ -613,6 +636,21 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
     plan128_ksplit(g, dtype, epilogue);
     g.ws = (float*)ws;
     hipStream_t s = (hipStream_t)stream;
+    if (aux && aux_dtype == MSQ_MASK1 && epilogue == MSQ_EPI_BIAS_RELU) {
+        // the persistent tile writes the mask in its epilogue; elsewhere the
+        // product runs without it and one pass over C makes it
+        if (M > 64 && gemm_route() == MSQ_ROUTE_DEFAULT && gemm256p_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, s)) {
+            MSQ_LAUNCH_CHECK();
+            return MSQ_OK;
+        }
+        const int rc = msq_gemm_ex(dtype, ta, tb, M, N, K, A, lda, strideA, B, ldb, strideB, C, c_dtype, ldc, strideC,
+                                   batch, epilogue, bias, nullptr, MSQ_F32, 0, 0, seed, site, p, ws, ws_bytes, stream);
+        if (rc != MSQ_OK) return rc;
+        hipLaunchKernelGGL(relu_bits_kernel, dim3((unsigned)((M * ((N + 31) / 32) + 255) / 256)), dim3(256), 0, s,
+                           (const bf16*)C, ldc, (uint32_t*)aux, ld_aux, M, N);
+        MSQ_LAUNCH_CHECK();
+        return MSQ_OK;
+    }
     if (dtype == MSQ_BF16 && M <= 64 &&
         gemm_skinny_launch(g, ta, tb, epilogue, c_dtype, aux_dtype, (size_t)ws_bytes, s)) {
         MSQ_LAUNCH_CHECK();
@@ -730,7 +768,7 @@ extern "C" int msq_gemm_colsum(int ta, int tb, int64_t M, int64_t N, int64_t K, 
         g.batch = 1;
         const int xsz = aux_dtype == MSQ_BF16 ? 2 : 4;
         g.vec = (ldc % 4 == 0) && ((uintptr_t)C % 8 == 0) &&
-                (!aux || ((ld_aux % 4 == 0) && ((uintptr_t)aux % (4 * xsz) == 0)));
+                (!aux || aux_dtype == MSQ_MASK1 || ((ld_aux % 4 == 0) && ((uintptr_t)aux % (4 * xsz) == 0)));
         if (gemm256_colsum_launch(g, ta, tb, epilogue, aux_dtype, dbias, accumulate, (float*)ws, (size_t)ws_bytes, s)) {
             MSQ_LAUNCH_CHECK();
             return MSQ_OK;

@@ -310,7 +310,8 @@ void dispatch_epi(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hip
         case MSQ_EPI_BIAS_RELU: dispatch_t<MSQ_EPI_BIAS_RELU, TC, float>(g, ta, tb, s); break;
         case MSQ_EPI_BIAS_RESID: dispatch_t<MSQ_EPI_BIAS_RESID, TC, float>(g, ta, tb, s); break;
         case MSQ_EPI_RELU_MASK:
-            if (aux_dtype == MSQ_BF16) dispatch_t<MSQ_EPI_RELU_MASK, TC, bf16>(g, ta, tb, s);
+            if (aux_dtype == MSQ_MASK1) dispatch_t<MSQ_EPI_RELU_MASK, TC, mask1_t>(g, ta, tb, s);
+            else if (aux_dtype == MSQ_BF16) dispatch_t<MSQ_EPI_RELU_MASK, TC, bf16>(g, ta, tb, s);
             else dispatch_t<MSQ_EPI_RELU_MASK, TC, float>(g, ta, tb, s);
             break;
         case MSQ_EPI_ACCUM: dispatch_t<MSQ_EPI_ACCUM, TC, float>(g, ta, tb, s); break;
@@ -374,13 +375,15 @@ bool gemm256_colsum_launch(GemmArgs g, int ta, int tb, int epi, int aux_dtype, f
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * HALF);
         hipLaunchKernelGGL(kern, dim3(g.tiles_m * g.tiles_n), dim3(NT), 8 * HALF, s, g);
     };
-    const bool bx = aux_dtype == MSQ_BF16;
+    const bool bx = aux_dtype == MSQ_BF16, b1 = aux_dtype == MSQ_MASK1;
     if (ta == 0 && tb == 1) {
         if (epi == MSQ_EPI_NONE) go(gemm256_kernel<0, 1, MSQ_EPI_NONE, bf16, float, 0, true>);
+        else if (b1) go(gemm256_kernel<0, 1, MSQ_EPI_RELU_MASK, bf16, mask1_t, 0, true>);
         else if (bx) go(gemm256_kernel<0, 1, MSQ_EPI_RELU_MASK, bf16, bf16, 0, true>);
         else go(gemm256_kernel<0, 1, MSQ_EPI_RELU_MASK, bf16, float, 0, true>);
     } else if (ta == 0 && tb == 0) {
         if (epi == MSQ_EPI_NONE) go(gemm256_kernel<0, 0, MSQ_EPI_NONE, bf16, float, 0, true>);
+        else if (b1) go(gemm256_kernel<0, 0, MSQ_EPI_RELU_MASK, bf16, mask1_t, 0, true>);
         else if (bx) go(gemm256_kernel<0, 0, MSQ_EPI_RELU_MASK, bf16, bf16, 0, true>);
         else go(gemm256_kernel<0, 0, MSQ_EPI_RELU_MASK, bf16, float, 0, true>);
     } else {

@@ -51,6 +51,13 @@ __device__ __forceinline__ f32x4 p_aux_load(__amdgpu_buffer_rsrc_t rx, uint32_t 
     }
 }
 
+// MSQ_MASK1 aux: read as the ReLU mask of the dX product (RELU_MASK), written
+// beside C by the FFN1 forward (BIAS_RELU: 16 more stores per lane and tile)
+template <int EPI, typename TX>
+constexpr bool p_writes_bits() {
+    return EPI == MSQ_EPI_BIAS_RELU && std::is_same<TX, mask1_t>::value;
+}
+
 // epilogue of one tile: exactly p_stores<TC>() buffer stores per lane
 // CS: also the column sums of the written values (fp32, before the rounding
 // to TC) over the tile's rows, one partial row per (M-tile, wave-row) into
@@ -64,6 +71,7 @@ __device__ __forceinline__ void p_epilogue(const GemmArgs& g, __amdgpu_buffer_rs
     constexpr bool HAS_BIAS = EPI == MSQ_EPI_BIAS || EPI == MSQ_EPI_BIAS_RELU || EPI == MSQ_EPI_BIAS_RESID ||
                               EPI == MSQ_EPI_BIAS_DROP_RESID;
     constexpr bool CS = CSM == 1, ST = CSM == 2;
+    constexpr bool M1 = std::is_same<TX, mask1_t>::value, WB = p_writes_bits<EPI, TX>();
     const int r = lane & 15, gq = lane >> 4;
     f32x4 bv[2][2];
 #pragma unroll
@@ -117,7 +125,20 @@ __device__ __forceinline__ void p_epilogue(const GemmArgs& g, __amdgpu_buffer_rs
 #pragma unroll
     for (int ih = 0; ih < 2; ++ih) {
         f32x4 xp[4][2][2];
-        if (epi_reads_aux<EPI>()) {
+        if constexpr (M1 && epi_reads_aux<EPI>()) {
+            // one mask word per (row, 32-column span): the lane's 2 x 4 columns of it
+#pragma unroll
+            for (int i = 2 * ih; i < 2 * ih + 2; ++i)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const int64_t m = m0 + a * 128 + wr * 64 + i * 16 + r;
+                    const int64_t wd = (n0 + b * 128 + wc * 32) >> 5;
+                    const uint32_t off = (m < g.M && wd * 32 < g.N) ? (uint32_t)((m * g.ldx + wd) * 4) : OOB;
+                    const uint32_t wv = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rx, off, 0, 0);
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) xp[i][b][j] = mask1_bits(wv, j * 16 + 4 * gq);
+                }
+        } else if (epi_reads_aux<EPI>()) {
 #pragma unroll
             for (int i = 2 * ih; i < 2 * ih + 2; ++i)
 #pragma unroll
@@ -160,6 +181,22 @@ __device__ __forceinline__ void p_epilogue(const GemmArgs& g, __amdgpu_buffer_rs
                             if (cmax[b][j][e] != -INFINITY)
                                 csum[b][j][e] += __builtin_amdgcn_exp2f(((float)(TC)t[e] - cmax[b][j][e]) * L2E);
                     }
+                }
+                if constexpr (WB) {
+                    // bit (j 16 + 4 gq + e) of the span's word = (C as stored > 0); the
+                    // four gq lanes of a row OR their bits, lane gq = 0 stores the word
+                    uint32_t bits = 0u;
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            bits |= ((float)(TC)v[j][e] > 0.f ? 1u : 0u) << (j * 16 + 4 * gq + e);
+                    bits |= (uint32_t)__shfl_xor((int)bits, 16, 64);
+                    bits |= (uint32_t)__shfl_xor((int)bits, 32, 64);
+                    const int64_t wd = (n0 + b * 128 + wc * 32) >> 5;
+                    const uint32_t off =
+                        (gq == 0 && m < g.M && wd * 32 < g.N) ? (uint32_t)((m * g.ldx + wd) * 4) : OOB;
+                    __builtin_amdgcn_raw_buffer_store_b32(bits, rx, off, 0, 0);
                 }
                 if (sizeof(TC) == 2) {
                     uint32_t p0x = pack_bf16(v[0][0], v[0][1]), p0y = pack_bf16(v[0][2], v[0][3]);
@@ -224,7 +261,7 @@ template <int TA, int TB, int EPI, typename TC, typename TX, int CSM = 0>
 __global__ __launch_bounds__(NT, 1) void gemm256p_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     lds_t* smem = (lds_t*)smem_raw;
-    constexpr int S = p_stores<TC>() + (CSM == 1 ? 4 : CSM == 2 ? 8 : 0);
+    constexpr int S = p_stores<TC>() + (CSM == 1 ? 4 : CSM == 2 ? 8 : 0) + (p_writes_bits<EPI, TX>() ? 16 : 0);
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = w >> 2, wc = w & 3;
@@ -449,11 +486,15 @@ void dispatch_p(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hipSt
     switch (epi) {
         case MSQ_EPI_NONE: dispatch_p_t<MSQ_EPI_NONE, TC, float>(g, ta, tb, s); break;
         case MSQ_EPI_BIAS: dispatch_p_t<MSQ_EPI_BIAS, TC, float>(g, ta, tb, s); break;
-        case MSQ_EPI_BIAS_RELU: dispatch_p_t<MSQ_EPI_BIAS_RELU, TC, float>(g, ta, tb, s); break;
+        case MSQ_EPI_BIAS_RELU:
+            if (aux_dtype == MSQ_MASK1 && g.aux) dispatch_p_t<MSQ_EPI_BIAS_RELU, TC, mask1_t>(g, ta, tb, s);
+            else dispatch_p_t<MSQ_EPI_BIAS_RELU, TC, float>(g, ta, tb, s);
+            break;
         case MSQ_EPI_BIAS_RESID: dispatch_p_t<MSQ_EPI_BIAS_RESID, TC, float>(g, ta, tb, s); break;
         case MSQ_EPI_BIAS_DROP_RESID: dispatch_p_t<MSQ_EPI_BIAS_DROP_RESID, TC, float>(g, ta, tb, s); break;
         case MSQ_EPI_RELU_MASK:
-            if (aux_dtype == MSQ_BF16) dispatch_p_t<MSQ_EPI_RELU_MASK, TC, bf16>(g, ta, tb, s);
+            if (aux_dtype == MSQ_MASK1) dispatch_p_t<MSQ_EPI_RELU_MASK, TC, mask1_t>(g, ta, tb, s);
+            else if (aux_dtype == MSQ_BF16) dispatch_p_t<MSQ_EPI_RELU_MASK, TC, bf16>(g, ta, tb, s);
             else dispatch_p_t<MSQ_EPI_RELU_MASK, TC, float>(g, ta, tb, s);
             break;
     }
@@ -464,12 +505,18 @@ void dispatch_p(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hipSt
 static bool p_prepare(GemmArgs& g, int ta, int tb, int epi, int c_dtype, int aux_dtype) {
     if (epi == MSQ_EPI_ACCUM || g.batch != 1) return false;
     const int esz = c_dtype == MSQ_BF16 ? 2 : 4, xsz = aux_dtype == MSQ_BF16 ? 2 : 4;
+    // MASK1: words of 32 columns (its writer needs bf16 C: the bits are of the stored values)
+    if (aux_dtype == MSQ_MASK1 && g.aux && (c_dtype != MSQ_BF16 || (epi != MSQ_EPI_RELU_MASK && epi != MSQ_EPI_BIAS_RELU)))
+        return false;
     // 16-B C pieces (bf16: 8 columns, fp32: 4), 16-B aligned rows
     if (g.N % 8 || g.ldc % 8 || ((uintptr_t)g.C % 16)) return false;
     if (g.bias && ((uintptr_t)g.bias % 16)) return false;
-    if (g.aux && (g.ldx % 4 || ((uintptr_t)g.aux % 16))) return false;
+    if (g.aux && aux_dtype != MSQ_MASK1 && (g.ldx % 4 || ((uintptr_t)g.aux % 16))) return false;
+    if (g.aux && aux_dtype == MSQ_MASK1 && ((uintptr_t)g.aux % 4)) return false;
     const int64_t cext = ((g.M - 1) * g.ldc + g.N) * esz;
-    const int64_t xext = g.aux ? ((g.M - 1) * g.ldx + g.N) * xsz : 0;
+    const int64_t xext = !g.aux ? 0
+                         : aux_dtype == MSQ_MASK1 ? ((g.M - 1) * g.ldx + (g.N + 31) / 32) * 4
+                                                  : ((g.M - 1) * g.ldx + g.N) * xsz;
     if (cext >= (int64_t)OOB || xext >= (int64_t)OOB || g.N * 4 >= (int64_t)OOB) return false;
     if (!gemm256_plan(g, ta, tb, epi) || g.ksplit != 1) return false;
     g.c_ext = (uint32_t)cext;
@@ -494,13 +541,15 @@ bool gemm256p_colsum_launch(GemmArgs g, int ta, int tb, int epi, int aux_dtype, 
     if (ta != 0 || (epi != MSQ_EPI_NONE && epi != MSQ_EPI_RELU_MASK)) return false;
     if (!p_prepare(g, ta, tb, epi, MSQ_BF16, aux_dtype)) return false;
     if ((int64_t)g.tiles_m * 2 * g.N * 4 >= (int64_t)OOB) return false;
-    const bool bx = aux_dtype == MSQ_BF16;
+    const bool bx = aux_dtype == MSQ_BF16, b1 = aux_dtype == MSQ_MASK1;
     if (tb == 0) {
         if (epi == MSQ_EPI_NONE) launch_p<0, 0, MSQ_EPI_NONE, bf16, float, 1>(g, s);
+        else if (b1) launch_p<0, 0, MSQ_EPI_RELU_MASK, bf16, mask1_t, 1>(g, s);
         else if (bx) launch_p<0, 0, MSQ_EPI_RELU_MASK, bf16, bf16, 1>(g, s);
         else launch_p<0, 0, MSQ_EPI_RELU_MASK, bf16, float, 1>(g, s);
     } else {
         if (epi == MSQ_EPI_NONE) launch_p<0, 1, MSQ_EPI_NONE, bf16, float, 1>(g, s);
+        else if (b1) launch_p<0, 1, MSQ_EPI_RELU_MASK, bf16, mask1_t, 1>(g, s);
         else if (bx) launch_p<0, 1, MSQ_EPI_RELU_MASK, bf16, bf16, 1>(g, s);
         else launch_p<0, 1, MSQ_EPI_RELU_MASK, bf16, float, 1>(g, s);
     }

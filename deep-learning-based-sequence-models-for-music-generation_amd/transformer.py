@@ -167,6 +167,11 @@ class _Acts:
         self.o = e(Lc, M, d)
         self.lse = e(Lc, B, H, S, dt=f32)
         self.h = e(Lc, M, 4 * d)
+        # the FFN ReLU mask at 1 bit per element (MSQ_MASK1, written by the FFN1
+        # forward beside h): the FFN2 dX epilogue reads 1/16 of the bytes of h
+        self.hm = (e(Lc, M, 4 * d // 32, dt=torch.int32)
+                   if save and act == torch.bfloat16 and (4 * d) % 32 == 0 and os.environ.get("MSQ_RELU_BITS", "1") != "0"
+                   else None)
         self.f = e(B * T, d)
         self.stf = e(2, B * T, dt=f32)
         self.logits = e(B * T, cfg.v_pad)
@@ -405,7 +410,8 @@ class TransformerEngine:
                      drop=pdrop)
             ops.layernorm_fwd(A.xm[k], P[f"{l}.ln2_w"], P[f"{l}.ln2_b"], out=A.c[k], mean=A.st2[k, 0],
                               rstd=A.st2[k, 1])
-            ops.gemm(A.c[k], W[f"{l}.w1"], out=A.h[k], epilogue=L.EPI_BIAS_RELU, bias=P[f"{l}.b1"])
+            ops.gemm(A.c[k], W[f"{l}.w1"], out=A.h[k], epilogue=L.EPI_BIAS_RELU, bias=P[f"{l}.b1"],
+                     aux=A.hm[k] if save and A.hm is not None else None)
             ops.gemm(A.h[k], W[f"{l}.w2"], out=xo, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.b2"], aux=A.xm[k],
                      drop=fdrop)
         x_last = A.x[cfg.n_layer] if save else A.x[cfg.n_layer % 2]
@@ -607,12 +613,13 @@ class TransformerEngine:
             on_side("gb", ffn2_w)
             before_write("dh")
             # dh = ReLU-masked FFN2 dX; the FFN1 bias gradient (its column sums) in the same epilogue
+            hmask = A.hm[l] if A.hm is not None else A.h[l]
             if Wt is not None:
-                ops.gemm_colsum(gb, Wt[f"{l}.w2"], Bw["dh"], G[f"{l}.b1"], epilogue=L.EPI_RELU_MASK, aux=A.h[l],
+                ops.gemm_colsum(gb, Wt[f"{l}.w2"], Bw["dh"], G[f"{l}.b1"], epilogue=L.EPI_RELU_MASK, aux=hmask,
                                 accumulate=True)
             else:
                 ops.gemm_colsum(gb, W[f"{l}.w2"], Bw["dh"], G[f"{l}.b1"], tb=True, epilogue=L.EPI_RELU_MASK,
-                                aux=A.h[l], accumulate=True)
+                                aux=hmask, accumulate=True)
 
             def ffn1_w(l=l):
                 ops.gemm(Bw["dh"], A.c[l], ta=True, tb=True, out=G[f"{l}.w1"], epilogue=L.EPI_ACCUM)

@@ -33,6 +33,13 @@ extern "C" {
 /* element types */
 #define MSQ_F32 0
 #define MSQ_BF16 1
+/* aux of the bf16 GEMM only: a ReLU mask at 1 bit per element, bit n % 32 of
+ * the uint32 word [m][n / 32] (ld_aux in words, one batch). With
+ * MSQ_EPI_RELU_MASK the product reads it (C = acc * bit); with
+ * MSQ_EPI_BIAS_RELU it is written: bit = (C[m][n] as stored > 0). It stands in
+ * for the bf16 post-ReLU activation as the FFN dX mask (model_transformer.py:97-100)
+ * at 1/16 of the bytes. */
+#define MSQ_MASK1 2
 
 /* GEMM epilogues */
 #define MSQ_EPI_NONE 0       /* C = acc                                   */

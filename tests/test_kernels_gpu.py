@@ -201,6 +201,52 @@ def test_gemm256_epilogues_bf16_out(route, M):
                                                                              torch.zeros(()))) < 2e-3
 
 
+def _pack_bits(h):
+    """MSQ_MASK1 reference: word [m][w] bit c = (h[m][32 w + c] > 0), as int32"""
+    M, N = h.shape
+    nw = (N + 31) // 32
+    pos = torch.zeros(M, nw * 32, dtype=torch.int64)
+    pos[:, :N] = (h.float().cpu() > 0).long()
+    words = (pos.view(M, nw, 32) << torch.arange(32)).sum(-1)
+    return ((words + 2 ** 31) % 2 ** 32 - 2 ** 31).int()
+
+
+@pytest.mark.parametrize("route", list(ROUTES))
+@pytest.mark.parametrize("M,N,K", [(3000, 4096, 1024), (65728 // 16, 1024, 256), (100, 512, 64)])
+def test_gemm_relu_bits(route, M, N, K):
+    """MSQ_MASK1: the FFN1 forward (BIAS_RELU) writes the 1-bit ReLU mask of
+    its stored bf16 output (in the persistent tile's epilogue, else one pass
+    over C) and the FFN2 dX product reads it (RELU_MASK, plain and with the
+    fused bias column sums): the mask is exact, C is unchanged, and the dX
+    outputs equal those masked by the bf16 activation itself, bitwise."""
+    g = torch.Generator().manual_seed(M + N + K + len(route))
+    a = torch.randn(M, K, generator=g).bfloat16().to(dev)
+    w = (torch.randn(N, K, generator=g) * 0.05).bfloat16().to(dev)
+    bias = torch.randn(N, generator=g).to(dev)
+    dy = torch.randn(M, K, generator=g).bfloat16().to(dev)
+    w2 = torch.randn(K, N, generator=g).bfloat16().to(dev)  # [K][N]: tb
+    with ops.gemm_route(ROUTES[route]):
+        h0 = ops.gemm(a, w, out_dtype=torch.bfloat16, epilogue=L.EPI_BIAS_RELU, bias=bias)
+        bits = torch.full((M, (N + 31) // 32 + 2), -7, device=dev, dtype=torch.int32)[:, :(N + 31) // 32]
+        h = ops.gemm(a, w, out_dtype=torch.bfloat16, epilogue=L.EPI_BIAS_RELU, bias=bias, aux=bits)
+        torch.cuda.synchronize()
+        assert torch.equal(h, h0)
+        assert torch.equal(bits.cpu(), _pack_bits(h))
+        o_ref = ops.gemm(dy, w2, tb=True, out_dtype=torch.bfloat16, epilogue=L.EPI_RELU_MASK, aux=h)
+        o = ops.gemm(dy, w2, tb=True, out_dtype=torch.bfloat16, epilogue=L.EPI_RELU_MASK, aux=bits)
+        torch.cuda.synchronize()
+        assert torch.equal(o, o_ref)
+        out_ref, out = torch.empty_like(o), torch.empty_like(o)
+        db_ref, db = torch.zeros(N, device=dev), torch.zeros(N, device=dev)
+        ops.gemm_colsum(dy, w2, out_ref, db_ref, tb=True, epilogue=L.EPI_RELU_MASK, aux=h)
+        ops.gemm_colsum(dy, w2, out, db, tb=True, epilogue=L.EPI_RELU_MASK, aux=bits)
+        torch.cuda.synchronize()
+        assert torch.equal(out, out_ref)
+        # below the 256 tile's size (and on the 128 tile's route) the columns are
+        # summed by msq_colsum, whose split rows add in a varying order
+        assert torch.equal(db, db_ref) or _rel(db, db_ref) < 1e-5
+
+
 def test_gemm_routes_bitwise_mask_and_layout():
     """The persistent tile's bf16 store widening (16-lane swaps) against the
     per-tile kernel: identical bf16 outputs, bitwise, on a shape with several
