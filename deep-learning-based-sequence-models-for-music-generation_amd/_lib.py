@@ -49,6 +49,7 @@ SIGNATURES = {
                                 _f, _p, _sz, _p]),
     "msq_relattn_decode_workspace": (_sz, [_i64, _i64, _i64]),
     "msq_midi_encode": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _p, _i64, _p, _p, _p, _p, _p]),
+    "msq_dropout_attn_table": (_i, [_f, _p]),
     "msq_dropout_attn_mask": (_i, [_p, _p, _i64, _i64, _i64, _u32, _u32, _f, _p]),
     "msq_relattn_fwd_dropout": (_i, [_i, _p, _i64, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f, _i64, _p, _p,
                                      _f, _p]),

@@ -118,3 +118,52 @@ static inline uint32_t drop_threshold(float p) {
     const double t = (double)p * 4294967296.0;
     return t <= 0.0 ? 0u : (t >= 4294967295.0 ? 0xffffffffu : (uint32_t)(t + 0.5));
 }
+
+// Attention-probability dropout (model_transformer.py:80) draws one 64-bit keep
+// word per (query row i, 64-key block jb) instead of one hash per element:
+//   key = drop_mix(drop_row(base, i) ^ ((jb + 1) * 0xc2b2ae35))
+//   k   = #{t < 64 : key >= T[t]},  T[t] = round(2^32 P(K <= t)), K ~ Binomial(64, p)
+//   k dropped keys, distinct and uniform: for s = 0 .. k-1 the n-th (from bit 0)
+//   still-kept bit is cleared, n = mulhi(drop_mix(key + (s + 1) * 0x9e3779b9), 64 - s).
+// Every element is then kept with probability 1 - p, independently (up to the
+// 2^-32 quantisation of T and of the n draws), as in nn.Dropout; a row word
+// costs 1 + k hashes (k = 0.64 on average at p = 0.01) instead of 64.
+// oracle/dropout.py (attn_keep) restates this bit-exactly.
+__host__ __device__ __forceinline__ uint32_t attn_word_key(uint32_t rowkey, uint32_t jb) {
+    return drop_mix(rowkey ^ ((jb + 1u) * 0xc2b2ae35u));
+}
+__host__ __device__ __forceinline__ uint32_t attn_drop_draw(uint32_t key, uint32_t s) {
+    return drop_mix(key + (s + 1u) * 0x9e3779b9u);
+}
+// bit index of the n-th (0-based, from bit 0) set bit of w (n < popcount(w))
+__host__ __device__ __forceinline__ int nth_set_bit(uint64_t w, uint32_t n) {
+    int pos = 0;
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        const uint32_t c = (uint32_t)__builtin_popcountll(w & ((1ull << sh) - 1));
+        if (n >= c) {
+            n -= c;
+            w >>= sh;
+            pos += sh;
+        }
+    }
+    return pos;
+}
+// host: T of attn_word_key's Binomial(64, p) draw (double recurrence, no
+// contraction, so that oracle/dropout.py's float64 numpy reproduces it exactly)
+static inline void attn_drop_table(float p, uint32_t* T) {
+#pragma clang fp contract(off)
+    const double q = (double)p;
+    const double r = q / (1.0 - q);
+    double pmf = 1.0 - q;  // (1 - q)^64 by six squarings
+    for (int i = 0; i < 6; ++i) pmf = pmf * pmf;
+    double cdf = 0.0;
+    for (int t = 0; t < 64; ++t) {
+        cdf = cdf + pmf;
+        const double sc = cdf * 4294967296.0;
+        const double rd = sc + 0.5;
+        T[t] = q <= 0.0 || rd >= 4294967295.0 ? 0xffffffffu : (uint32_t)rd;
+        pmf = pmf * (double)(64 - t);
+        pmf = pmf / (double)(t + 1);
+        pmf = pmf * r;
+    }
+}

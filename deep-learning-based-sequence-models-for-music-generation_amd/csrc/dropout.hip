@@ -9,20 +9,25 @@
 //   colmask[((bh*nb + j/64)*nb + i/64)*64 + j%64] bit i%64 = keep(i, j)   (backward: lanes own keys)
 // (as uint32 words: low word = keys / queries 0-31 of the block, high = 32-63).
 // One wave computes one 64x64 block of the causal lower block triangle: lane l
-// holds key j = 64 jb + l; per query row the 64 keep bits come out of one
-// __ballot (the row word), and each lane collects bit l of those ballots into
-// its column word. Blocks strictly above the diagonal are never read by the
-// attention kernels (every such element is masked) and are not written.
+// draws the keep word of query row 64 ib + l over keys 64 jb .. +63
+// (attn_word_key, common.h: one hash plus one per dropped key), and the 64
+// row words are bit-transposed across the wave into the column words.
+// Blocks strictly above the diagonal are never read by the attention kernels
+// (every such element is masked) and are not written.
 #include "common.h"
 
 namespace {
 
-// v_writelane_b32 (llvm.amdgcn.writelane): lane `lane` of `old` := uniform `val`
-__device__ int amdgcn_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+struct DropTable {
+    uint32_t t[64];
+};
 
 __global__ __launch_bounds__(256) void attn_mask_kernel(uint32_t* __restrict__ rowmask, uint32_t* __restrict__ colmask,
                                                         int S, int ld, int nb, int ntri, int H, uint32_t seed,
-                                                        uint32_t site0, uint32_t thr) {
+                                                        uint32_t site0, DropTable tab, int on) {
+    __shared__ uint32_t T[64];
+    if (threadIdx.x < 64) T[threadIdx.x] = tab.t[threadIdx.x];
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int task = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     const int bh = blockIdx.y;
@@ -33,17 +38,15 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(uint32_t* __restrict__ r
     while ((ib + 1) * (ib + 2) / 2 <= task) ++ib;
     const int jb = task - ib * (ib + 1) / 2;
     const uint32_t base = drop_base(seed, site0 + (uint32_t)bh);
-    const uint32_t ck = (uint32_t)(jb * 64 + lane) * 0x85ebca6bu;  // lane l: key 64 jb + l
-    // row words: query row 64 ib + ii is one ballot; its row key is wave-uniform
-    // (scalar unit), written into lane ii with v_writelane
-    uint32_t rlo = 0, rhi = 0;
-#pragma unroll 16
-    for (int ii = 0; ii < 64; ++ii) {
-        const uint32_t rki = drop_row(base, (uint32_t)(ib * 64 + ii));
-        const uint64_t bal = __ballot(drop_mix(rki ^ ck) >= thr);
-        rlo = (uint32_t)amdgcn_writelane((int)(uint32_t)bal, ii, (int)rlo);
-        rhi = (uint32_t)amdgcn_writelane((int)(uint32_t)(bal >> 32), ii, (int)rhi);
+    const uint32_t key = attn_word_key(drop_row(base, (uint32_t)(ib * 64 + lane)), (uint32_t)jb);
+    int k = 0;  // p = 0: every key kept
+    while (on && k < 64 && key >= T[k]) ++k;
+    uint64_t word = ~0ull;
+    for (int s = 0; s < k; ++s) {
+        const uint32_t n = __umulhi(attn_drop_draw(key, (uint32_t)s), 64u - (uint32_t)s);
+        word &= ~(1ull << nth_set_bit(word, n));
     }
+    const uint32_t rlo = (uint32_t)word, rhi = (uint32_t)(word >> 32);
     const uint64_t myrow = ((uint64_t)rhi << 32) | rlo;
     // column words: 64x64 bit transpose across the wave, six butterfly stages;
     // at stage s element (r, c) with r&s == 0, c&s != 0 swaps with (r+s, c-s)
@@ -83,8 +86,18 @@ extern "C" int msq_dropout_attn_mask(uint32_t* rowmask, uint32_t* colmask, int64
                   "msq_dropout_attn_mask: bad args");
     const int nb = (int)((S + 63) / 64), ntri = nb * (nb + 1) / 2;
     const dim3 grid((unsigned)((ntri + 3) / 4), (unsigned)(B * H));
+    DropTable tab;
+    attn_drop_table(p, tab.t);
     hipLaunchKernelGGL(attn_mask_kernel, grid, dim3(256), 0, (hipStream_t)stream, rowmask, colmask, (int)S,
-                       (int)msq_dropout_mask_ld(S), nb, ntri, (int)H, seed, site0, drop_threshold(p));
+                       (int)msq_dropout_mask_ld(S), nb, ntri, (int)H, seed, site0, tab, p > 0.f ? 1 : 0);
     MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}
+
+// the Binomial(64, p) thresholds of the attention keep words (host only):
+// oracle/dropout.py's table is checked against this one bit for bit
+extern "C" int msq_dropout_attn_table(float p, uint32_t* out64) {
+    MSQ_CHECK_ARG(out64 && p >= 0.f && p < 1.f, "msq_dropout_attn_table: bad args");
+    attn_drop_table(p, out64);
     return MSQ_OK;
 }

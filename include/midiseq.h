@@ -215,13 +215,19 @@ int msq_relattn_fwd(int dtype, void* out, int64_t ld_out, float* lse, const void
  * msq_dropout_mask_words(B, H, S) uint32 each (nb = ceil(S/64), bh = b*H + h):
  *   rowmask as uint64 [((bh*nb + i/64)*nb + j/64)*64 + i%64] bit j%64 = keep(i, j)
  *   colmask as uint64 [((bh*nb + j/64)*nb + i/64)*64 + j%64] bit i%64 = keep(i, j)
- * keep(i,j) = hash(seed, site0 + b*H + h, i, j) >= p*2^32 (counter-based,
- * csrc/common.h). Only the causal lower block triangle is written.
+ * The keep bits of row i over keys 64 jb .. +63 are one word drawn from the
+ * counter-based hash of (seed, site0 + b*H + h, i, jb) (csrc/common.h
+ * attn_word_key): k ~ Binomial(64, p) dropped keys at uniformly drawn distinct
+ * positions, so every element is kept with probability 1 - p independently.
+ * Only the causal lower block triangle is written.
  * msq_dropout_mask_ld(S) = 2*nb, the uint32 words of one block row.          */
 int64_t msq_dropout_mask_ld(int64_t S);
 int64_t msq_dropout_mask_words(int64_t B, int64_t H, int64_t S);
 int msq_dropout_attn_mask(uint32_t* rowmask, uint32_t* colmask, int64_t B, int64_t H, int64_t S, uint32_t seed,
                           uint32_t site0, float p, void* stream);
+/* the 64 Binomial(64, p) thresholds of that draw (host only, no device):
+ * out64[t] = round(2^32 P(K <= t)), clamped to 2^32 - 1                       */
+int msq_dropout_attn_table(float p, uint32_t* out64);
 /* msq_relattn_fwd / _bwd with dropout p on the attention probabilities: the
  * masks of msq_dropout_attn_mask; kept probabilities are scaled by 1/(1-p);
  * lse stays the undropped softmax normaliser. p = 0 = the plain entry points. */
