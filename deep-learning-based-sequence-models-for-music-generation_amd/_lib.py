@@ -74,6 +74,9 @@ SIGNATURES = {
     "msq_filtered_ce_bias_part": (_i, [_p, _p, _i64, _p, _p, _i, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
                                        _i64, _i64, _f, _p, _p, _i64, _i64, _p, _p]),
     "msq_gemm_set_route": (_i, [_i]),
+    "msq_gemm_resid_ln_workspace": (_i64, [_i, _i64, _i64, _i64, _i64, _i64]),
+    "msq_gemm_resid_ln": (_i, [_i, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _p, _p, _f, _p, _i,
+                               _i64, _p, _i64, _p]),
     "msq_ring_step": (_i, [_p, _p, _p, _p, _i, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p]),
     "msq_ring_state_bytes": (_sz, [_i64, _i64, _i64]),
     "msq_relattn_decode_pos": (_i, [_i, _p, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _f,
@@ -118,7 +121,12 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"libmidiseq.so not built ({LIB_PATH}); run __graft_entry__.build()")
         L = ctypes.CDLL(LIB_PATH)
+        # an A/B twin library (MSQ_LIB_PATH) of an older revision may lack newer
+        # entry points; the in-tree library must export every one
+        twin = "MSQ_LIB_PATH" in os.environ
         for name, (res, args) in SIGNATURES.items():
+            if twin and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -336,3 +336,152 @@ extern "C" int msq_mamba_in_proj_conv_step(void* zx, int64_t ldz, void* xc, int6
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Decode step: residual product + the next LayerNorm in the split-K reduce.
+//   C = aux + A . W^T + bias   (fp32 [M][N], the residual stream)
+//   Y = LayerNorm(C rows; gamma, beta, eps)   (the next product's input)
+// The skinny product runs split over K into fp32 partials (gemm_skinny_kernel
+// PART), and one workgroup per ROW then owns the whole row: it sums the
+// partials in slice order, adds bias and residual (epi_apply's order), stores
+// C, and normalises the row it already holds -- the LayerNorm that otherwise
+// follows as its own launch (model_transformer.py:115,119: ln2 after the
+// proj residual, the next block's ln1 / ln_f after the FFN residual).
+template <typename TY, int NC>
+__global__ __launch_bounds__(256) void skinny_reduce_ln_kernel(GemmArgs g, int ks, const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, float eps,
+                                                               TY* __restrict__ Y, int64_t ldy) {
+    __shared__ float red[2][4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t m = blockIdx.x, MN = g.M * g.N;
+    const float* X = (const float*)g.aux;
+    float* C = (float*)g.C;
+    f32x4 v[NC];
+    float s1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int64_t n = (int64_t)(c * 256 + tid) * 4;
+        v[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        if (n < g.N) {
+            f32x4 t = load4(g.ws + m * g.N + n);
+            for (int s = 1; s < ks; ++s) t += load4(g.ws + s * MN + m * g.N + n);
+            if (g.bias) t += load4(g.bias + n);
+            t += load4(X + m * g.ldx + n);
+            store4(C + m * g.ldc + n, t);
+            v[c] = t;
+            s1 += (t[0] + t[1]) + (t[2] + t[3]);
+        }
+    }
+    s1 = wave_sum(s1);
+    if (lane == 0) red[0][w] = s1;
+    __syncthreads();
+    const float mu = ((red[0][0] + red[0][1]) + (red[0][2] + red[0][3])) / (float)g.N;
+    float s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int64_t n = (int64_t)(c * 256 + tid) * 4;
+        if (n < g.N) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float z = v[c][t] - mu;
+                s2 += z * z;
+            }
+        }
+    }
+    s2 = wave_sum(s2);
+    if (lane == 0) red[1][w] = s2;
+    __syncthreads();
+    const float rs = rsqrtf(((red[1][0] + red[1][1]) + (red[1][2] + red[1][3])) / (float)g.N + eps);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int64_t n = (int64_t)(c * 256 + tid) * 4;
+        if (n < g.N) {
+            const f32x4 gm = load4(gamma + n), bt = load4(beta + n);
+            f32x4 o;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) o[t] = (v[c][t] - mu) * rs * gm[t] + bt[t];
+            store4(Y + m * ldy + n, o);
+        }
+    }
+}
+
+// K slices of the fused path: the skinny split (FFN2, K = 4096: 4), at least 2
+// (a K <= 1024 product otherwise runs the persistent kernel, whose epilogue
+// cannot see whole rows)
+static int resid_ln_ksplit(int64_t M, int64_t N, int64_t K, int64_t* kper) {
+    int ks = skinny_ksplit(M, N, K, kper);
+    if (ks <= 1) {
+        const int64_t q = SK_WAVES * 32;
+        *kper = ((K + 1) / 2 + q - 1) / q * q;
+        ks = (int)((K + *kper - 1) / *kper);
+    }
+    return ks;
+}
+static bool resid_ln_fused(int dtype, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldw, int64_t ldc,
+                           int64_t ldx, const void* A, const void* W, const float* C, const float* aux,
+                           const float* bias, const void* Y, int y_dtype, int64_t ldy) {
+    return dtype == MSQ_BF16 && M <= 64 && N % 4 == 0 && N <= 4096 && K % 8 == 0 && lda % 8 == 0 && ldw % 8 == 0 &&
+           ldc % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && (y_dtype == MSQ_BF16 || y_dtype == MSQ_F32) &&
+           ((uintptr_t)A | (uintptr_t)W | (uintptr_t)C | (uintptr_t)aux | (uintptr_t)Y) % 16 == 0 &&
+           (!bias || (uintptr_t)bias % 16 == 0);
+}
+
+extern "C" int64_t msq_gemm_resid_ln_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t lda,
+                                               int64_t ldw) {
+    // fused: the fp32 partials; otherwise msq_gemm_ex's workspace + LayerNorm mean / rstd
+    int64_t kper;
+    const int64_t fused = (int64_t)resid_ln_ksplit(M, N, K, &kper) * M * N * 4;
+    const int64_t plain = msq_gemm_workspace_size(dtype, 0, 0, M, N, K, lda, ldw, 1, MSQ_EPI_BIAS_RESID);
+    return std::max(fused, (plain + 255) / 256 * 256 + 2 * M * 4);
+}
+
+// C = aux + A . W^T + bias (fp32), Y = LayerNorm(C) (y_dtype): see
+// skinny_reduce_ln_kernel. Outside the fused shapes (M > 64, N > 4096, fp32
+// operands, ...) it runs msq_gemm_ex + msq_layernorm_fwd.
+extern "C" int msq_gemm_resid_ln(int dtype, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                                 const void* W, int64_t ldw, float* C, int64_t ldc, const float* bias,
+                                 const float* aux, int64_t ldx, const float* gamma, const float* beta, float eps,
+                                 void* Y, int y_dtype, int64_t ldy, void* ws, int64_t ws_bytes, void* stream) {
+    MSQ_CHECK_ARG(M > 0 && N > 0 && K > 0 && A && W && C && aux && gamma && beta && Y && ldc >= N && ldx >= N &&
+                      ldy >= N && lda >= K && ldw >= K,
+                  "msq_gemm_resid_ln: bad args");
+    MSQ_CHECK_ARG(ws && ws_bytes >= msq_gemm_resid_ln_workspace(dtype, M, N, K, lda, ldw) && (uintptr_t)ws % 16 == 0,
+                  "msq_gemm_resid_ln: workspace of msq_gemm_resid_ln_workspace() bytes, 16-B aligned");
+    hipStream_t s = (hipStream_t)stream;
+    if (!resid_ln_fused(dtype, M, N, K, lda, ldw, ldc, ldx, A, W, C, aux, bias, Y, y_dtype, ldy)) {
+        const int64_t plain = msq_gemm_workspace_size(dtype, 0, 0, M, N, K, lda, ldw, 1, MSQ_EPI_BIAS_RESID);
+        const int64_t off = (plain + 255) / 256 * 256;
+        int rc = msq_gemm_ex(dtype, 0, 0, M, N, K, A, lda, 0, W, ldw, 0, C, MSQ_F32, ldc, 0, 1, MSQ_EPI_BIAS_RESID,
+                             bias, aux, MSQ_F32, ldx, 0, 0u, 0u, 0.f, plain > 0 ? ws : nullptr, plain, stream);
+        if (rc != MSQ_OK) return rc;
+        float* st = (float*)((char*)ws + off);
+        MSQ_CHECK_ARG(ldy == N, "msq_gemm_resid_ln: the unfused path writes Y densely (ldy == N)");
+        return msq_layernorm_fwd(Y, y_dtype, st, st + M, C, gamma, beta, M, N, eps, 0, 0, stream);
+    }
+    GemmArgs g{};
+    g.M = M; g.N = N; g.K = K;
+    g.A = A; g.lda = lda;
+    g.B = W; g.ldb = ldw;
+    g.C = C; g.ldc = ldc;
+    g.bias = bias;
+    g.aux = aux; g.ldx = ldx;
+    g.batch = 1;
+    g.vec = 1;
+    g.ws = (float*)ws;
+    int64_t kper;
+    const int ks = resid_ln_ksplit(M, N, K, &kper);
+    g.kper = kper;
+    const int mt = (int)((M + 15) / 16);
+    launch_plain<MSQ_EPI_NONE, float, float, true>(g, mt, ks, s);
+    const int nc = (int)((N + 1023) / 1024);
+#define RL_GO(TY, NCV) \
+    hipLaunchKernelGGL((skinny_reduce_ln_kernel<TY, NCV>), dim3((unsigned)M), dim3(256), 0, s, g, ks, gamma, beta, eps, (TY*)Y, ldy)
+    if (y_dtype == MSQ_BF16) {
+        if (nc == 1) RL_GO(bf16, 1); else if (nc == 2) RL_GO(bf16, 2); else RL_GO(bf16, 4);
+    } else {
+        if (nc == 1) RL_GO(float, 1); else if (nc == 2) RL_GO(float, 2); else RL_GO(float, 4);
+    }
+#undef RL_GO
+    MSQ_LAUNCH_CHECK();
+    return MSQ_OK;
+}

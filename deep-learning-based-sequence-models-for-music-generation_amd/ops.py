@@ -96,6 +96,21 @@ def gemm_colsum(A, B, out, dbias, *, ta=False, tb=False, epilogue=L.EPI_NONE, au
     return out
 
 
+def gemm_resid_ln(A, W, out, bias, aux, gamma, beta, y, eps=1e-5):
+    """out = aux + A . W^T + bias (fp32) and y = LayerNorm(out rows) (msq_gemm_resid_ln:
+    the decode step's residual product and the next LayerNorm, the norm fused
+    into the split-K reduce for <= 64 bf16 rows)."""
+    M, K = A.shape
+    N = W.shape[0]
+    assert out.shape == (M, N) and out.dtype == torch.float32 and aux.shape == (M, N) and y.shape == (M, N)
+    nws = L.lib().msq_gemm_resid_ln_workspace(dt(A), M, N, K, A.stride(0), W.stride(0))
+    ws = workspace(nws, A.device, "resid_ln")
+    call("msq_gemm_resid_ln", dt(A), M, N, K, ptr(A), A.stride(0), ptr(W), W.stride(0), ptr(out), out.stride(0),
+         ptr(bias), ptr(aux), aux.stride(0), ptr(gamma), ptr(beta), float(eps), ptr(y), dt(y), y.stride(0), ptr(ws),
+         ws.numel(), stream())
+    return out
+
+
 def gemm_bias_colstats(A, W, out, bias, part):
     """out = A . W^T + bias (bf16; W [N, K] as nn.Linear.weight) and the
     column (max, sum exp) partials of out per 128 rows into part

@@ -487,16 +487,31 @@ class TransformerEngine:
     def _layers_step(self, x, cache, attn):
         """the per-layer body of a decode step; attn(l) runs the decode attention"""
         cfg, P, W = self.cfg, self.P, self.W
-        for l in range(cfg.n_layer):
-            ops.layernorm_fwd(x, P[f"{l}.ln1_w"], P[f"{l}.ln1_b"], out=cache.a, mean=cache.st[0], rstd=cache.st[1])
+        L_ = cfg.n_layer
+        if os.environ.get("MSQ_DECODE_RESID_LN", "1") == "0":  # A/B: the separate LayerNorm launches
+            for l in range(L_):
+                ops.layernorm_fwd(x, P[f"{l}.ln1_w"], P[f"{l}.ln1_b"], out=cache.a, mean=cache.st[0], rstd=cache.st[1])
+                ops.gemm(cache.a, W[f"{l}.wqkv"], out=cache.qkv)
+                attn(l)
+                ops.gemm(cache.o, W[f"{l}.wproj"], out=cache.xm, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.bproj"],
+                         aux=x)
+                ops.layernorm_fwd(cache.xm, P[f"{l}.ln2_w"], P[f"{l}.ln2_b"], out=cache.c, mean=cache.st[0],
+                                  rstd=cache.st[1])
+                ops.gemm(cache.c, W[f"{l}.w1"], out=cache.h, epilogue=L.EPI_BIAS_RELU, bias=P[f"{l}.b1"])
+                ops.gemm(cache.h, W[f"{l}.w2"], out=x, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.b2"], aux=cache.xm)
+            ops.layernorm_fwd(x, P["lnf_w"], P["lnf_b"], out=cache.f, mean=cache.stf[0], rstd=cache.stf[1])
+            return
+        # every LayerNorm but layer 0's ln1 comes out of the residual product before it
+        # (msq_gemm_resid_ln: the split-K reduce owns whole rows and normalises them)
+        ops.layernorm_fwd(x, P["0.ln1_w"], P["0.ln1_b"], out=cache.a, mean=cache.st[0], rstd=cache.st[1])
+        for l in range(L_):
             ops.gemm(cache.a, W[f"{l}.wqkv"], out=cache.qkv)
             attn(l)
-            ops.gemm(cache.o, W[f"{l}.wproj"], out=cache.xm, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.bproj"], aux=x)
-            ops.layernorm_fwd(cache.xm, P[f"{l}.ln2_w"], P[f"{l}.ln2_b"], out=cache.c, mean=cache.st[0],
-                              rstd=cache.st[1])
+            ops.gemm_resid_ln(cache.o, W[f"{l}.wproj"], cache.xm, P[f"{l}.bproj"], x, P[f"{l}.ln2_w"],
+                              P[f"{l}.ln2_b"], cache.c)
             ops.gemm(cache.c, W[f"{l}.w1"], out=cache.h, epilogue=L.EPI_BIAS_RELU, bias=P[f"{l}.b1"])
-            ops.gemm(cache.h, W[f"{l}.w2"], out=x, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.b2"], aux=cache.xm)
-        ops.layernorm_fwd(x, P["lnf_w"], P["lnf_b"], out=cache.f, mean=cache.stf[0], rstd=cache.stf[1])
+            nxt = (P[f"{l + 1}.ln1_w"], P[f"{l + 1}.ln1_b"], cache.a) if l + 1 < L_ else (P["lnf_w"], P["lnf_b"], cache.f)
+            ops.gemm_resid_ln(cache.h, W[f"{l}.w2"], x, P[f"{l}.b2"], cache.xm, *nxt)
 
     def _step_dev(self, tok, cache):
         """step() with every position-dependent quantity read from cache.pos_dev"""

@@ -138,6 +138,21 @@ int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, cons
                 int64_t strideC, int64_t batch, int epilogue, const float* bias, const void* aux, int aux_dtype,
                 int64_t ld_aux, int64_t stride_aux, uint32_t seed, uint32_t site, float p, void* ws,
                 int64_t ws_bytes, void* stream);
+/* Decode step: a residual product and the LayerNorm that follows it
+ * (model_transformer.py:115,119: x + proj(attn) -> ln2, x + FFN -> the next
+ * block's ln1 / ln_f at :146) in two launches instead of three:
+ *   C = aux + A . W^T + bias   (fp32 [M, N], ldc; aux fp32 ldx; bias may be NULL)
+ *   Y = LayerNorm(rows of C; gamma, beta, eps) in y_dtype (ldy)
+ * A [M, K] and W [N, K] (nn.Linear) in dtype. For M <= 64 bf16 rows the product
+ * runs split over K into fp32 partials and one workgroup per row sums them,
+ * adds bias and residual and normalises the row it holds; other shapes run
+ * msq_gemm_ex + msq_layernorm_fwd (ldy == N). ws of
+ * msq_gemm_resid_ln_workspace(...) bytes, 16-B aligned.                       */
+int64_t msq_gemm_resid_ln_workspace(int dtype, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldw);
+int msq_gemm_resid_ln(int dtype, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* W,
+                      int64_t ldw, float* C, int64_t ldc, const float* bias, const float* aux, int64_t ldx,
+                      const float* gamma, const float* beta, float eps, void* Y, int y_dtype, int64_t ldy, void* ws,
+                      int64_t ws_bytes, void* stream);
 /* Which kernel family runs the large (M > 64) bf16 products (tests / A-B
  * tools; process-wide, default from the environment at the first call):
  *   MSQ_ROUTE_DEFAULT  persistent 256 tile for the forward / dX products, the

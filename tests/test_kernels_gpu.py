@@ -452,3 +452,38 @@ def test_transpose_bf16(rows, cols, lds, ldd):
     torch.cuda.synchronize()
     assert torch.equal(dst[:, :rows], src[:, :cols].t())
     assert bool((dst[:, rows:] == 7.0).all())  # nothing written past the rows
+
+
+@pytest.mark.parametrize("M", [1, 7, 33, 64])
+@pytest.mark.parametrize("N,K", [(1024, 1024), (1024, 4096), (1000, 520), (256, 1024)])
+def test_gemm_resid_ln_matches_unfused(M, N, K):
+    """msq_gemm_resid_ln (the decode step's residual product with the next
+    LayerNorm in its split-K reduce) against msq_gemm (BIAS_RESID) +
+    msq_layernorm_fwd: the residual rows equal within fp32 summation order
+    (bitwise where both split K the same way), the normalised rows within bf16
+    rounding; and the fp32 operand path (which runs the unfused pair) exactly."""
+    g = torch.Generator().manual_seed(M * 13 + N + K)
+    a = torch.randn(M, K, generator=g).bfloat16().to(dev)
+    w = (torch.randn(N, K, generator=g) * 0.05).bfloat16().to(dev)
+    bias = torch.randn(N, generator=g).to(dev)
+    res = (torch.randn(M, N, generator=g) * 2 + 0.3).to(dev)
+    gamma, beta = (1 + 0.1 * torch.randn(N, generator=g)).to(dev), (0.1 * torch.randn(N, generator=g)).to(dev)
+    c_ref = ops.gemm(a, w, out_dtype=torch.float32, epilogue=L.EPI_BIAS_RESID, bias=bias, aux=res)
+    y_ref = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ops.layernorm_fwd(c_ref, gamma, beta, out=y_ref)
+    c = torch.full((M, N), float("nan"), device=dev)
+    y = torch.full((M, N), float("nan"), device=dev).bfloat16()
+    ops.gemm_resid_ln(a, w, c, bias, res, gamma, beta, y)
+    torch.cuda.synchronize()
+    assert _rel(c, c_ref) < 1e-5
+    if K > 1024 and K % 512 == 0:
+        assert torch.equal(c, c_ref)  # the same K slices and summation order
+    assert _rel(y.float(), y_ref.float()) < 1e-2
+    # fp32 operands: the unfused pair itself
+    af, wf = a.float(), w.float()
+    c32, y32 = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
+    ops.gemm_resid_ln(af, wf, c32, bias, res, gamma, beta, y32)
+    c32r = ops.gemm(af, wf, out_dtype=torch.float32, epilogue=L.EPI_BIAS_RESID, bias=bias, aux=res)
+    y32r, _, _ = ops.layernorm_fwd(c32r, gamma, beta)
+    torch.cuda.synchronize()
+    assert torch.equal(c32, c32r) and torch.equal(y32, y32r)
