@@ -424,6 +424,133 @@ void splitk_reduce(const GemmArgs& g, hipStream_t s) {
                        (int64_t)g.batch, g.ksplit);
 }
 
+namespace {
+// dR product (tri 2: K = nseg segments of seg rows, output row m = r needs
+// k % seg >= seg - 1 - r) on 256-row M tiles: 8 waves of the 128 tile's 64x64
+// wave tile, A = dQR^T ([K][M], two 128-column LDS halves), B = q ([K][N]).
+// Every M tile re-reads the q rows of its K range, so the 256-row tile halves
+// that traffic (1.05 GB per cfg-2 launch with 128 rows); the A operand and the
+// per-segment K ranges are as in gemm_bf16_kernel. fp32 split-K partials only
+// (ACCUM with ws), reduced by splitk_reduce.
+constexpr int TBM = 256, TNT = 512;
+__global__ __launch_bounds__(TNT, 1) void gemm_tri2_256_kernel(GemmArgs g) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tiles = g.tiles_m * g.tiles_n;
+    int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int kslice = bid % g.ksplit;
+    bid /= g.ksplit;
+    const int bz = bid / tiles;
+    bid -= bz * tiles;
+    const int tm = g.tiles_m - 1 - bid / g.tiles_n, tn = bid % g.tiles_n;  // long K ranges first
+    const int m0 = tm * TBM, n0 = tn * BN;
+    const bf16* A = (const bf16*)g.A + bz * g.sA;
+    const bf16* B = (const bf16*)g.B + bz * g.sB;
+    constexpr int SA = TBM * BK * 2, SB = BN * BK * 2, STG = SA + SB;
+    const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int64_t nseg = g.K / g.seg, spb = (nseg + g.ksplit - 1) / g.ksplit;
+    const int64_t sg_lo = (int64_t)kslice * spb, sg_hi = min<int64_t>(nseg, sg_lo + spb);
+    const int64_t imin = max<int64_t>(0, g.seg - 1 - ((int64_t)m0 + TBM - 1));
+    int64_t cs = sg_lo, ck = cs * g.seg + imin, cke = (cs + 1) * g.seg;
+    auto skip_empty = [&]() {
+        while (cs < sg_hi && ck >= cke) {
+            ++cs;
+            if (cs < sg_hi) ck = cs * g.seg + imin, cke = (cs + 1) * g.seg;
+        }
+    };
+    struct Regs { u32x4 a[4], b[2]; };
+    auto load = [&](Regs& x, int64_t k0, int64_t kend) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // A [K][M]: 64 k rows x 32 chunks (two 128-column halves)
+            const int c = tid + TNT * i, kr = (c & 1023) >> 4, ch = c & 15, half = c >> 10;
+            const int64_t gk = k0 + kr, gm = m0 + half * 128 + ch * 8;
+            // columns m >= M only feed output rows that are not stored: a chunk
+            // inside the row pitch is read whole (no element-wise edge path)
+            const int valid = (gk < kend) ? (gm + 8 <= g.lda ? 8 : (int)min<int64_t>(8, g.M - gm)) : 0;
+            x.a[i] = load_chunk(A + gk * g.lda + gm, valid);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {  // B [K][N]: 64 k rows x 16 chunks
+            const int c = tid + TNT * i, kr = c >> 4, ch = c & 15;
+            const int64_t gk = k0 + kr, gn = n0 + ch * 8;
+            const int valid = (gk < kend) ? (int)min<int64_t>(8, g.N - gn) : 0;
+            x.b[i] = load_chunk(B + gk * g.ldb + gn, valid);
+        }
+    };
+    auto store = [&](const Regs& x, char* st) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = tid + TNT * i, kr = (c & 1023) >> 4, ch = c & 15, half = c >> 10;
+            *(u32x4*)(st + half * (SA / 2) + kr * 256 + swz_mn(kr, ch) * 16) = x.a[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = tid + TNT * i, kr = c >> 4, ch = c & 15;
+            *(u32x4*)(st + SA + kr * 256 + swz_mn(kr, ch) * 16) = x.b[i];
+        }
+    };
+    auto fetch = [&](Regs& x) {
+        if (cs >= sg_hi) return false;
+        load(x, ck, cke);
+        ck += BK;
+        skip_empty();
+        return true;
+    };
+    auto mma = [&](const char* st) {
+        const char* sa = st + (wm >> 7) * (SA / 2);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 af[4], bfr[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[i] = read_frag<false>(sa, (wm & 127) + i * 16, ks, lane);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bfr[j] = read_frag<false>(st + SA, wn + j * 16, ks, lane);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        }
+    };
+    char* s0 = smem;
+    char* s1 = smem + STG;
+    Regs r0, r1;
+    skip_empty();
+    bool v0 = fetch(r0);
+    if (v0) store(r0, s0);
+    bool v1 = fetch(r1);
+    __syncthreads();
+    while (v0) {
+        const bool v2 = fetch(r0);
+        mma(s0);
+        if (v1) store(r1, s1);
+        __syncthreads();
+        if (!v1) break;
+        const bool v3 = fetch(r1);
+        mma(s1);
+        if (v2) store(r0, s0);
+        __syncthreads();
+        v0 = v2;
+        v1 = v3;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t m = m0 + wm + i * 16 + (lane & 15);
+        if (m >= g.M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t n = n0 + wn + j * 16 + 4 * (lane >> 4);
+            if (n < g.N) store4(g.ws + (((int64_t)kslice * g.batch + bz) * g.M + m) * g.N + n, acc[i][j]);
+        }
+    }
+}
+}  // namespace
+
 int gemm_bf16_tri_ksplit(int tri, int64_t M, int64_t N, int64_t K, int64_t seg, int64_t batch) {
     if (tri != 2) return 1;
     const int64_t nb = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * batch, nseg = K / seg;
@@ -455,6 +582,30 @@ int gemm_bf16_tri(int tri, int64_t seg, int ta, int tb, int64_t M, int64_t N, in
     if (epi == MSQ_EPI_ACCUM && g.ksplit > 1 && ws && c_dtype == MSQ_F32 &&
         splitk_ws_bytes(M, N, batch, g.ksplit) && ws_bytes >= splitk_ws_bytes(M, N, batch, g.ksplit))
         g.ws = ws;
+    // the dR product (fp32 C += dQR^T q): 256-row M tiles when the split-K
+    // workspace holds their partials (MSQ_TRI2_128=1: the 128 tile)
+    static const bool t128 = getenv("MSQ_TRI2_128") != nullptr;
+    if (!t128 && tri == 2 && ta == 1 && tb == 1 && epi == MSQ_EPI_ACCUM && c_dtype == MSQ_F32 && ws && N % 4 == 0) {
+        GemmArgs h = g;
+        h.tiles_m = (int)((M + TBM - 1) / TBM);
+        const int64_t nseg = K / seg, nb = (int64_t)h.tiles_m * h.tiles_n * batch;
+        // every slice a whole number of segments, none empty
+        const int64_t want = std::max<int64_t>(1, std::min<int64_t>(nseg, (2048 + nb - 1) / nb));
+        const int64_t spb = (nseg + want - 1) / want;
+        h.ksplit = (int)((nseg + spb - 1) / spb);
+        if (ws_bytes >= splitk_ws_bytes(M, N, batch, h.ksplit) && splitk_ws_bytes(M, N, batch, h.ksplit)) {
+            h.ws = ws;
+            constexpr int lds = 2 * (TBM * BK * 2 + BN * BK * 2);
+            static bool attr = false;
+            if (!attr) {
+                (void)hipFuncSetAttribute((const void*)gemm_tri2_256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                attr = true;
+            }
+            hipLaunchKernelGGL(gemm_tri2_256_kernel, dim3((unsigned)(nb * h.ksplit)), dim3(TNT), lds, s, h);
+            splitk_reduce(h, s);
+            return 0;
+        }
+    }
     const int rc = c_dtype == MSQ_BF16 ? dispatch_epi<true, bf16>(g, ta, tb, epi, aux_dtype, s)
                                        : dispatch_epi<true, float>(g, ta, tb, epi, aux_dtype, s);
     if (!rc && g.ws) splitk_reduce(g, s);
