@@ -391,6 +391,24 @@ class TransformerEngine:
             masks = A.masks(cfg, self.device)
         else:
             A.drop = None
+        # training: every layer's attention keep words drawn up front on a side
+        # stream (store-bound; they overlap the MFMA-bound forward), layer l's
+        # attention waits for its own event. The words of the previous step were
+        # last read by its backward, which precedes this point on the main stream.
+        mask_ev = None
+        if p > 0 and save and cfg.n_layer > 1 and os.environ.get("MSQ_MASK_SIDE", "1") != "0":
+            main = torch.cuda.current_stream(self.device)
+            if getattr(self, "_mask_stream", None) is None:
+                self._mask_stream = torch.cuda.Stream(self.device)
+            side = self._mask_stream
+            side.wait_stream(main)
+            mask_ev = []
+            with torch.cuda.stream(side):
+                for l in range(cfg.n_layer):
+                    ops.dropout_attn_mask(B, H, S, seed, DROP_ATTN + l * 65536, p, self.device, out=masks[l])
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    mask_ev.append(ev)
         ops.embed_fwd(A.x[0].view(B, S, d), P["tok_emb"], P["meta_emb"], idx, meta)
         for l in range(cfg.n_layer):
             k = l if save else 0
@@ -403,7 +421,10 @@ class TransformerEngine:
                 cache.v[l][:, :, :S].copy_(kv[:, :, 2].transpose(1, 2))
             adrop = pdrop = fdrop = None
             if p > 0:
-                ops.dropout_attn_mask(B, H, S, seed, DROP_ATTN + l * 65536, p, self.device, out=masks[k])
+                if mask_ev is not None:
+                    torch.cuda.current_stream(self.device).wait_event(mask_ev[l])
+                else:
+                    ops.dropout_attn_mask(B, H, S, seed, DROP_ATTN + l * 65536, p, self.device, out=masks[k])
                 adrop, pdrop, fdrop = (masks[k], p), (seed, DROP_PROJ + l, p), (seed, DROP_FFN + l, p)
             relattn_fwd(A.qkv[k], W[f"{l}.R"], B, S, H, hs, scale, out=A.o[k], lse=A.lse[k], drop=adrop)
             ops.gemm(A.o[k], W[f"{l}.wproj"], out=A.xm[k], epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.bproj"], aux=x,
