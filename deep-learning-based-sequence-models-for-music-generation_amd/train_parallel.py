@@ -68,10 +68,17 @@ class TrainStep:
     def __call__(self, src, trg, meta):
         eng, cfg = self.eng, self.eng.cfg
         B, T = src.shape
-        eng.forward(src, meta, train=self.model.training)
+        # the flat gradient is zero-filled on the Transformer forward's side
+        # stream, under the forward (MSQ_MASK_SIDE=0: on the main stream below)
+        eng.side_zero = [self.grads]
+        try:
+            eng.forward(src, meta, train=self.model.training)
+        finally:
+            eng.side_zero = None
         A = eng.acts(B, T)
         dl = eng.dlogits_buffer(B, T)
-        self.grads.zero_()
+        if not getattr(eng, "side_zeroed", False):  # else zero-filled on the forward's side stream
+            self.grads.zero_()
         # the output-bias gradient (column sums of dlogits) comes out of the loss pass
         loss, _ = ce_forward_backward(src, A.logits.view(B, T, cfg.v_pad), trg, cfg.vocab_size, self.grammar,
                                       dlogits=dl.view(B, T, cfg.v_pad), dbias=self.lm_bias_grad,

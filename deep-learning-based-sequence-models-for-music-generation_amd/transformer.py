@@ -181,6 +181,7 @@ class _Acts:
         self.colpart_valid = False
         self.gen = 0
         self._bwd = None
+        self.bwd_zeroed = False  # gres / gb zero-filled by the last training forward
         self.drop = None      # (seed, p) of the last training forward
         self._masks = None    # [L, 2, n] attention keep bits (row / col layouts)
 
@@ -395,20 +396,35 @@ class TransformerEngine:
         # stream (store-bound; they overlap the MFMA-bound forward), layer l's
         # attention waits for its own event. The words of the previous step were
         # last read by its backward, which precedes this point on the main stream.
-        mask_ev = None
-        if p > 0 and save and cfg.n_layer > 1 and os.environ.get("MSQ_MASK_SIDE", "1") != "0":
+        # The same side stream then zero-fills the backward's accumulators (the
+        # residual-stream gradient and the branch-gradient copy, plus the
+        # buffers a train step lists in `side_zero`, e.g. its flat gradient),
+        # which the end of the forward waits for.
+        mask_ev = zero_ev = None
+        A.bwd_zeroed = self.side_zeroed = False
+        zero = getattr(self, "side_zero", None) if (train and save and os.environ.get("MSQ_ZERO_SIDE") != "0") else None
+        use_side = os.environ.get("MSQ_MASK_SIDE", "1") != "0"
+        if use_side and save and ((p > 0 and cfg.n_layer > 1) or zero):
             main = torch.cuda.current_stream(self.device)
             if getattr(self, "_mask_stream", None) is None:
                 self._mask_stream = torch.cuda.Stream(self.device)
             side = self._mask_stream
             side.wait_stream(main)
-            mask_ev = []
             with torch.cuda.stream(side):
-                for l in range(cfg.n_layer):
-                    ops.dropout_attn_mask(B, H, S, seed, DROP_ATTN + l * 65536, p, self.device, out=masks[l])
-                    ev = torch.cuda.Event()
-                    ev.record(side)
-                    mask_ev.append(ev)
+                if p > 0 and cfg.n_layer > 1:
+                    mask_ev = []
+                    for l in range(cfg.n_layer):
+                        ops.dropout_attn_mask(B, H, S, seed, DROP_ATTN + l * 65536, p, self.device, out=masks[l])
+                        ev = torch.cuda.Event()
+                        ev.record(side)
+                        mask_ev.append(ev)
+                if zero:
+                    Bw = A.bwd(cfg, self.device, self.act)
+                    for t in [Bw["gres"], Bw["gb"]] + list(zero):
+                        if t is not None:
+                            t.zero_()
+                    zero_ev = torch.cuda.Event()
+                    zero_ev.record(side)
         ops.embed_fwd(A.x[0].view(B, S, d), P["tok_emb"], P["meta_emb"], idx, meta)
         for l in range(cfg.n_layer):
             k = l if save else 0
@@ -449,6 +465,9 @@ class TransformerEngine:
             A.colpart_valid = ops.gemm_bias_colstats(A.f, W["lm_w"], A.logits, P["lm_b"], A.colpart)
         if not A.colpart_valid:
             ops.gemm(A.f, W["lm_w"], out=A.logits, epilogue=L.EPI_BIAS, bias=P["lm_b"])
+        if zero_ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(zero_ev)
+            A.bwd_zeroed = self.side_zeroed = True
         if cache is not None:
             if T > cache.ctx:
                 raise ValueError(f"prefill of {T} tokens exceeds the cache context {cache.ctx}")
@@ -626,11 +645,13 @@ class TransformerEngine:
         Wt = self.transposed_weights()
         dx_gemm(dlogits, W, Wt, "lm_w", Bw["df"])
         gres = Bw["gres"]
-        gres.zero_()
         gb = Bw["gb"] if Bw["gb"] is not None else gres
         gb2 = Bw["gb2"] if ov else gb
-        if Bw["gb"] is not None:
-            gb.zero_()
+        if not A.bwd_zeroed:  # else zero-filled on the forward's side stream
+            gres.zero_()
+            if Bw["gb"] is not None:
+                gb.zero_()
+        A.bwd_zeroed = False
         # dropout: gb is the gradient INTO the dropped branch (gres masked by the
         # keep mask of the site whose output was added to the residual there);
         # the bias gradients then sum gb instead of gres
