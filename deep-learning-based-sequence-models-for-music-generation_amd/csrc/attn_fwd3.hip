@@ -39,11 +39,6 @@ constexpr float RESCALE = FWD3_RESCALE;
 #ifndef FWD3_REGSTAGE
 #define FWD3_REGSTAGE 0
 #endif
-// 1: static priority 1 for the second-dispatched half of the workgroup (waves
-// 4-7), set once before the tile loop (the arbitration loser of each SIMD's pair)
-#ifndef FWD3_PRIO
-#define FWD3_PRIO 0
-#endif
 // ablation builds (tools/build_var.sh -DFWD3_LAB=n): the LAB mask of the launched kernel
 #ifndef FWD3_LAB
 #define FWD3_LAB 0
@@ -194,7 +189,6 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
     u32x4 gk, gv, gr;
     uint32_t gm = 0u;
 #endif
-    if (FWD3_PRIO && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
     for (int kt = 0; kt < nkt; ++kt) {
         const int j0 = kt * KB, cur = kt & 1;
         // one barrier per tile: it publishes tile kt (DMA'd in the prologue,
