@@ -275,7 +275,7 @@ def test_gemm_batched_strided():
     assert _rel(out, ref) < 2e-3
 
 
-@pytest.mark.parametrize("d", [32, 128, 1024])
+@pytest.mark.parametrize("d", [32, 128, 1024, 1500, 2048])
 @pytest.mark.parametrize("ydt", [torch.float32, torch.bfloat16])
 def test_layernorm(d, ydt):
     g = torch.Generator().manual_seed(d)
