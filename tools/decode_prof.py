@@ -3,6 +3,7 @@ cached step at B=64, replayed as HIP graphs vs launched eagerly, beside the
 whole generate() iteration (sampling, host k choice, one D2H sync).
 
   python tools/decode_prof.py [mamba|transformer] [steps]"""
+import os
 import random
 import sys
 import time
@@ -32,7 +33,7 @@ def ev_time(fn, n):
 
 def main(kind="mamba", n=50):
     dev = "cuda"
-    B, T0 = 64, 1024
+    B, T0 = 64, int(os.environ.get("DP_T0", 1024))
     if kind == "mamba":
         from midiseq.mamba import Mamba
         m = Mamba(precision="bf16").to(dev)
