@@ -402,6 +402,14 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(TY* __restrict__ y, float* 
 // 512 and 4.72 at 1024 (same box, round 2).
 constexpr int LN_BWD_MAX_BLOCKS = 1024;
 static int ln_bwd_blocks() { return 768; }
+// MSQ_LN_STATIC=1: the static row schedule instead of the work queue
+static bool ln_bwd_queue() {
+    static const bool on = [] {
+        const char* e = getenv("MSQ_LN_STATIC");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
 
 // dropout keep mask applied to the copy (the gradient into the dropped branch)
 struct CopyDrop {
@@ -421,12 +429,40 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
                                                      float* __restrict__ part, const TD* __restrict__ dy,
                                                      const float* __restrict__ x, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const float* __restrict__ gamma,
-                                                     int64_t rows, int d, int64_t seg, int64_t skip, CopyDrop cd) {
+                                                     int64_t rows, int d, int64_t seg, int64_t skip, CopyDrop cd,
+                                                     int* __restrict__ ctr) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     f32x4 pg[MAXC], pb[MAXC], pc[MAXC];
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) pg[c] = pb[c] = pc[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int64_t row = blockIdx.x * 4LL + wid; row < rows; row += (int64_t)gridDim.x * 4) {
+    // row schedule: with ctr, a work queue of LNQ-row chunks per WAVE: chunk
+    // (wave id) first, then tickets nwaves + atomicAdd(ctr, 1) (lane 0,
+    // broadcast by readfirstlane, each requested one chunk ahead), so waves
+    // that start late (their CUs held by the other stream's GEMM tiles) take
+    // fewer rows instead of finishing last; without, rows blockIdx*4 + wid +
+    // k gridDim*4
+    constexpr int LNQ = 4;
+    const int nwaves = gridDim.x * 4;
+    int64_t row, rend;
+    int tk = 0;
+    if (ctr) {
+        row = (int64_t)(blockIdx.x * 4 + wid) * LNQ;
+        rend = row + LNQ;
+        if (lane == 0 && row < rows) tk = atomicAdd(ctr, 1);
+    } else {
+        row = blockIdx.x * 4LL + wid;
+        rend = rows;
+    }
+    for (;;) {
+        if (row >= rend) {
+            if (!ctr) break;
+            const int t = nwaves + __builtin_amdgcn_readfirstlane(__shfl(tk, 0, 64));
+            row = (int64_t)t * LNQ;
+            rend = row + LNQ;
+            if (lane == 0 && row < rows) tk = atomicAdd(ctr, 1);
+        }
+        if (row >= rows) break;
+        {
         const float mu = mean[row], rs = rstd[row];
         const int64_t xrow = map_row(row, seg, skip);
         f32x4 xh[MAXC], g[MAXC], acc[MAXC];
@@ -476,6 +512,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
                 if (BIAS) pc[c] += o;
             }
         }
+        }
+        row += ctr ? 1 : (int64_t)gridDim.x * 4;
     }
     // block reduce of the partials through LDS, then one row per block
     __shared__ f32x4 red[4][64 * MAXC];
@@ -543,7 +581,7 @@ __global__ __launch_bounds__(256) void ln_reduce_kernel(float* __restrict__ dg, 
 
 extern "C" size_t msq_layernorm_bwd_workspace(int64_t rows, int64_t d) {
     (void)rows;
-    return (size_t)LN_BWD_MAX_BLOCKS * 3 * d * sizeof(float);
+    return (size_t)LN_BWD_MAX_BLOCKS * 3 * d * sizeof(float) + 64;
 }
 
 template <typename TY>
@@ -571,10 +609,13 @@ template <typename TD, typename TO, bool BIAS>
 static void ln_bwd_launch_b(float* dxa, TO* dcopy, float* part, const TD* dy, const float* x, const float* mean,
                             const float* rstd, const float* gamma, int64_t rows, int d, int64_t seg, int64_t skip,
                             CopyDrop cd, hipStream_t s) {
+    // the work-queue ticket counter sits after the partials (zeroed per launch)
+    int* ctr = ln_bwd_queue() ? (int*)(part + (int64_t)LN_BWD_MAX_BLOCKS * 3 * d) : nullptr;
+    if (ctr) (void)hipMemsetAsync(ctr, 0, sizeof(int), s);
     const dim3 grid(ln_bwd_blocks());
-    if (d <= 256) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 1, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
-    else if (d <= 1024) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
-    else hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 8, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd);
+    if (d <= 256) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 1, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd, ctr);
+    else if (d <= 1024) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd, ctr);
+    else hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 8, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd, ctr);
 }
 template <typename TD, typename TO>
 static void ln_bwd_launch(float* dxa, TO* dcopy, float* part, const TD* dy, const float* x, const float* mean,
