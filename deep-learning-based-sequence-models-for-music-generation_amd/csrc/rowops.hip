@@ -402,6 +402,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(TY* __restrict__ y, float* 
 // 512 and 4.72 at 1024 (same box, round 2).
 constexpr int LN_BWD_MAX_BLOCKS = 1024;
 static int ln_bwd_blocks() { return 768; }
+// rows per work-queue ticket of the LayerNorm backward (lab: tools/build_var.sh -DLN_QROWS=n)
+#ifndef LN_QROWS
+#define LN_QROWS 4
+#endif
 // MSQ_LN_STATIC=1: the static row schedule instead of the work queue
 static bool ln_bwd_queue() {
     static const bool on = [] {
@@ -441,7 +445,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
     // that start late (their CUs held by the other stream's GEMM tiles) take
     // fewer rows instead of finishing last; without, rows blockIdx*4 + wid +
     // k gridDim*4
-    constexpr int LNQ = 4;
+    constexpr int LNQ = LN_QROWS;
     const int nwaves = gridDim.x * 4;
     int64_t row, rend;
     int tk = 0;
