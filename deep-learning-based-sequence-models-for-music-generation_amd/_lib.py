@@ -38,7 +38,7 @@ SIGNATURES = {
     "msq_gemm_ex": (_i, [_i, _i, _i, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _p, _i, _i64, _i64, _i64,
                          _i, _p, _p, _i, _i64, _i64, _u32, _u32, _f, _p, _i64, _p]),
     "msq_layernorm_bwd_bias": (_i, [_p, _p, _i, _p, _p, _p, _p, _i, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _u32, _u32,
-                                    _f, _p, _p]),
+                                    _f, _i, _p, _p]),
     "msq_layernorm_bwd_dropout": (_i, [_p, _p, _i, _p, _p, _p, _i, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _u32, _u32,
                                        _f, _p, _p]),
     "msq_dropout_mask_ld": (_i64, [_i64]),

@@ -15,7 +15,7 @@ struct AttnArgs {
     const uint32_t* colmask = nullptr;
     int64_t mask_ld = 0;
     float keep_scale = 1.f;
-    // XCD-aware block order in the flash kernels (xcd_blk3); MSQ_ATTN_NO_XCD=1 clears it
+    // XCD-aware block order in the flash kernels (xcd_blk3)
     int xcd = 1;
 };
 
@@ -48,8 +48,9 @@ size_t flash_bwd_workspace(int64_t B, int64_t S, int64_t H);
 // [H][B][S][ldr] (its j-view: row pitch ldr - 1 from element S - 1); -1 if unsupported
 int flash_bwd_kv5(const AttnArgs& a, const float* nls, const float* ndk, const bf16* dout, int64_t ldo, bf16* dqkv,
                   int64_t ldd, bf16* dqr, int64_t ldr, hipStream_t s);
-// dq = dS.K (dQR's j-view) + dQR.R into the q columns of dqkv (attn_dq.hip)
-void flash_bwd_dq(const AttnArgs& a, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd, hipStream_t s);
+// dq = dS.K (dQR's skewed view) + dQR.R into the q columns of dqkv, dQR read
+// once through an LDS ring (attn_dq.hip); -1 if unsupported
+int flash_bwd_dq(const AttnArgs& a, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd, hipStream_t s);
 // v3 forward (attn_fwd3.hip): 8 waves x 32 queries, 32-key tiles; -1 if unsupported
 int flash_fwd3(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s);
 int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo, const bf16* out, bf16* dqkv,

@@ -2,61 +2,59 @@
 // differentiated w.r.t. q):
 //   dq_i = sum_j dS_ij k_j  +  sum_j dS_ij R[S-1-i+j]
 //        = sum_j dQR[i][S-1-i+j] K[j]  +  sum_r dQR[i][r] R[r]     (r = S-1-i+j)
-// The key/value pass (attn_bwd5.hip) writes dS once, r-indexed (dQR, zero for
-// j > i inside the tiles it visits); the K term reads its j-view, i.e. the same
-// memory with row pitch ldr - 1 from element S - 1 (unaligned 16-B loads: row i
-// starts S-1-i elements into its r-row). Both products are plain
-// contractions over one K axis, so one kernel runs them back to back into the
-// same accumulators: a 128-query x 128-dim output tile per (b, h), K range
-// j in [0, i0+128) then r in [S-1-i_last rounded down to 64, S) (rows below
-// S-1-i are zero: the band the dQR writer zeroes). The metadata entries j > i
-// are added afterwards by flash_bwd_meta5_kernel.
+// The key/value pass (attn_bwd5.hip) writes dS once, r-indexed (dQR). Both
+// terms contract the SAME entries of row i, r in [S-1-i, S): the R term as
+// stored, the K term skewed (column S-1-i+j of row i pairs with key j). This
+// pass reads each dQR entry from HBM once: a 128-query tile's r-window is
+// streamed through an LDS ring, and the K term takes its skewed fragments from
+// the same ring (three 8-B reads + a per-lane funnel shift; the shift is
+// (S-1-i) mod 4, a lane constant). The metadata entries j > i are added
+// afterwards by flash_bwd_meta5_kernel.
 //
-// Tile: 256 threads = 4 waves (2x2), each 64x64 from v_mfma_f32_16x16x32_bf16;
-// operands staged global -> registers -> LDS (double buffered, one barrier per
-// 64-deep K step). A (dSj / dQR rows, K-contiguous) is read with ds_read_b128
-// from a (row>>1)&7 chunk-swizzled image; B (K / R rows = [k][d], d contiguous)
-// with ds_read_b64_tr_b16 from a 2*g(k) chunk-swizzled image (T10).
-#include "attn.h"
+// Tile: 128 queries x 128 dims of one (b, h); tiles are aligned to the END of
+// the sequence (tile 0 = the last 128 queries, the heaviest; the ragged tile
+// holds the first rows), so the r-window starts at R0 = S-1-i_last = 128 qb, a
+// multiple of the 32-wide r-block, and tile row ro (query i0 + ro) reads its
+// K term at ring column x = (127 - ro) + j.
+// Workgroup: 4 waves, two workgroups per CU. Wave 0 / 1 run the K term of
+// query half wr = 0 / 1, waves 2 / 3 the R term, each 64 queries x 128 dims
+// (v_mfma_f32_16x16x32_bf16); the partial sums meet in LDS at the end.
+// Iteration t (one barrier): the R term contracts r-block t (32 columns)
+// against R rows [R0 + 32 t, +32); the K term of half wr contracts key block
+// u = t - 4 + 2 wr, whose skewed columns lie in r-blocks t-2 .. t for both
+// halves. LDS (80 KB): a ring of 4 r-blocks (128 x 32), 4 key blocks and 2 R
+// blocks (32 x 128). The blocks of iteration t+1 are loaded into registers
+// at the top of iteration t (K-term waves: the ring block; R-term waves: the
+// key and R blocks) and written to LDS after its MFMAs.
+#include "attn_tiles.h"
 
 namespace {
+using namespace attn;
 
-constexpr int BM = 128, NT = 256, HSZ = 128;
+constexpr int NT = 256, BM = 128, BK = 32;
+constexpr int SLOT = BM * BK * 2;  // 8 KB: a ring block (128 x 32) or a key / R block (32 x 128)
+constexpr int NRING = 4, NKS = 4, NRS = 2;
+constexpr int O_RING = 0, O_K = NRING * SLOT, O_R = O_K + NKS * SLOT;
+constexpr int LDS_BYTES = O_R + NRS * SLOT;
+constexpr uint32_t OOB = 0xFFFF0000u;
+static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU");
+static_assert(2 * 32 * 64 * 16 <= LDS_BYTES, "epilogue scratch");
 
-// A rows of BK bf16: 8 chunks (BK 64, chunk ^= (row >> 1) & 7) or 4 chunks
-// (BK 32, chunk ^= (row >> 2) & 3); either way 16 rows at one chunk are conflict-free
-template <int BK>
-__device__ __forceinline__ int swz_k(int row, int chunk) {
-    return BK == 64 ? chunk ^ ((row >> 1) & 7) : chunk ^ ((row >> 2) & 3);
-}
-__device__ __forceinline__ int swz_mn(int k, int chunk) { return chunk ^ ((((k & 3) | ((k >> 1) & 4))) << 1); }
+// ring image: row ro (64 B) at ro * 64, 16-B chunk k at k ^ f(ro),
+// f = {0, 2, 3, 1}[(ro >> 2) & 3]: the R term's aligned fragment reads are
+// conflict-free (each ds_read_b128 lane group meets 16 distinct 16-B slots)
+__device__ __forceinline__ int ring_f(int ro) { return (0x78 >> (2 * ((ro >> 2) & 3))) & 3; }
+// key / R image: row k (256 B) chunk c at c ^ 2 g(k) (transposed reads, T10)
+__device__ __forceinline__ int kr_pos(int k, int c) { return c ^ ((((k & 3) | ((k >> 1) & 4))) << 1); }
 
-__device__ __forceinline__ u32x4 load_chunk(const bf16* p, int valid) {
-    if (valid >= 8) return *(const u32x4*)p;
-    union { u32x4 v; bf16 e[8]; } u;
-    u.v = (u32x4){0u, 0u, 0u, 0u};
-    for (int i = 0; i < valid; ++i) u.e[i] = p[i];
-    return u.v;
-}
-
-template <int BK>
-__device__ __forceinline__ bf16x8 frag_k(const char* s, int rb, int ks, int lane) {
-    const int row = rb + (lane & 15), ch = ks * 4 + (lane >> 4);
-    return *(const bf16x8*)(s + row * (BK * 2) + swz_k<BK>(row, ch) * 16);
-}
-__device__ __forceinline__ bf16x8 frag_mn(const char* s, int rb, int ks, int lane) {
+// B fragment (key / R rows [k][d], d contiguous) by ds_read_b64_tr_b16: lane
+// (n = lane & 15 of column block cb, k-group g) gets k = 8 g + 0..7
+__device__ __forceinline__ bf16x8 frag_b(const char* s, int cb, int lane) {
     const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
-    const int kA = ks * 32 + 8 * g + q, kB = kA + 4;
-    const int ch = (rb >> 3) + (p >> 1);
-    typedef __attribute__((address_space(3))) char lc;
-    const i16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (i16x4 __attribute__((address_space(3)))*)((lc*)s + kA * 256 + swz_mn(kA, ch) * 16 + (p & 1) * 8));
-    const i16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (i16x4 __attribute__((address_space(3)))*)((lc*)s + kB * 256 + swz_mn(kB, ch) * 16 + (p & 1) * 8));
-    union { i16x4 h[2]; bf16x8 v; } u;
-    u.h[0] = a;
-    u.h[1] = b;
-    return u.v;
+    const int kA = 8 * g + q, kB = kA + 4;
+    const int ch = (cb >> 3) + (p >> 1);
+    return cat8(tr_read(s, kA * 256 + kr_pos(kA, ch) * 16 + (p & 1) * 8),
+                tr_read(s, kB * 256 + kr_pos(kB, ch) * 16 + (p & 1) * 8));
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t dq_rsrc(const void* base, uint32_t bytes) {
@@ -67,121 +65,203 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t dq_rsrc(const void* base, uint
     return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
-// 64 KB of LDS, two workgroups per CU.
+__device__ __forceinline__ void bar() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const bf16* __restrict__ dqr, int64_t ldr,
                                                              bf16* __restrict__ dqkv, int64_t ldd) {
-    constexpr int BK = 64;
-    constexpr int A_BYTES = BM * BK * 2, B_BYTES = BK * HSZ * 2, STAGE = A_BYTES + B_BYTES;
-    constexpr int NU = BK / 16;  // 16-B chunks per thread per operand and stage
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int64_t S = a.S, H = a.H, ldq = a.ldq;
-    const int nqt = (int)((S + BM - 1) / BM);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int S = (int)a.S, H = (int)a.H;
+    const int64_t ldq = a.ldq;
     const Blk3 blk = xcd_blk3(a.xcd);
-    const int qt = nqt - 1 - blk.x;  // the longest K ranges first
-    const int64_t h = blk.y, b = blk.z;
-    const int64_t i0 = (int64_t)qt * BM, ilast = min<int64_t>(S - 1, i0 + BM - 1);
-    const int64_t rows = ((h * a.B + b) * S) * ldr;
-    const uint32_t slab = (uint32_t)(S * ldr * 2);
-    const __amdgpu_buffer_rsrc_t rR = dq_rsrc(dqr + rows, slab);
-    const bf16* B0 = (const bf16*)a.qkv + b * S * ldq + (H + h) * HSZ;
-    const bf16* B1 = (const bf16*)a.R + h * a.S_max * HSZ;
-    const int64_t ke0 = min<int64_t>(S, i0 + BM);        // j range [0, ke0)
-    const int64_t kb1 = (S - 1 - ilast) / BK * BK;       // r range [kb1, S)
-    const int n0 = (int)((ke0 + BK - 1) / BK), nt = n0 + (int)((S - kb1 + BK - 1) / BK);
-    // A-operand load u of this wave: rows 64 rb + r8 + 8 m (m = lane / 8), chunk lane % 8
-    const int m8 = lane >> 3, ch8 = lane & 7;
-    int arow[NU];
+    const int qb = blk.x;  // 0 = the last 128 queries (the longest key range)
+    const int h = blk.y, b = blk.z;
+    const int ihi = S - BM * qb, i0 = ihi - BM;  // tile rows i0 + ro, ro in [0, 128) (i0 < 0: ragged)
+    const int R0 = BM * qb;                      // S - 1 - (i0 + 127)
+    const int nk = (ihi + BK - 1) / BK;          // key blocks; also the R term's r-blocks
+    const int T = nk + 4;
+
+    const bool kterm = w < 2;
+    const int wr = w & 1;  // query half
+    const int rho = lane & 15, g = lane >> 4;
+
+    // ---- staging (global -> registers at the top of an iteration, -> LDS after its MFMAs)
+    // K-term waves: the ring block, 4 x 16 B per lane: row 64 wr + 16 n + lane / 4, chunk lane % 4
+    // R-term waves: 4 pieces of the key block and 4 of the R block: row 16 wr + 4 n + lane / 16,
+    // chunk kr_pos(row, lane % 16)
+    const __amdgpu_buffer_rsrc_t rsrc =
+        kterm ? dq_rsrc(dqr + ((int64_t)h * a.B + b) * S * ldr, (uint32_t)((int64_t)S * ldr * 2))
+              : dq_rsrc((const bf16*)a.qkv + (int64_t)b * S * ldq, (uint32_t)((int64_t)S * ldq * 2));
+    const __amdgpu_buffer_rsrc_t rR = dq_rsrc((const bf16*)a.R + (int64_t)h * a.S_max * HS, (uint32_t)(S * HS * 2));
+    uint32_t g_off[4], l_off[4];  // global byte offset at block 0, LDS offset inside the slot
+    int lim[4];                   // ring: block bi valid while 32 bi < lim; R-term waves: R offset at block 0
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
-        const int cls = wid * NU + u, r8 = cls & 7, rb = cls >> 3;
-        arow[u] = 64 * rb + r8 + 8 * m8;
+    for (int n = 0; n < 4; ++n) {
+        if (kterm) {
+            const int ro = 64 * wr + 16 * n + (lane >> 2), k = lane & 3, i = i0 + ro;
+            const bool ok = i >= 0 && i < S;
+            g_off[n] = (uint32_t)(((int64_t)(ok ? i : 0) * ldr + R0 + 8 * k) * 2);
+            l_off[n] = ro * 64 + ((k ^ ring_f(ro)) << 4);
+            lim[n] = ok ? S - (R0 + 8 * k) : 0;
+        } else {
+            const int kr = 16 * wr + 4 * n + (lane >> 4), ch = kr_pos(kr, lane & 15);
+            g_off[n] = (uint32_t)(((int64_t)kr * ldq + (int64_t)(H + h) * HS + ch * 8) * 2);  // key block 0
+            l_off[n] = kr * 256 + (lane & 15) * 16;
+            lim[n] = (R0 + kr) * HS * 2 + ch * 16;  // R block 0
+        }
     }
-
-    u32x4 ra[NU], rb[NU];
-    auto load = [&](int t) {
-        const bool s1 = t >= n0;
-        const int64_t k0 = s1 ? kb1 + (int64_t)(t - n0) * BK : (int64_t)t * BK;
-        const int64_t kend = s1 ? S : ke0;
-        const bf16* B = s1 ? B1 : B0;
-        const int64_t ldb = s1 ? HSZ : ldq;
+    u32x4 stg[8];
+    auto stage_load = [&](int t) {
+        if (kterm) {
+            const int bi = t + 1;  // ring block
 #pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            {  // A [128 rows][BK k]
-                const int64_t gi = i0 + arow[u];
-                // K term: element j of row gi's j-view = r = S-1-gi+j of its r-row
-                const int64_t c0 = s1 ? k0 : S - 1 - gi + k0;
-                const uint32_t off = gi < S ? (uint32_t)((gi * ldr + c0 + 8 * ch8) * 2) : 0xFFFF0000u;
-                ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rR, off, 0, 0);
-            }
-            {  // B [BK k][128 d]
-                const int c = tid + NT * u;
-                const int kr = c >> 4, ch = c & 15;
-                const int64_t gk = k0 + kr;
-                rb[u] = load_chunk(B + gk * ldb + ch * 8, gk < kend ? 8 : 0);
+            for (int n = 0; n < 4; ++n)
+                stg[n] = __builtin_amdgcn_raw_buffer_load_b128(
+                    rsrc, BK * bi < lim[n] ? g_off[n] + (uint32_t)(BK * bi * 2) : OOB, 0, 0);
+        } else {
+            const int u = t - 1, rt = t + 1;  // key block u, R block rt
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                stg[n] = __builtin_amdgcn_raw_buffer_load_b128(
+                    rsrc, u >= 0 && u < nk ? g_off[n] + (uint32_t)((int64_t)BK * u * ldq * 2) : OOB, 0, 0);
+                stg[4 + n] = __builtin_amdgcn_raw_buffer_load_b128(
+                    rR, rt < nk ? (uint32_t)lim[n] + (uint32_t)(BK * rt * HS * 2) : OOB, 0, 0);
             }
         }
     };
-    auto store = [&](int buf) {
-        char* sa = smem + buf * STAGE;
-        char* sb = sa + A_BYTES;
+    auto stage_store = [&](int t) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (kterm) {
+            char* dst = smem + O_RING + ((t + 1) & 3) * SLOT;
 #pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            const int row = arow[u];
-            *(u32x4*)(sa + row * (BK * 2) + swz_k<BK>(row, ch8) * 16) = ra[u];
-            const int c = tid + NT * u;
-            const int kr = c >> 4, chb = c & 15;
-            *(u32x4*)(sb + kr * 256 + swz_mn(kr, chb) * 16) = rb[u];
+            for (int n = 0; n < 4; ++n) *(u32x4*)(dst + l_off[n]) = stg[n];
+        } else {
+            char* dk = smem + O_K + ((t - 1) & 3) * SLOT;
+            char* dr = smem + O_R + ((t + 1) & 1) * SLOT;
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                *(u32x4*)(dk + l_off[n]) = stg[n];
+                *(u32x4*)(dr + l_off[n]) = stg[4 + n];
+            }
         }
     };
 
-    const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
-    f32x4 acc[4][4];
+    // ---- fragment addressing (ring rows 64 wr + 16 rf + rho; f(row) depends on rho only)
+    const int fr = ring_f(rho);
+    // K term, fragment rf of iteration t: ring element E = (127 - ro) + 32 u + 8 g with
+    // u = t - 4 + 2 wr, i.e. E = 32 t + 8 c + e, c = g - 1 - 2 rf - rho / 8, e = 7 - rho % 8:
+    // chunks c0 = 4 t + c and c0 + 1 (block t + floor(c / 4), the next one when c % 4 == 3).
+    // Three 8-B pieces from element 4 floor(E / 4) — e < 4: (c0, lo) (c0, hi) (c1, lo);
+    // e >= 4: (c0, hi) (c1, lo) (c1, hi) — then elements [e % 4, +8) of the 12:
+    // dword select by bit 1 of e, 16-bit funnel shift by bit 0.
+    const int e = 7 - (rho & 7);
+    const bool sel2 = (e & 2) != 0, hi4 = (e & 4) != 0;
+    const uint32_t sh = (uint32_t)(e & 1) * 16u;
+    int kb_hi[4], kp0[4], kp1[4];
+    bool c1wrap[4];
+#pragma unroll
+    for (int rf = 0; rf < 4; ++rf) {
+        const int ro = 64 * wr + 16 * rf + rho;
+        const int c = g - 1 - 2 * rf - (rho >> 3);  // c0 - 4 t (may be negative)
+        kb_hi[rf] = c >> 2;                       // floor
+        c1wrap[rf] = (c & 3) == 3;
+        kp0[rf] = ro * 64 + (((c & 3) ^ fr) << 4) + (hi4 ? 8 : 0);
+        kp1[rf] = ro * 64 + ((((c + 1) & 3) ^ fr) << 4);
+    }
+    // R term, fragment rf: row 64 wr + 16 rf + rho, chunk g
+    int ra[4];
+#pragma unroll
+    for (int rf = 0; rf < 4; ++rf) ra[rf] = (64 * wr + 16 * rf + rho) * 64 + ((g ^ fr) << 4);
+
+    f32x4 acc[4][8];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 8; ++j) acc[i][j] = zero4();
 
-    load(0);
-    store(0);
-    __syncthreads();
-    for (int t = 0; t < nt; ++t) {
-        const int cur = t & 1;
-        const char* sa = smem + cur * STAGE;
-        const char* sb = sa + A_BYTES;
-        const bool more = t + 1 < nt;
-        if (more) load(t + 1);
+    // prologue: ring block 0 and R block 0
+    stage_load(-1);
+    stage_store(-1);
+    bar();
+    for (int t = 0; t < T; ++t) {
+        if (t + 1 < T) stage_load(t);
+        const int u = t - 4 + 2 * wr;
+        const bool active = kterm ? (u >= 0 && u < nk) : (t < nk);
+        if (active) {
+            bf16x8 af[4];
+            if (kterm) {
 #pragma unroll
-        for (int ks = 0; ks < BK / 32; ++ks) {
-            bf16x8 af[4], bfr[4];
+                for (int rf = 0; rf < 4; ++rf) {
+                    const int blk0 = (t + kb_hi[rf]) & 3;
+                    const int blk1 = c1wrap[rf] ? ((t + kb_hi[rf] + 1) & 3) : blk0;
+                    const char* p0 = smem + O_RING + blk0 * SLOT + kp0[rf];
+                    const char* p1 = smem + O_RING + blk1 * SLOT + kp1[rf];
+                    const uint2 d0 = *(const uint2*)p0;
+                    const uint2 d1 = *(const uint2*)(hi4 ? p1 : p0 + 8);
+                    const uint2 d2 = *(const uint2*)(p1 + (hi4 ? 8 : 0));
+                    const uint32_t W[6] = {d0.x, d0.y, d1.x, d1.y, d2.x, d2.y};
+                    uint32_t X[5];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) af[i] = frag_k<64>(sa, wm + i * 16, ks, lane);
+                    for (int k = 0; k < 5; ++k) X[k] = sel2 ? W[k + 1] : W[k];
+                    const u32x4 o = {__builtin_amdgcn_alignbit(X[1], X[0], sh), __builtin_amdgcn_alignbit(X[2], X[1], sh),
+                                     __builtin_amdgcn_alignbit(X[3], X[2], sh), __builtin_amdgcn_alignbit(X[4], X[3], sh)};
+                    af[rf] = __builtin_bit_cast(bf16x8, o);
+                }
+            } else {
+                const char* sq = smem + O_RING + (t & 3) * SLOT;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bfr[j] = frag_mn(sb, wn + j * 16, ks, lane);
+                for (int rf = 0; rf < 4; ++rf) af[rf] = *(const bf16x8*)(sq + ra[rf]);
+            }
+            const char* sb = kterm ? smem + O_K + (u & 3) * SLOT : smem + O_R + (t & 1) * SLOT;
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 8; ++j) {
+                const bf16x8 bfr = frag_b(sb, 16 * j, lane);
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+                for (int rf = 0; rf < 4; ++rf) acc[rf][j] = mfma(bfr, af[rf], acc[rf][j]);
+            }
         }
-        if (more) store(cur ^ 1);
-        __syncthreads();
+        if (t + 1 < T) stage_store(t);
+        bar();  // iteration t+1's blocks written; iteration t's slots free
     }
 
+    // the R-term waves hand their sums to the K-term wave of the same half
+    f32x4* scr = (f32x4*)smem;
+    if (!kterm) {
+#pragma unroll
+        for (int rf = 0; rf < 4; ++rf)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) scr[(wr * 32 + rf * 8 + j) * 64 + lane] = acc[rf][j];
+    }
+    bar();
+    if (!kterm) return;
     // lane holds dq[i = row][d .. d+3]
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int64_t m = i0 + wm + i * 16 + (lane & 15);
-        if (m >= S) continue;
-        bf16* p = dqkv + (b * S + m) * ldd + h * HSZ;
+    for (int rf = 0; rf < 4; ++rf) {
+        const int m = i0 + 64 * wr + 16 * rf + rho;
+        if (m < 0 || m >= S) continue;
+        bf16* p = dqkv + ((int64_t)b * S + m) * ldd + (int64_t)h * HS + 4 * g;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) store4(p + wn + j * 16 + 4 * (lane >> 4), acc[i][j]);
+        for (int j = 0; j < 8; ++j) store4(p + 16 * j, acc[rf][j] + scr[(wr * 32 + rf * 8 + j) * 64 + lane]);
     }
 }
 
 }  // namespace
 
-void flash_bwd_dq(const AttnArgs& a, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd, hipStream_t s) {
+int flash_bwd_dq(const AttnArgs& a, const bf16* dqr, int64_t ldr, bf16* dqkv, int64_t ldd, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)flash_bwd_dq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS_BYTES);
+        attr = true;
+    }
+    // 32-bit buffer offsets (rows past S of the key / R blocks included)
+    if ((a.S + BK) * ldr * 2 >= (int64_t)OOB || (a.S + BK) * a.ldq * 2 >= (int64_t)OOB || ldr < a.S + 8) return -1;
     const dim3 grid((unsigned)((a.S + BM - 1) / BM), (unsigned)a.H, (unsigned)a.B);
-    hipLaunchKernelGGL(flash_bwd_dq_kernel, grid, dim3(NT), 0, s, a, dqr, ldr, dqkv, ldd);
+    hipLaunchKernelGGL(flash_bwd_dq_kernel, grid, dim3(NT), LDS_BYTES, s, a, dqr, ldr, dqkv, ldd);
+    return 0;
 }

@@ -208,11 +208,7 @@ static AttnArgs mk(int64_t B, int64_t S, int64_t H, int64_t hs, int64_t S_max, i
     AttnArgs a;
     a.B = B; a.S = S; a.H = H; a.hs = hs; a.S_max = S_max; a.n_meta = n_meta; a.scale = scale;
     a.qkv = qkv; a.ldq = ldq; a.R = R;
-    static const int xcd = [] {
-        const char* e = getenv("MSQ_ATTN_NO_XCD");
-        return e && e[0] == '1' ? 0 : 1;
-    }();
-    a.xcd = xcd;
+    a.xcd = 1;  // XCD-aware block order (xcd_blk3)
     return a;
 }
 

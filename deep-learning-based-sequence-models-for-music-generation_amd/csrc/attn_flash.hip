@@ -225,8 +225,9 @@ int flash_bwd(const AttnArgs& a, const float* lse, const bf16* dout, int64_t ldo
     // j-indexed copy cost the pass a quarter of its time: DESIGN.md §10)
     if (flash_bwd_kv5(a, nls, ndk, dout, ldo, dqkv, ldd, dqr, ldr, s))
         return msq_set_error(MSQ_ERR_UNSUPPORTED, "flash_bwd: shape outside the key/value pass (n_meta > 8 or > 4 GB)");
-    // dq (bf16, q columns of dqkv) = dS . K (dQR's j-view) + dQR . R
-    flash_bwd_dq(a, dqr, ldr, dqkv, ldd, s);
+    // dq (bf16, q columns of dqkv) = dS . K (dQR's skewed view) + dQR . R
+    if (flash_bwd_dq(a, dqr, ldr, dqkv, ldd, s))
+        return msq_set_error(MSQ_ERR_UNSUPPORTED, "flash_bwd: shape outside the query pass (> 4 GB)");
     // dR[h][r] += sum_{b,i} dQR[h][b,i][r] q_{b,i}   (batched over heads; per batch
     // segment only i >= S-1-r contributes: tri 2, split over segments)
     // (a strided-batched hipBLASLt product over the whole K range, 2x the

@@ -22,18 +22,9 @@ extern "C" int msq_colsum(float* out, int accumulate, const void* x, int dtype, 
 #include <atomic>
 
 namespace {
-// msq_gemm_set_route; -1 = not read from the environment yet
-std::atomic<int> g_route{-1};
-int gemm_route() {
-    int r = g_route.load(std::memory_order_relaxed);
-    if (r < 0) {
-        r = getenv("MSQ_GEMM128") ? MSQ_ROUTE_TILE128 : getenv("MSQ_GEMM_NOP") ? MSQ_ROUTE_TILE256 : MSQ_ROUTE_DEFAULT;
-        int expect = -1;
-        g_route.compare_exchange_strong(expect, r);
-        r = g_route.load(std::memory_order_relaxed);
-    }
-    return r;
-}
+// msq_gemm_set_route (the tests' route selector; the product runs the default)
+std::atomic<int> g_route{MSQ_ROUTE_DEFAULT};
+int gemm_route() { return g_route.load(std::memory_order_relaxed); }
 
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 
@@ -583,9 +574,8 @@ int gemm_bf16_tri(int tri, int64_t seg, int ta, int tb, int64_t M, int64_t N, in
         splitk_ws_bytes(M, N, batch, g.ksplit) && ws_bytes >= splitk_ws_bytes(M, N, batch, g.ksplit))
         g.ws = ws;
     // the dR product (fp32 C += dQR^T q): 256-row M tiles when the split-K
-    // workspace holds their partials (MSQ_TRI2_128=1: the 128 tile)
-    static const bool t128 = getenv("MSQ_TRI2_128") != nullptr;
-    if (!t128 && tri == 2 && ta == 1 && tb == 1 && epi == MSQ_EPI_ACCUM && c_dtype == MSQ_F32 && ws && N % 4 == 0) {
+    // workspace holds their partials (else the 128 tile below)
+    if (tri == 2 && ta == 1 && tb == 1 && epi == MSQ_EPI_ACCUM && c_dtype == MSQ_F32 && ws && N % 4 == 0) {
         GemmArgs h = g;
         h.tiles_m = (int)((M + TBM - 1) / TBM);
         const int64_t nseg = K / seg, nb = (int64_t)h.tiles_m * h.tiles_n * batch;

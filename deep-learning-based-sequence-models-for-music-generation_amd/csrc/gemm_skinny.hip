@@ -449,13 +449,14 @@ extern "C" int msq_gemm_resid_ln(int dtype, int64_t M, int64_t N, int64_t K, con
                   "msq_gemm_resid_ln: workspace of msq_gemm_resid_ln_workspace() bytes, 16-B aligned");
     hipStream_t s = (hipStream_t)stream;
     if (!resid_ln_fused(dtype, M, N, K, lda, ldw, ldc, ldx, A, W, C, aux, bias, Y, y_dtype, ldy)) {
+        // msq_layernorm_fwd reads C and writes Y densely: checked before anything is written
+        MSQ_CHECK_ARG(ldc == N && ldy == N, "msq_gemm_resid_ln: the unfused path needs ldc == N and ldy == N");
         const int64_t plain = msq_gemm_workspace_size(dtype, 0, 0, M, N, K, lda, ldw, 1, MSQ_EPI_BIAS_RESID);
         const int64_t off = (plain + 255) / 256 * 256;
         int rc = msq_gemm_ex(dtype, 0, 0, M, N, K, A, lda, 0, W, ldw, 0, C, MSQ_F32, ldc, 0, 1, MSQ_EPI_BIAS_RESID,
                              bias, aux, MSQ_F32, ldx, 0, 0u, 0u, 0.f, plain > 0 ? ws : nullptr, plain, stream);
         if (rc != MSQ_OK) return rc;
         float* st = (float*)((char*)ws + off);
-        MSQ_CHECK_ARG(ldy == N, "msq_gemm_resid_ln: the unfused path writes Y densely (ldy == N)");
         return msq_layernorm_fwd(Y, y_dtype, st, st + M, C, gamma, beta, M, N, eps, 0, 0, stream);
     }
     GemmArgs g{};

@@ -27,7 +27,7 @@ struct MambaArgs {
     int64_t B, L, d_inner, nheads, conv_dim, ldz;  // ldz: row stride of zxbcdt
     int64_t ldxc;                                  // row stride of the conv output (xBC)
     // chunk kernels: XCD-aware block order, the heads of one (b, chunk) on one
-    // XCD (they share the chunk's B / C rows); MSQ_MAMBA_NO_XCD=1 clears it
+    // XCD (they share the chunk's B / C rows)
     int xcd;
 };
 
@@ -929,11 +929,7 @@ MambaArgs mk(int64_t B, int64_t L, int64_t d_inner, int64_t nheads, int64_t ldz,
     MambaArgs a;
     a.B = B; a.L = L; a.d_inner = d_inner; a.nheads = nheads; a.conv_dim = d_inner + 2 * N; a.ldz = ldz;
     a.ldxc = ldxc;
-    static const int xcd = [] {
-        const char* e = getenv("MSQ_MAMBA_NO_XCD");
-        return e && e[0] == '1' ? 0 : 1;
-    }();
-    a.xcd = xcd;
+    a.xcd = 1;  // the chunk kernels walk one (b, chunk)'s heads on one XCD (chunk_of)
     return a;
 }
 

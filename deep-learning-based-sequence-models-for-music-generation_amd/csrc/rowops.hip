@@ -402,18 +402,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(TY* __restrict__ y, float* 
 // 512 and 4.72 at 1024 (same box, round 2).
 constexpr int LN_BWD_MAX_BLOCKS = 1024;
 static int ln_bwd_blocks() { return 768; }
-// rows per work-queue ticket of the LayerNorm backward (lab: tools/build_var.sh -DLN_QROWS=n)
-#ifndef LN_QROWS
-#define LN_QROWS 4
-#endif
-// MSQ_LN_STATIC=1: the static row schedule instead of the work queue
-static bool ln_bwd_queue() {
-    static const bool on = [] {
-        const char* e = getenv("MSQ_LN_STATIC");
-        return !(e && e[0] == '1');
-    }();
-    return on;
-}
+// rows per work-queue ticket of the LayerNorm backward (2 and 8 measured slower)
+constexpr int LN_QROWS = 4;
 
 // dropout keep mask applied to the copy (the gradient into the dropped branch)
 struct CopyDrop {
@@ -612,9 +602,9 @@ extern "C" int msq_layernorm_fwd(void* y, int y_dtype, float* mean, float* rstd,
 template <typename TD, typename TO, bool BIAS>
 static void ln_bwd_launch_b(float* dxa, TO* dcopy, float* part, const TD* dy, const float* x, const float* mean,
                             const float* rstd, const float* gamma, int64_t rows, int d, int64_t seg, int64_t skip,
-                            CopyDrop cd, hipStream_t s) {
+                            CopyDrop cd, bool queue, hipStream_t s) {
     // the work-queue ticket counter sits after the partials (zeroed per launch)
-    int* ctr = ln_bwd_queue() ? (int*)(part + (int64_t)LN_BWD_MAX_BLOCKS * 3 * d) : nullptr;
+    int* ctr = queue ? (int*)(part + (int64_t)LN_BWD_MAX_BLOCKS * 3 * d) : nullptr;
     if (ctr) (void)hipMemsetAsync(ctr, 0, sizeof(int), s);
     const dim3 grid(ln_bwd_blocks());
     if (d <= 256) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 1, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd, ctr);
@@ -624,9 +614,9 @@ static void ln_bwd_launch_b(float* dxa, TO* dcopy, float* part, const TD* dy, co
 template <typename TD, typename TO>
 static void ln_bwd_launch(float* dxa, TO* dcopy, float* part, const TD* dy, const float* x, const float* mean,
                           const float* rstd, const float* gamma, int64_t rows, int d, int64_t seg, int64_t skip,
-                          CopyDrop cd, bool bias, hipStream_t s) {
-    if (bias) ln_bwd_launch_b<TD, TO, true>(dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd, s);
-    else ln_bwd_launch_b<TD, TO, false>(dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd, s);
+                          CopyDrop cd, bool bias, bool queue, hipStream_t s) {
+    if (bias) ln_bwd_launch_b<TD, TO, true>(dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd, queue, s);
+    else ln_bwd_launch_b<TD, TO, false>(dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd, queue, s);
 }
 
 extern "C" int msq_layernorm_bwd(float* dx_acc, void* dx_copy, int copy_dtype, float* dgamma, float* dbeta,
@@ -643,14 +633,14 @@ extern "C" int msq_layernorm_bwd_dropout(float* dx_acc, void* dx_copy, int copy_
                                          int64_t seg_len, int64_t seg_skip, uint32_t seed, uint32_t site, float p,
                                          void* workspace, void* stream) {
     return msq_layernorm_bwd_bias(dx_acc, dx_copy, copy_dtype, dgamma, dbeta, nullptr, dy, dy_dtype, x, mean, rstd,
-                                  gamma, rows, d, seg_len, seg_skip, seed, site, p, workspace, stream);
+                                  gamma, rows, d, seg_len, seg_skip, seed, site, p, 0, workspace, stream);
 }
 
 extern "C" int msq_layernorm_bwd_bias(float* dx_acc, void* dx_copy, int copy_dtype, float* dgamma, float* dbeta,
                                       float* dbias, const void* dy, int dy_dtype, const float* x, const float* mean,
                                       const float* rstd, const float* gamma, int64_t rows, int64_t d, int64_t seg_len,
-                                      int64_t seg_skip, uint32_t seed, uint32_t site, float p, void* workspace,
-                                      void* stream) {
+                                      int64_t seg_skip, uint32_t seed, uint32_t site, float p, int schedule,
+                                      void* workspace, void* stream) {
     MSQ_CHECK_ARG(d % 4 == 0 && d <= 2048 && rows > 0 && workspace, "msq_layernorm_bwd: bad args");
     MSQ_CHECK_ARG(p >= 0.f && p < 1.f && (p == 0.f || dx_copy), "msq_layernorm_bwd: dropout needs dx_copy");
     CopyDrop cd{drop_base(seed, site), drop_threshold(p), 1.f / (1.f - p), p > 0.f ? 1 : 0};
@@ -658,13 +648,14 @@ extern "C" int msq_layernorm_bwd_bias(float* dx_acc, void* dx_copy, int copy_dty
     hipStream_t s = (hipStream_t)stream;
     float* part = (float*)workspace;
     const int di = (int)d;
-    const bool bias = dbias != nullptr;
+    const bool bias = dbias != nullptr, queue = schedule == 1;
+    MSQ_CHECK_ARG(schedule == 0 || schedule == 1, "msq_layernorm_bwd_bias: schedule must be 0 or 1");
     if (dy_dtype == MSQ_BF16) {
-        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, bias, s);
-        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, bias, s);
+        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, bias, queue, s);
+        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const bf16*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, bias, queue, s);
     } else {
-        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, bias, s);
-        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, bias, s);
+        if (copy_dtype == MSQ_BF16) ln_bwd_launch(dx_acc, (bf16*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, bias, queue, s);
+        else ln_bwd_launch(dx_acc, (float*)dx_copy, part, (const float*)dy, x, mean, rstd, gamma, rows, di, seg_len, seg_skip, cd, bias, queue, s);
     }
     const int nout = (bias ? 3 : 2) * di;
     hipLaunchKernelGGL(ln_reduce_kernel, dim3((unsigned)((nout + 63) / 64)), dim3(256), 0, s, dgamma, dbeta, dbias,

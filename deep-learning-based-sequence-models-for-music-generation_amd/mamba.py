@@ -185,10 +185,10 @@ class DecodeCache:
 
 
 class MambaEngine:
-    # decode steps replay a captured HIP graph (MSQ_NO_STEP_GRAPH=1: eager launches)
-    step_graphs = not os.environ.get("MSQ_NO_STEP_GRAPH")
+    # decode steps replay a captured HIP graph (False: eager launches; tests / profiling)
+    step_graphs = True
     # weight-gradient GEMMs of the backward on a second stream (see backward())
-    overlap_dw = os.environ.get("MSQ_SERIAL_DW") != "1"
+    overlap_dw = True
 
     def __init__(self, cfg: MambaConfig, flat):
         self.cfg = cfg
@@ -371,7 +371,7 @@ class MambaEngine:
         # GEMMs (MFMA-bound) overlap the HBM-bound gated-norm / SSD / conv
         # backward of the main stream. Shared buffers they read: gin (gxb in
         # bf16, else gx) and dzx, each overwritten one step later only after
-        # the side launch that reads it (before_write). MSQ_SERIAL_DW=1 or
+        # the side launch that reads it (before_write).
         # overlap_dw = False keeps one stream.
         sd = ops.SideStream(self.device, self.overlap_dw, hook)
 
@@ -385,7 +385,7 @@ class MambaEngine:
         gx, gxb = Bw["gx"], Bw["gxb"]
         gx.zero_()
         ops.layernorm_bwd(gx, Bw["df"], A.xlast, A.stf[0], A.stf[1], P["lnf_w"], G["lnf_w"], G["lnf_b"],
-                          seg=(T, N_META))
+                          seg=(T, N_META), ordered=True)
         sd.layer_done("head")
         # per-chunk state gradients of the bf16 SSD backward (msq_mamba_ssd_bwd_workspace)
         ssd_ws = ops.workspace(L.lib().msq_mamba_ssd_bwd_workspace(Bb, Ll, H), self.device, "ssd_bwd")

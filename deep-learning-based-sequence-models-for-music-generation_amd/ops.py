@@ -234,17 +234,20 @@ def workspace(nbytes, device, tag="ws"):
 
 
 def layernorm_bwd(dx_acc, dy, x, mean, rstd, gamma, dgamma, dbeta, dx_copy=None, seg=(0, 0), drop=None,
-                  dbias=None):
+                  dbias=None, ordered=False):
     """dx_acc[map(r)] += LN'(dy[r]); dgamma/dbeta += ...; optional copy of the updated rows
     (drop=(seed, site, p): the copy is masked by that site's dropout keep mask and scaled);
-    dbias += column sums of the written rows (the copy, else dx_acc)."""
+    dbias += column sums of the written rows (the copy, else dx_acc).
+    ordered=True: the parameter-gradient sums in a fixed order (bitwise reproducible;
+    the ln_f backward, whose beta gradient is analytically zero round-off that Adam
+    normalises); else rows from the work queue (timing decides the last bits)."""
     d = x.shape[-1]
     rows = mean.numel()
     ws = workspace(L.lib().msq_layernorm_bwd_workspace(rows, d), x.device, "ln")
     seed, site, p = drop if drop is not None else (0, 0, 0.0)
     call("msq_layernorm_bwd_bias", ptr(dx_acc), ptr(dx_copy), dt(dx_copy) if dx_copy is not None else L.F32,
          ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(dy), dt(dy), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), rows, d,
-         seg[0], seg[1], int(seed), int(site), float(p), ptr(ws), stream())
+         seg[0], seg[1], int(seed), int(site), float(p), 0 if ordered else 1, ptr(ws), stream())
 
 
 def colsum(x2d, out, accumulate=False):

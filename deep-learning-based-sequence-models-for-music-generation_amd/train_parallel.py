@@ -41,7 +41,7 @@ class TrainStep:
         self.lm_bias_grad = self.eng.layout.views(self.grads)["lm_b"][:self.eng.cfg.vocab_size]
         self.step_no = 0
         if hasattr(self.eng, "head_stats"):  # the loss's column statistics from the lm_head epilogue
-            self.eng.head_stats = os.environ.get("MSQ_NO_HEAD_STATS") != "1"
+            self.eng.head_stats = True
         self.buckets = None
         # with world > 1 the fused Adam runs per bucket, on the all-reduce side
         # stream, as each bucket's SUM arrives (MSQ_GLOBAL_ADAM=1: one Adam over
@@ -69,7 +69,7 @@ class TrainStep:
         eng, cfg = self.eng, self.eng.cfg
         B, T = src.shape
         # the flat gradient is zero-filled on the Transformer forward's side
-        # stream, under the forward (MSQ_MASK_SIDE=0: on the main stream below)
+        # stream, under the forward
         eng.side_zero = [self.grads]
         try:
             eng.forward(src, meta, train=self.model.training)

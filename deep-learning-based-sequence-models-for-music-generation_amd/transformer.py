@@ -14,7 +14,6 @@ Layout in HBM (one allocation per kind, everything resident):
 Names in state_dict() are exactly the reference's (406 keys incl. the 64
 ``tril`` buffers, which are emitted as views of ONE shared mask)."""
 import math
-import os
 from collections import OrderedDict
 from dataclasses import dataclass
 
@@ -170,8 +169,7 @@ class _Acts:
         # the FFN ReLU mask at 1 bit per element (MSQ_MASK1, written by the FFN1
         # forward beside h): the FFN2 dX epilogue reads 1/16 of the bytes of h
         self.hm = (e(Lc, M, 4 * d // 32, dt=torch.int32)
-                   if save and act == torch.bfloat16 and (4 * d) % 32 == 0 and os.environ.get("MSQ_RELU_BITS", "1") != "0"
-                   else None)
+                   if save and act == torch.bfloat16 and (4 * d) % 32 == 0 else None)
         self.f = e(B * T, d)
         self.stf = e(2, B * T, dt=f32)
         self.logits = e(B * T, cfg.v_pad)
@@ -294,7 +292,7 @@ class TransformerEngine:
         # lm_head forward emits the loss's column statistics (set by TrainStep)
         self.head_stats = False
         # weight-gradient GEMMs on a second stream in the backward (see backward())
-        self.overlap_dw = os.environ.get("MSQ_SERIAL_DW") != "1"
+        self.overlap_dw = True
 
     def bind(self, flat):
         self.flat = flat
@@ -402,9 +400,8 @@ class TransformerEngine:
         # which the end of the forward waits for.
         mask_ev = zero_ev = None
         A.bwd_zeroed = self.side_zeroed = False
-        zero = getattr(self, "side_zero", None) if (train and save and os.environ.get("MSQ_ZERO_SIDE") != "0") else None
-        use_side = os.environ.get("MSQ_MASK_SIDE", "1") != "0"
-        if use_side and save and ((p > 0 and cfg.n_layer > 1) or zero):
+        zero = getattr(self, "side_zero", None) if (train and save) else None
+        if save and ((p > 0 and cfg.n_layer > 1) or zero):
             main = torch.cuda.current_stream(self.device)
             if getattr(self, "_mask_stream", None) is None:
                 self._mask_stream = torch.cuda.Stream(self.device)
@@ -483,8 +480,8 @@ class TransformerEngine:
         return TransformerDecodeCache(self.cfg, B, context or self.cfg.block_len, self.device, self.act)
 
     # decode steps after the first replay one captured HIP graph
-    # (MSQ_NO_STEP_GRAPH=1: eager launches with host-side positions)
-    step_graphs = not os.environ.get("MSQ_NO_STEP_GRAPH")
+    # (False: eager launches with host-side positions; tests / profiling)
+    step_graphs = True
 
     @torch.no_grad()
     def step(self, tok, cache):
@@ -528,19 +525,6 @@ class TransformerEngine:
         """the per-layer body of a decode step; attn(l) runs the decode attention"""
         cfg, P, W = self.cfg, self.P, self.W
         L_ = cfg.n_layer
-        if os.environ.get("MSQ_DECODE_RESID_LN", "1") == "0":  # A/B: the separate LayerNorm launches
-            for l in range(L_):
-                ops.layernorm_fwd(x, P[f"{l}.ln1_w"], P[f"{l}.ln1_b"], out=cache.a, mean=cache.st[0], rstd=cache.st[1])
-                ops.gemm(cache.a, W[f"{l}.wqkv"], out=cache.qkv)
-                attn(l)
-                ops.gemm(cache.o, W[f"{l}.wproj"], out=cache.xm, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.bproj"],
-                         aux=x)
-                ops.layernorm_fwd(cache.xm, P[f"{l}.ln2_w"], P[f"{l}.ln2_b"], out=cache.c, mean=cache.st[0],
-                                  rstd=cache.st[1])
-                ops.gemm(cache.c, W[f"{l}.w1"], out=cache.h, epilogue=L.EPI_BIAS_RELU, bias=P[f"{l}.b1"])
-                ops.gemm(cache.h, W[f"{l}.w2"], out=x, epilogue=L.EPI_BIAS_RESID, bias=P[f"{l}.b2"], aux=cache.xm)
-            ops.layernorm_fwd(x, P["lnf_w"], P["lnf_b"], out=cache.f, mean=cache.stf[0], rstd=cache.stf[1])
-            return
         # every LayerNorm but layer 0's ln1 comes out of the residual product before it
         # (msq_gemm_resid_ln: the split-K reduce owns whole rows and normalises them)
         ops.layernorm_fwd(x, P["0.ln1_w"], P["0.ln1_b"], out=cache.a, mean=cache.st[0], rstd=cache.st[1])
@@ -626,7 +610,7 @@ class TransformerEngine:
         # Weight gradients (dW GEMMs, and the bias column sums when they read a
         # bf16 branch gradient) only feed the optimizer, not the next layer's
         # backward: with overlap_dw (the default since round 3: 87.9 -> 86.8 ms
-        # per step, same box; MSQ_SERIAL_DW=1 or overlap_dw = False keeps one
+        # per step, same box; overlap_dw = False keeps one
         # stream) they run on a second stream, overlapped
         # with the dX / LayerNorm / attention chain of the main stream. Each
         # side launch waits for the main stream's producer of its inputs; the
@@ -661,7 +645,7 @@ class TransformerEngine:
         # ln2 of layer l -> bproj of layer l
         ops.layernorm_bwd(gres, Bw["df"], A.x[cfg.n_layer], A.stf[0], A.stf[1], P["lnf_w"], G["lnf_w"], G["lnf_b"],
                           dx_copy=Bw["gb"], seg=(T, N_META), drop=dsite(DROP_FFN + cfg.n_layer - 1),
-                          dbias=G[f"{cfg.n_layer - 1}.b2"])
+                          dbias=G[f"{cfg.n_layer - 1}.b2"], ordered=True)
         layer_done("head")
         for l in reversed(range(cfg.n_layer)):
             # FFN (model_transformer.py:92-105,120)

@@ -99,11 +99,15 @@ int msq_layernorm_bwd_dropout(float* dx_acc, void* dx_copy, int copy_dtype, floa
  * unless NULL) the column sums of the rows it writes (the copy after its
  * mask, else the updated dx_acc): the bias gradient of the residual branch
  * feeding this LayerNorm (proj / FFN output biases, model_transformer.py
- * :46,101), fused instead of a separate pass over those rows.              */
+ * :46,101), fused instead of a separate pass over those rows.
+ * schedule 0: every row's contribution to dgamma / dbeta / dbias is summed
+ * in a fixed order (bitwise reproducible; msq_layernorm_bwd and _dropout use
+ * it); 1: rows are taken from a work queue, so the fp32 summation order (the
+ * last bits of those sums) depends on timing.                              */
 int msq_layernorm_bwd_bias(float* dx_acc, void* dx_copy, int copy_dtype, float* dgamma, float* dbeta, float* dbias,
                            const void* dy, int dy_dtype, const float* x, const float* mean, const float* rstd,
                            const float* gamma, int64_t rows, int64_t d, int64_t seg_len, int64_t seg_skip,
-                           uint32_t seed, uint32_t site, float p, void* workspace, void* stream);
+                           uint32_t seed, uint32_t site, float p, int schedule, void* workspace, void* stream);
 /* ---- GEMM (nn.Linear fwd/bwd: model_transformer.py:46,57-59,97-100,147;
  * Mamba2 in_proj/out_proj). C[b] = op(A[b]) . op(B[b]) with
  *   ta = 0: A stored [M,K] (K contiguous)     ta = 1: A stored [K,M]

@@ -136,7 +136,10 @@ def _main_rccl1(kind, out):
     torch.manual_seed(0)
     model = build_model(kind).to(torch.device("cuda", local))
     start = model.flat.data.clone()
-    step = TrainStep(model, ddp=True)
+    # the mamba case takes the bucket path from MSQ_DDP_BUCKETS=1 (set by the
+    # test: bench.py under torch.distributed.run with one rank), the
+    # transformer case from the argument
+    step = TrainStep(model, ddp=None if os.environ.get("MSQ_DDP_BUCKETS") == "1" else True)
     assert step.buckets is not None and step.buckets.force and step.eng.layer_grad_ready is not None
     src, trg, meta = (t[0:2].cuda() for t in full_batch())
     ref, m, v = model.flat.data.clone(), torch.zeros_like(start), torch.zeros_like(start)

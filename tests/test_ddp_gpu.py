@@ -108,7 +108,7 @@ def test_rccl_world1_bucket_path(kind, tmp_path):
     collective, or never, or twice, breaks this), and the gradients equal a
     bucket-free TrainStep's up to the backward's atomics noise.
     Reference: train_parallel.py:144-151 (init_process_group nccl, DDP)."""
-    a = _run_world2(kind, "rccl1", tmp_path, nproc=1)
+    a = _run_world2(kind, "rccl1", tmp_path, nproc=1, env={"MSQ_DDP_BUCKETS": "1"} if kind == "mamba" else None)
     assert str(a["backend"]) == "nccl"
     assert np.array_equal(a["flat"], a["ref"])
     assert np.array_equal(a["m"], a["m_ref"]) and np.array_equal(a["v"], a["v_ref"])

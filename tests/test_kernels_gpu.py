@@ -299,6 +299,19 @@ def test_layernorm(d, ydt):
     assert _rel(acc - 1, xr.grad) < 1e-5
     assert _rel(dg, gr.grad) < 1e-5 and _rel(db, br.grad) < 1e-5
     assert _rel(cp.float(), acc) < 1e-2
+    # the fixed-order schedule (ln_f, ordered=True) against the same reference,
+    # and bitwise equal from one launch to the next
+    outs = []
+    for _ in range(2):
+        acc2 = torch.ones(rows, d, device=dev)
+        dg2, db2, dbias2 = (torch.zeros(d, device=dev) for _ in range(3))
+        ops.layernorm_bwd(acc2, dy.to(dev), x.to(dev), mean, rstd, gamma.to(dev), dg2, db2, dbias=dbias2, ordered=True)
+        outs.append((acc2, dg2, db2, dbias2))
+    acc2, dg2, db2, dbias2 = outs[0]
+    assert _rel(acc2 - 1, xr.grad) < 1e-5
+    assert _rel(dg2, gr.grad) < 1e-5 and _rel(db2, br.grad) < 1e-5
+    assert _rel(dbias2, acc2.sum(0).cpu()) < 1e-5
+    assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[1]))
 
 
 def test_embedding():

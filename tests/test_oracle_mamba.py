@@ -10,6 +10,7 @@ import torch
 from oracle import loss as oloss
 from oracle import mamba2 as om
 from oracle.fill import REAL, hash_uniform
+from golden_check import check_grad
 
 G = Path(__file__).parent / "golden"
 
@@ -37,6 +38,7 @@ def test_mamba_fwd_bwd_matches_golden(chunked):
     np.testing.assert_allclose((logits.detach() @ P).numpy(), g5["logits_proj"], rtol=1e-3, atol=1e-3)
     np.testing.assert_allclose(logits.detach()[:, [0, 149, 299]].numpy(), g5["logits_rows"], rtol=1e-4, atol=1e-4)
     for k, t in p.items():
-        gf = t.grad.reshape(-1).double()
-        ref = g5[f"gsum:{k}"]
-        assert abs(gf.abs().sum().item() - ref[1]) <= 2e-3 * abs(ref[1]) + 1e-6, (k, gf.abs().sum().item(), ref[1])
+        if k in ("norm.bias", "output_layer.bias"):  # analytically zero (shift invariance along T)
+            assert t.grad.abs().max().item() < 1e-4 * p["output_layer.weight"].grad.abs().max().item(), k
+            continue
+        check_grad(k, t.grad.numpy(), g5[f"gsum:{k}"], g5[f"gpick:{k}"], 2e-3)

@@ -12,7 +12,9 @@ filtered-logit row, and the two top-k index sets (k replayed from the same RNG
 stream) are compared. Also checked: the token the engine sampled is the
 inverse-CDF pick over ITS OWN top-k with that step's uniform.
 Shape: the smallest bf16 flash-path model (hs = 128) with the reference
-vocabulary; G4's own shapes (hs = 16) have no bf16 path."""
+vocabulary; G4's own shapes (hs = 16) have no bf16 path. 12 rows x 56 steps
+= 672 draws (past block_len, so the window slides), so the 0.99 bar allows
+six near-ties rather than one."""
 import random
 
 import numpy as np
@@ -30,7 +32,7 @@ RATE_MIN = 0.99
 
 def test_bf16_topk_sets_agree_with_fp32_oracle():
     hp = dict(n_embd=256, n_heads=2, n_layer=2, block_len=64)
-    B, T0, steps, mv = 6, 40, 24, 568
+    B, T0, steps, mv = 12, 40, 56, 568  # 672 (row, step) draws; the window slides past block_len
     cfg = TransformerConfig(vocab_size=REAL.size, metadata_vocab_size=mv, precision="bf16", dropout=0.0, **hp)
     m = Transformer(cfg).to("cuda").eval()
     shapes = otr.param_shapes(hp["n_embd"], hp["n_heads"], hp["n_layer"], hp["block_len"], REAL.size, mv)
@@ -40,7 +42,7 @@ def test_bf16_topk_sets_agree_with_fp32_oracle():
     src = torch.from_numpy(np.stack([grammar_tokens(rng, REAL, T0) for _ in range(B)]))
     meta = torch.tensor([[519, 279, 202, 202, 202, 178], [432, 277, 202, 202, 202, 173],
                          [437, 279, 272, 202, 202, 180], [452, 272, 202, 202, 202, 184],
-                         [508, 272, 202, 202, 202, 184], [519, 279, 202, 202, 202, 178]])
+                         [508, 272, 202, 202, 202, 184], [519, 279, 202, 202, 202, 178]]).repeat(2, 1)
     us = np.random.default_rng(11).random(B * steps).tolist()
     seqs = np.array(generate(m, hp["block_len"], src, meta, num_tokens=steps, rng=random.Random(5),
                              uniforms=iter(us)))

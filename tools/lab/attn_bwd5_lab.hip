@@ -5,8 +5,8 @@
 //   dS_ij = P_ij (dO_i.v_j m_ij ks - D_i) scale,   D_i = dO_i.O_i
 //   dV_j  = ks sum_i P_ij m_ij dO_i,  dK_j = sum_i dS_ij q_i   (accumulated here)
 //   (m_ij the dropout keep bit, ks = 1/(1-p); m = 1, ks = 1 without dropout)
-//   dS written once, r-indexed, dQR[h][b][i][r = S-1-i+j] (the dq kernel and
-//   the dR product read it).
+//   dS written r-indexed, dQR[h][b][i][r = S-1-i+j] (the dq kernel reads its
+//   j-view, the dR product its r-view), and j-indexed (dSj, dq's K term).
 //   The metadata-block entries j > i (i < j < n_meta: keys every query sees)
 //   are masked here like the rest of the upper triangle; flash_bwd_meta_kernel
 //   adds their dK / dV / dq / dR terms.
@@ -58,10 +58,12 @@ constexpr int LDS_BYTES = O_T + 2 * T_BYTES;
 // R 2), then the dS row stores (2, or 4 with the j-indexed copy)
 constexpr int NDMA = 7;
 constexpr uint32_t OOB = 0xFFFF0000u;
+#ifndef KV_STORE_AUX
 // cache policy of the dS row stores: nt (2.16 GB per layer streamed through
 // L2 evicted the staging reads' lines): kv 1578 -> 1498 us, and the dq pass
 // that reads them back 795 -> 763 us (same box)
-constexpr int STORE_AUX = 2;
+#define KV_STORE_AUX 2
+#endif
 static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 
 template <typename F, int... I>
@@ -91,7 +93,11 @@ __device__ __forceinline__ void bar() {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 }
+#ifndef KV5_NOSB
 #define SB() __builtin_amdgcn_sched_barrier(0)
+#else
+#define SB() ((void)0)
+#endif
 
 // MFMAs as asm statements so the register classes stay fixed (AGPRs: dK^T /
 // dV^T and the K / V operands; VGPRs: the per-tile S, dP, QR accumulators that
@@ -135,7 +141,9 @@ __device__ __forceinline__ void mfma_init_va(f32x16& acc, bf16x8 a, const bf16x8
 // the softmax of 16 gaps into 3 (one gap carried 71 VALU and 8 v_exp).
 template <typename T>
 __device__ __forceinline__ void pin(T& x) {
+#ifndef KV_NOPIN
     asm volatile("" : "+v"(x));
+#endif
 }
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
     const bf16x2 v = (bf16x2){(bf16)a, (bf16)b};
@@ -166,7 +174,11 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
                                                               const bf16* __restrict__ dout, int64_t ldo,
                                                               bf16* __restrict__ dqkv, int64_t ldd,
                                                               bf16* __restrict__ dqr, int64_t ldr) {
-    constexpr int NST = 2;  // dS row stores per wave and iteration (r-indexed)
+#ifndef KV_ABL_NOSTORE
+    constexpr int NST = 2;  // dS row stores per wave and iteration (r-indexed; the dq pass reads the j-view)
+#else
+    constexpr int NST = 0;  // (ablation build: no dS stores)
+#endif
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sR = smem + O_R;
     const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, c32 = lane & 31;
@@ -322,7 +334,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
         // keys j0.. start at r = S-1-i+j0
         const __amdgpu_buffer_rsrc_t rqr = make_rsrc(qr_rows, ds_bytes);
         __builtin_amdgcn_raw_buffer_store_b128(v, rqr, valid ? st_r[k] + (uint32_t)ip * (uint32_t)(ldr2 - 2) : OOB, 0,
-                                               STORE_AUX);
+                                               KV_STORE_AUX);
     };
 
     // skew: register e of lane c32 takes the window value from lane
@@ -379,7 +391,11 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
         pin(x1);
         const float sel = __uint_as_float((__float_as_uint(x0) & skm[e]) | (__float_as_uint(x1) & ~skm[e]));
         float r;
+#ifndef KV_ABL_NOSKEW
         asm volatile("ds_bpermute_b32 %0, %1, %2" : "=v"(r) : "v"(ska[e]), "v"(sel));
+#else
+        r = sel;
+#endif
         bp[e] = r;
     };
     // row constants of tile T as the initial accumulators (register e = row
@@ -413,8 +429,14 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
         asm volatile("" : "+v"(rof[0]), "+v"(rof[1]), "+v"(tb[0]), "+v"(tb[1]), "+v"(ltid), "+v"(ljk), "+v"(lhh),
                      "+v"(lc32));
         // tile t+1's data: issued DEPTH iterations ago
+#ifndef KV_ABL_NODMA
         if (t >= DEPTH) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST + (NDMA + NST) * (DEPTH - 1)) : "memory");
+#endif
+#ifndef KV_ABL_NOBAR
         bar();  // tile t+1 landed everywhere; tile t-1's buffers and dS(t-1) staging published
+#else
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
         float pv[16], dsv[16];
         uint32_t pw[8], dw[8];  // bf16 pairs (rows e, e+1 of the lane's key) of P and dS
         // stage a: P ks scale = exp2(c2 (s' + bp) + lks), -inf where masked;
@@ -499,9 +521,13 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kv5_kernel(AttnArgs a, const 
                 if constexpr (g == 11) Lrow = row_consts(T, 0);
                 if constexpr (g >= 13) lds1(g - 13);
             }
+#ifndef KV_ABL_NODMA
             if constexpr (g < NDMA) dma_piece(g, t + 1 + DEPTH);
+#endif
+#ifndef KV_ABL_NOSTORE
             if constexpr (g == 1 || g == 2) stv[g - 1] = store_read(g - 1, sb ^ 1);
             if constexpr (g == NDMA || g == NDMA + 1) store_piece(g - NDMA, stv[g - NDMA], i0 - QT, t >= 1);
+#endif
             if constexpr (g >= 2) stage_a(std::integral_constant<int, g - 2>{});
             if constexpr (g >= 14) stage_a(std::integral_constant<int, g>{});
             if constexpr (g >= 6) stage_b(std::integral_constant<int, g - 6>{});
