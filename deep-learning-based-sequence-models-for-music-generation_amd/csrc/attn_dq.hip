@@ -90,66 +90,41 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
     const int wr = w & 1;  // query half
     const int rho = lane & 15, g = lane >> 4;
 
-    // ---- staging (global -> registers at the top of an iteration, -> LDS after its MFMAs)
-    // K-term waves: the ring block, 4 x 16 B per lane: row 64 wr + 16 n + lane / 4, chunk lane % 4
-    // R-term waves: 4 pieces of the key block and 4 of the R block: row 16 wr + 4 n + lane / 16,
-    // chunk kr_pos(row, lane % 16)
-    const __amdgpu_buffer_rsrc_t rsrc =
-        kterm ? dq_rsrc(dqr + ((int64_t)h * a.B + b) * S * ldr, (uint32_t)((int64_t)S * ldr * 2))
-              : dq_rsrc((const bf16*)a.qkv + (int64_t)b * S * ldq, (uint32_t)((int64_t)S * ldq * 2));
+    // ---- staging: every wave moves a quarter of each block, global -> registers
+    // -> LDS. Iteration t loads key block t-1 and R block t+1 (written to LDS at
+    // its end) and ring block t+2 (written one iteration later: the dQR stream
+    // is the HBM one, so it gets two iterations of latency). Per lane: ring rows
+    // 32 w + 16 n + lane / 4, chunk lane % 4; key / R rows 8 w + 4 n + lane / 16,
+    // chunk kr_pos(row, lane % 16) (n = 0, 1).
+    const __amdgpu_buffer_rsrc_t rQ =
+        dq_rsrc(dqr + ((int64_t)h * a.B + b) * S * ldr, (uint32_t)((int64_t)S * ldr * 2));
+    const __amdgpu_buffer_rsrc_t rK = dq_rsrc((const bf16*)a.qkv + (int64_t)b * S * ldq, (uint32_t)((int64_t)S * ldq * 2));
     const __amdgpu_buffer_rsrc_t rR = dq_rsrc((const bf16*)a.R + (int64_t)h * a.S_max * HS, (uint32_t)(S * HS * 2));
-    uint32_t g_off[4], l_off[4];  // global byte offset at block 0, LDS offset inside the slot
-    int lim[4];                   // ring: block bi valid while 32 bi < lim; R-term waves: R offset at block 0
+    uint32_t q_off[2], k_off[2], r_off[2];  // global byte offsets at block 0
+    int q_lds[2], kr_lds[2], q_lim[2];      // LDS offsets in a slot; ring block bi valid while 32 bi < q_lim
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-        if (kterm) {
-            const int ro = 64 * wr + 16 * n + (lane >> 2), k = lane & 3, i = i0 + ro;
-            const bool ok = i >= 0 && i < S;
-            g_off[n] = (uint32_t)(((int64_t)(ok ? i : 0) * ldr + R0 + 8 * k) * 2);
-            l_off[n] = ro * 64 + ((k ^ ring_f(ro)) << 4);
-            lim[n] = ok ? S - (R0 + 8 * k) : 0;
-        } else {
-            const int kr = 16 * wr + 4 * n + (lane >> 4), ch = kr_pos(kr, lane & 15);
-            g_off[n] = (uint32_t)(((int64_t)kr * ldq + (int64_t)(H + h) * HS + ch * 8) * 2);  // key block 0
-            l_off[n] = kr * 256 + (lane & 15) * 16;
-            lim[n] = (R0 + kr) * HS * 2 + ch * 16;  // R block 0
-        }
+    for (int n = 0; n < 2; ++n) {
+        const int ro = 32 * w + 16 * n + (lane >> 2), k = lane & 3, i = i0 + ro;
+        const bool ok = i >= 0 && i < S;
+        q_off[n] = (uint32_t)(((int64_t)(ok ? i : 0) * ldr + R0 + 8 * k) * 2);
+        q_lds[n] = ro * 64 + ((k ^ ring_f(ro)) << 4);
+        q_lim[n] = ok ? S - (R0 + 8 * k) : 0;
+        const int kr = 8 * w + 4 * n + (lane >> 4), ch = kr_pos(kr, lane & 15);
+        k_off[n] = (uint32_t)(((int64_t)kr * ldq + (int64_t)(H + h) * HS + ch * 8) * 2);
+        r_off[n] = (uint32_t)(((R0 + kr) * HS + ch * 8) * 2);
+        kr_lds[n] = kr * 256 + (lane & 15) * 16;
     }
-    u32x4 stg[8];
-    auto stage_load = [&](int t) {
-        if (kterm) {
-            const int bi = t + 1;  // ring block
-#pragma unroll
-            for (int n = 0; n < 4; ++n)
-                stg[n] = __builtin_amdgcn_raw_buffer_load_b128(
-                    rsrc, BK * bi < lim[n] ? g_off[n] + (uint32_t)(BK * bi * 2) : OOB, 0, 0);
-        } else {
-            const int u = t - 1, rt = t + 1;  // key block u, R block rt
-#pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                stg[n] = __builtin_amdgcn_raw_buffer_load_b128(
-                    rsrc, u >= 0 && u < nk ? g_off[n] + (uint32_t)((int64_t)BK * u * ldq * 2) : OOB, 0, 0);
-                stg[4 + n] = __builtin_amdgcn_raw_buffer_load_b128(
-                    rR, rt < nk ? (uint32_t)lim[n] + (uint32_t)(BK * rt * HS * 2) : OOB, 0, 0);
-            }
-        }
-    };
-    auto stage_store = [&](int t) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (kterm) {
-            char* dst = smem + O_RING + ((t + 1) & 3) * SLOT;
-#pragma unroll
-            for (int n = 0; n < 4; ++n) *(u32x4*)(dst + l_off[n]) = stg[n];
-        } else {
-            char* dk = smem + O_K + ((t - 1) & 3) * SLOT;
-            char* dr = smem + O_R + ((t + 1) & 1) * SLOT;
-#pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                *(u32x4*)(dk + l_off[n]) = stg[n];
-                *(u32x4*)(dr + l_off[n]) = stg[4 + n];
-            }
-        }
-    };
+    u32x4 sq0[2], sq1[2], sk[2], sr[2];  // ring (one iteration ahead, two ahead), key, R
+#define DQ_LOAD_RING(dst, bi)                                                                                  \
+    _Pragma("unroll") for (int n = 0; n < 2; ++n) dst[n] = __builtin_amdgcn_raw_buffer_load_b128(             \
+        rQ, BK * (bi) < q_lim[n] ? q_off[n] + (uint32_t)(BK * (bi) * 2) : OOB, 0, 0)
+#define DQ_LOAD_KR(u, rt)                                                                                      \
+    _Pragma("unroll") for (int n = 0; n < 2; ++n) {                                                            \
+        sk[n] = __builtin_amdgcn_raw_buffer_load_b128(                                                         \
+            rK, (u) >= 0 && (u) < nk ? k_off[n] + (uint32_t)((int64_t)BK * (u) * ldq * 2) : OOB, 0, 0);        \
+        sr[n] = __builtin_amdgcn_raw_buffer_load_b128(rR, (rt) < nk ? r_off[n] + (uint32_t)(BK * (rt) * HS * 2) : OOB, \
+                                                      0, 0);                                                   \
+    }
 
     // ---- fragment addressing (ring rows 64 wr + 16 rf + rho; f(row) depends on rho only)
     const int fr = ring_f(rho);
@@ -160,7 +135,8 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
     // e >= 4: (c0, hi) (c1, lo) (c1, hi) — then elements [e % 4, +8) of the 12:
     // dword select by bit 1 of e, 16-bit funnel shift by bit 0.
     const int e = 7 - (rho & 7);
-    const bool sel2 = (e & 2) != 0, hi4 = (e & 4) != 0;
+    const bool hi4 = (e & 4) != 0;
+    const uint32_t m2 = (e & 2) ? 0xffffffffu : 0u;
     const uint32_t sh = (uint32_t)(e & 1) * 16u;
     int kb_hi[4], kp0[4], kp1[4];
     bool c1wrap[4];
@@ -184,12 +160,23 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = zero4();
 
-    // prologue: ring block 0 and R block 0
-    stage_load(-1);
-    stage_store(-1);
+    // prologue: ring blocks 0 and 1, R block 0
+    DQ_LOAD_KR(-1, 0);
+    DQ_LOAD_RING(sq0, 0);
+    DQ_LOAD_RING(sq1, 1);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        *(u32x4*)(smem + O_RING + q_lds[n]) = sq0[n];
+        *(u32x4*)(smem + O_R + kr_lds[n]) = sr[n];
+        sq0[n] = sq1[n];
+    }
     bar();
     for (int t = 0; t < T; ++t) {
-        if (t + 1 < T) stage_load(t);
+        // key block t-1 and R block t+1 first, ring block t+2 last: the vmcnt(2)
+        // before the LDS writes leaves only the latter in flight
+        DQ_LOAD_KR(t - 1, t + 1);
+        DQ_LOAD_RING(sq1, t + 2);
         const int u = t - 4 + 2 * wr;
         const bool active = kterm ? (u >= 0 && u < nk) : (t < nk);
         if (active) {
@@ -205,9 +192,11 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
                     const uint2 d1 = *(const uint2*)(hi4 ? p1 : p0 + 8);
                     const uint2 d2 = *(const uint2*)(p1 + (hi4 ? 8 : 0));
                     const uint32_t W[6] = {d0.x, d0.y, d1.x, d1.y, d2.x, d2.y};
+                    // (a bit select: written as a ternary the compiler turned the pick into a
+                    // dynamically indexed scratch array)
                     uint32_t X[5];
 #pragma unroll
-                    for (int k = 0; k < 5; ++k) X[k] = sel2 ? W[k + 1] : W[k];
+                    for (int k = 0; k < 5; ++k) X[k] = W[k] ^ ((W[k] ^ W[k + 1]) & m2);
                     const u32x4 o = {__builtin_amdgcn_alignbit(X[1], X[0], sh), __builtin_amdgcn_alignbit(X[2], X[1], sh),
                                      __builtin_amdgcn_alignbit(X[3], X[2], sh), __builtin_amdgcn_alignbit(X[4], X[3], sh)};
                     af[rf] = __builtin_bit_cast(bf16x8, o);
@@ -225,9 +214,25 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
                 for (int rf = 0; rf < 4; ++rf) acc[rf][j] = mfma(bfr, af[rf], acc[rf][j]);
             }
         }
-        if (t + 1 < T) stage_store(t);
+        // ring block t+1 (loaded one iteration ago), key block t-1, R block t+1
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        {
+            char* dq_ = smem + O_RING + ((t + 1) & 3) * SLOT;
+            char* dk_ = smem + O_K + ((t - 1) & 3) * SLOT;
+            char* dr_ = smem + O_R + ((t + 1) & 1) * SLOT;
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+                *(u32x4*)(dq_ + q_lds[n]) = sq0[n];
+                *(u32x4*)(dk_ + kr_lds[n]) = sk[n];
+                *(u32x4*)(dr_ + kr_lds[n]) = sr[n];
+                sq0[n] = sq1[n];
+            }
+        }
         bar();  // iteration t+1's blocks written; iteration t's slots free
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef DQ_LOAD_RING
+#undef DQ_LOAD_KR
 
     // the R-term waves hand their sums to the K-term wave of the same half
     f32x4* scr = (f32x4*)smem;
