@@ -396,12 +396,12 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(TY* __restrict__ y, float* 
     }
 }
 
-// persistent grid of the LayerNorm backward (4 rows in flight per block); the
-// partial-sum workspace is sized for the largest grid. 768 = 3 waves per SIMD,
-// the kernel's VGPR-bound occupancy: 3.57 ms per cfg-2 step against 4.43 at
-// 512 and 4.72 at 1024 (same box, round 2).
+// persistent grid of the LayerNorm backward: one workgroup per SIMD-wave slot
+// the kernel's VGPR count allows (d <= 256: 3 per CU; d <= 1024, two rows in
+// flight per wave at 216 VGPRs: 2; wider: 1); the partial-sum workspace is
+// sized for the largest grid
 constexpr int LN_BWD_MAX_BLOCKS = 1024;
-static int ln_bwd_blocks() { return 768; }
+static int ln_bwd_blocks(int64_t d) { return d <= 256 ? 768 : (d <= 1024 ? 512 : 256); }
 // rows per work-queue ticket of the LayerNorm backward (2 and 8 measured slower)
 constexpr int LN_QROWS = 4;
 
@@ -447,38 +447,75 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
         row = blockIdx.x * 4LL + wid;
         rend = rows;
     }
-    for (;;) {
-        if (row >= rend) {
-            if (!ctr) break;
+    // the row after `row` in this wave's schedule
+    auto advance = [&]() {
+        if (!ctr) {
+            row += (int64_t)gridDim.x * 4;
+            return;
+        }
+        if (++row >= rend) {
             const int t = nwaves + __builtin_amdgcn_readfirstlane(__shfl(tk, 0, 64));
             row = (int64_t)t * LNQ;
             rend = row + LNQ;
             if (lane == 0 && row < rows) tk = atomicAdd(ctr, 1);
         }
+    };
+    f32x4 gm[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        const int col = (c * 64 + lane) * 4;
+        gm[c] = col < d ? *(const f32x4*)(gamma + col) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    // two rows in flight per wave: the next row's x / dy / dx_acc are loaded
+    // while this row is reduced and written (one row at a time left the
+    // kernel latency-bound: 80 % of wave cycles waiting at 3.6 TB/s)
+    f32x4 nx[MAXC], nacc[MAXC];
+    TD ndy[MAXC][4];
+    float nmu = 0.f, nrs = 0.f;
+    auto fetch = [&](int64_t r) {
+        nmu = mean[r];
+        nrs = rstd[r];
+        const int64_t xr = map_row(r, seg, skip);
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+            const int col = (c * 64 + lane) * 4;
+            if (col < d) {
+                nx[c] = *(const f32x4*)(x + xr * d + col);
+                nacc[c] = *(const f32x4*)(dxa + xr * d + col);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) ndy[c][t] = dy[r * d + col + t];
+            }
+        }
+    };
+    if (row < rows) fetch(row);
+    for (;;) {
         if (row >= rows) break;
+        const int64_t cur = row, xrow = map_row(cur, seg, skip);
+        const float mu = nmu, rs = nrs;
+        f32x4 xv[MAXC], acc[MAXC], dv[MAXC];
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+            xv[c] = nx[c];
+            acc[c] = nacc[c];
+            dv[c] = (f32x4){to_f(ndy[c][0]), to_f(ndy[c][1]), to_f(ndy[c][2]), to_f(ndy[c][3])};
+        }
+        advance();
+        if (row < rows) fetch(row);
         {
-        const float mu = mean[row], rs = rstd[row];
-        const int64_t xrow = map_row(row, seg, skip);
-        f32x4 xh[MAXC], g[MAXC], acc[MAXC];
+        f32x4 xh[MAXC], g[MAXC];
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int c = 0; c < MAXC; ++c) {
             const int col = (c * 64 + lane) * 4;
             if (col < d) {
-                const f32x4 xv = *(const f32x4*)(x + xrow * d + col);
-                const f32x4 dv = load4(dy + row * d + col);
-                // the accumulated gradient row is loaded with the inputs, so its
-                // latency overlaps theirs instead of following the reductions
-                acc[c] = *(const f32x4*)(dxa + xrow * d + col);
-                const f32x4 gm = *(const f32x4*)(gamma + col);
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    xh[c][t] = (xv[t] - mu) * rs;
-                    g[c][t] = dv[t] * gm[t];
+                    xh[c][t] = (xv[c][t] - mu) * rs;
+                    g[c][t] = dv[c][t] * gm[c][t];
                     s1 += g[c][t];
                     s2 += g[c][t] * xh[c][t];
-                    pg[c][t] += dv[t] * xh[c][t];
-                    pb[c][t] += dv[t];
+                    pg[c][t] += dv[c][t] * xh[c][t];
+                    pb[c][t] += dv[c][t];
                 }
             } else {
                 xh[c] = g[c] = acc[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -507,7 +544,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(float* __restrict__ dxa, TO
             }
         }
         }
-        row += ctr ? 1 : (int64_t)gridDim.x * 4;
     }
     // block reduce of the partials through LDS, then one row per block
     __shared__ f32x4 red[4][64 * MAXC];
@@ -606,7 +642,7 @@ static void ln_bwd_launch_b(float* dxa, TO* dcopy, float* part, const TD* dy, co
     // the work-queue ticket counter sits after the partials (zeroed per launch)
     int* ctr = queue ? (int*)(part + (int64_t)LN_BWD_MAX_BLOCKS * 3 * d) : nullptr;
     if (ctr) (void)hipMemsetAsync(ctr, 0, sizeof(int), s);
-    const dim3 grid(ln_bwd_blocks());
+    const dim3 grid(ln_bwd_blocks(d));
     if (d <= 256) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 1, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd, ctr);
     else if (d <= 1024) hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 4, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd, ctr);
     else hipLaunchKernelGGL((ln_bwd_kernel<TD, TO, 8, BIAS>), grid, dim3(256), 0, s, dxa, dcopy, part, dy, x, mean, rstd, gamma, rows, d, seg, skip, cd, ctr);
@@ -659,7 +695,7 @@ extern "C" int msq_layernorm_bwd_bias(float* dx_acc, void* dx_copy, int copy_dty
     }
     const int nout = (bias ? 3 : 2) * di;
     hipLaunchKernelGGL(ln_reduce_kernel, dim3((unsigned)((nout + 63) / 64)), dim3(256), 0, s, dgamma, dbeta, dbias,
-                       part, ln_bwd_blocks(), di, nout);
+                       part, ln_bwd_blocks(di), di, nout);
     MSQ_LAUNCH_CHECK();
     return MSQ_OK;
 }

@@ -234,13 +234,14 @@ def workspace(nbytes, device, tag="ws"):
 
 
 def layernorm_bwd(dx_acc, dy, x, mean, rstd, gamma, dgamma, dbeta, dx_copy=None, seg=(0, 0), drop=None,
-                  dbias=None, ordered=False):
+                  dbias=None, ordered=True):
     """dx_acc[map(r)] += LN'(dy[r]); dgamma/dbeta += ...; optional copy of the updated rows
     (drop=(seed, site, p): the copy is masked by that site's dropout keep mask and scaled);
     dbias += column sums of the written rows (the copy, else dx_acc).
-    ordered=True: the parameter-gradient sums in a fixed order (bitwise reproducible;
-    the ln_f backward, whose beta gradient is analytically zero round-off that Adam
-    normalises); else rows from the work queue (timing decides the last bits)."""
+    ordered=True: rows in a fixed order, so the parameter-gradient sums are bitwise
+    reproducible (the ln_f beta gradient is analytically-zero round-off that Adam
+    normalises); ordered=False: rows from a work queue (timing decides the last bits;
+    measured slower since the kernel keeps two rows in flight per wave)."""
     d = x.shape[-1]
     rows = mean.numel()
     ws = workspace(L.lib().msq_layernorm_bwd_workspace(rows, d), x.device, "ln")

@@ -16,8 +16,8 @@ vocabulary; G4's own shapes (hs = 16) have no bf16 path. 12 rows x 56 steps
 = 672 draws (past block_len, so the window slides). Measured (round 6):
 665 / 672 = 0.9896, each of the 7 misses a near-tie (fp32 gap 0.002-0.05 between
 the k-th and (k+1)-th filtered logit). The test asserts that every miss is a
-near-tie (gap within two bf16 ulps of the two tokens' raw logits), the rate
->= 0.98 and the engine's own draws >= 0.99."""
+near-tie (gap within the bound on how far bf16 rounding moved the two tokens'
+filtered logits), the rate >= 0.98 and the engine's own draws >= 0.99."""
 import random
 
 import numpy as np
@@ -61,6 +61,7 @@ def test_bf16_topk_sets_agree_with_fp32_oracle():
             eng_logits = m(window.cuda(), meta.cuda()).float().cpu()
         z_ref = oloss.filtered_logit(window, ref_logits, REAL)[:, -1, :].clone()
         z_eng = oloss.filtered_logit(window, eng_logits, REAL)[:, -1, :].clone()
+        wrow = oloss.weight_table_torch(REAL)[torch.from_numpy(oloss.bucket_of(window[:, -1].numpy(), REAL))].abs()
         for i in range(B):
             k = osamp.choose_k(int(seqs[i, cur - 1]), REAL, kr)
             recent = osamp.recent_window(seqs[i, :cur].tolist(), REAL)
@@ -72,11 +73,17 @@ def test_bf16_topk_sets_agree_with_fp32_oracle():
             agree += same
             total += 1
             if not same:
-                srt, ids = torch.sort(z_ref[i], descending=True)
-                gap = float(srt[k - 1] - srt[k])
-                # the bf16 scale of the two tokens: their raw logits in the last row
-                lmax = float(ref_logits[i, -1, ids[k - 1:k + 1]].abs().max())
-                worst.append((s, i, k, gap, lmax))
+                # a token of the fp32 top-k left out by the bf16 engine (a) and the one
+                # it took instead (b): z_ref[a] >= z_ref[b], z_eng[b] >= z_eng[a], so
+                # z_ref[a] - z_ref[b] <= |dz_a| + |dz_b|; z = -(l[T-1] - logsumexp_t l[t]) w
+                # (train.py:133-138, w the bucket weight of the row) moves by at most
+                # 2 w times the largest |bf16 - fp32| logit difference in its column
+                # (the penalty only divides by >= 1)
+                def dz(tok):
+                    return 2 * float(wrow[i, tok]) * float((eng_logits[i, :, tok] - ref_logits[i, :, tok]).abs().max())
+                for a_ in set(ir.tolist()) - set(ie.tolist()):
+                    for b_ in set(ie.tolist()) - set(ir.tolist()):
+                        worst.append((s, i, k, float(z_ref[i][a_] - z_ref[i][b_]), dz(a_) + dz(b_)))
             # the engine's draw: inverse CDF over its own top-k on this step's uniform
             # (the device computed its filtered logits from the same bf16 logits,
             # so this agrees up to fp32 rounding of the filtered-logit pass)
@@ -84,14 +91,13 @@ def test_bf16_topk_sets_agree_with_fp32_oracle():
             picks += pick == int(seqs[i, cur])
     rate = agree / total
     print(f"\nbf16 vs fp32 top-k set agreement: {agree}/{total} = {rate:.4f}; engine draws reproduced "
-          f"{picks}/{total}; disagreements (step, row, k, fp32 gap between k-th and (k+1)-th, their max |logit|): "
-          f"{worst}")
-    # every disagreement is a near-tie: the fp32 gap between the k-th and the
-    # (k+1)-th filtered logit is within two bf16 ulps of the larger of the two
-    # tokens' raw logits (the engine stores logits in bf16, so such a pair can
-    # swap order); the rate itself is reported and must stay >= RATE_MIN
-    # (672 draws: 13 near-ties allowed)
-    ties = [w for w in worst if w[3] <= 2 * 2.0 ** (np.floor(np.log2(max(abs(w[4]), 1e-30))) - 7)]
+          f"{picks}/{total}; disagreements (step, row, k, fp32 gap of the swapped pair, bound on their bf16 "
+          f"movement): {worst}")
+    # every disagreement is a near-tie: the fp32 gap of each swapped pair is
+    # within the bound on how far the two tokens' bf16 filtered logits can move
+    # (a larger gap could not swap); the rate itself is reported and must stay
+    # >= RATE_MIN (672 draws: 13 near-ties allowed)
+    ties = [w for w in worst if w[3] <= w[4]]
     assert len(ties) == len(worst), [w for w in worst if w not in ties]
     assert rate >= RATE_MIN, (rate, worst)
     assert picks / total >= 0.99, (picks, total)

@@ -16,16 +16,15 @@
 // holds the first rows), so the r-window starts at R0 = S-1-i_last = 128 qb, a
 // multiple of the 32-wide r-block, and tile row ro (query i0 + ro) reads its
 // K term at ring column x = (127 - ro) + j.
-// Workgroup: 4 waves, two workgroups per CU. Wave 0 / 1 run the K term of
-// query half wr = 0 / 1, waves 2 / 3 the R term, each 64 queries x 128 dims
-// (v_mfma_f32_16x16x32_bf16); the partial sums meet in LDS at the end.
-// Iteration t (one barrier): the R term contracts r-block t (32 columns)
-// against R rows [R0 + 32 t, +32); the K term of half wr contracts key block
-// u = t - 4 + 2 wr, whose skewed columns lie in r-blocks t-2 .. t for both
-// halves. LDS (80 KB): a ring of 4 r-blocks (128 x 32), 4 key blocks and 2 R
-// blocks (32 x 128). Every wave stages a quarter of each block, global ->
-// registers -> LDS: the key and R blocks one iteration ahead, the ring block
-// (the HBM stream) two.
+// Workgroup: 4 waves, two workgroups per CU. Wave w owns queries 32 w .. +31
+// (2 x 8 tiles of v_mfma_f32_16x16x32_bf16) and runs both terms into one
+// accumulator set: iteration t (one barrier) contracts r-block t (32 columns)
+// against R rows [R0 + 32 t, +32) and key block u = t - 4 + w, whose skewed
+// columns lie in r-blocks t-1 and t for every wave (the wave's 32-row skew is
+// absorbed by its key-block lag). LDS (80 KB): a ring of 3 r-blocks
+// (128 x 32), 5 key blocks and 2 R blocks (32 x 128). Every wave stages a
+// quarter of each block, global -> registers -> LDS: the key and R blocks one
+// iteration ahead, the ring block (the HBM stream) two.
 #include "attn_tiles.h"
 
 namespace {
@@ -33,12 +32,11 @@ using namespace attn;
 
 constexpr int NT = 256, BM = 128, BK = 32;
 constexpr int SLOT = BM * BK * 2;  // 8 KB: a ring block (128 x 32) or a key / R block (32 x 128)
-constexpr int NRING = 4, NKS = 4, NRS = 2;
+constexpr int NRING = 3, NKS = 5, NRS = 2;
 constexpr int O_RING = 0, O_K = NRING * SLOT, O_R = O_K + NKS * SLOT;
 constexpr int LDS_BYTES = O_R + NRS * SLOT;
 constexpr uint32_t OOB = 0xFFFF0000u;
 static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU");
-static_assert(2 * 32 * 64 * 16 <= LDS_BYTES, "epilogue scratch");
 
 // ring image: row ro (64 B) at ro * 64, 16-B chunk k at k ^ f(ro),
 // f = {0, 2, 3, 1}[(ro >> 2) & 3]: the R term's aligned fragment reads are
@@ -85,17 +83,10 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
     const int R0 = BM * qb;                      // S - 1 - (i0 + 127)
     const int nk = (ihi + BK - 1) / BK;          // key blocks; also the R term's r-blocks
     const int T = nk + 4;
-
-    const bool kterm = w < 2;
-    const int wr = w & 1;  // query half
     const int rho = lane & 15, g = lane >> 4;
 
-    // ---- staging: every wave moves a quarter of each block, global -> registers
-    // -> LDS. Iteration t loads key block t-1 and R block t+1 (written to LDS at
-    // its end) and ring block t+2 (written one iteration later: the dQR stream
-    // is the HBM one, so it gets two iterations of latency). Per lane: ring rows
-    // 32 w + 16 n + lane / 4, chunk lane % 4; key / R rows 8 w + 4 n + lane / 16,
-    // chunk kr_pos(row, lane % 16) (n = 0, 1).
+    // ---- staging: per lane, ring rows 32 w + 16 n + lane / 4, chunk lane % 4;
+    // key / R rows 8 w + 4 n + lane / 16, chunk kr_pos(row, lane % 16) (n = 0, 1)
     const __amdgpu_buffer_rsrc_t rQ =
         dq_rsrc(dqr + ((int64_t)h * a.B + b) * S * ldr, (uint32_t)((int64_t)S * ldr * 2));
     const __amdgpu_buffer_rsrc_t rK = dq_rsrc((const bf16*)a.qkv + (int64_t)b * S * ldq, (uint32_t)((int64_t)S * ldq * 2));
@@ -128,86 +119,89 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
                                                       0, 0);                                                   \
     }
 
-    // ---- fragment addressing (ring rows 64 wr + 16 rf + rho; f(row) depends on rho only)
+    // ---- fragment addressing; the wave's ring rows 32 w + 16 rf + rho, ring_f
+    // of them depends on rho only
     const int fr = ring_f(rho);
-    // K term, fragment rf of iteration t: ring element E = (127 - ro) + 32 u + 8 g with
-    // u = t - 4 + 2 wr, i.e. E = 32 t + 8 c + e, c = g - 1 - 2 rf - rho / 8, e = 7 - rho % 8:
-    // chunks c0 = 4 t + c and c0 + 1 (block t + floor(c / 4), the next one when c % 4 == 3).
-    // Three 8-B pieces from element 4 floor(E / 4) — e < 4: (c0, lo) (c0, hi) (c1, lo);
-    // e >= 4: (c0, hi) (c1, lo) (c1, hi) — then elements [e % 4, +8) of the 12:
-    // dword select by bit 1 of e (64-bit shift by 0 / 32), 16-bit funnel shift by bit 0.
+    // R term, fragment rf: chunk g of the row, in the slot of r-block t
+    int ra[2];
+#pragma unroll
+    for (int rf = 0; rf < 2; ++rf) ra[rf] = (32 * w + 16 * rf + rho) * 64 + ((g ^ fr) << 4);
+    // K term, fragment rf of iteration t: ring element E = (127 - ro) + 32 u + 8 g,
+    // u = t - 4 + w, i.e. E = 32 t + 8 c + e with c = g - 1 - 2 rf - rho / 8 (in
+    // [-4, 2]) and e = 7 - rho % 8: chunks c0 = 4 t + c and c0 + 1, each in
+    // r-block t or t - 1. Three 8-B pieces from element 4 floor(E / 4) — e < 4:
+    // (c0, lo) (c0, hi) (c1, lo); e >= 4: (c0, hi) (c1, lo) (c1, hi) — then
+    // elements [e % 4, +8) of the 12: a dword select by bit 1 of e (64-bit
+    // shift by 0 / 32), a 16-bit funnel shift by bit 0.
     const int e = 7 - (rho & 7);
     const bool hi4 = (e & 4) != 0;
-    const uint32_t s64 = (e & 2) ? 32u : 0u;
-    const uint32_t sh = (uint32_t)(e & 1) * 16u;
-    int kb_hi[4], kp0[4], kp1[4];
-    bool c1wrap[4];
+    const uint32_t s64 = (e & 2) ? 32u : 0u, sh = (uint32_t)(e & 1) * 16u;
+    int kp0[2], kp1[2];   // piece offsets inside the slot (the first piece of c0 / of c1)
+    bool km0[2], km1[2];  // chunk c0 / c1 in r-block t - 1
 #pragma unroll
-    for (int rf = 0; rf < 4; ++rf) {
-        const int ro = 64 * wr + 16 * rf + rho;
-        const int c = g - 1 - 2 * rf - (rho >> 3);  // c0 - 4 t (may be negative)
-        kb_hi[rf] = c >> 2;                       // floor
-        c1wrap[rf] = (c & 3) == 3;
+    for (int rf = 0; rf < 2; ++rf) {
+        const int ro = 32 * w + 16 * rf + rho;
+        const int c = g - 1 - 2 * rf - (rho >> 3);
+        km0[rf] = c < 0;
+        km1[rf] = c + 1 < 0;
         kp0[rf] = ro * 64 + (((c & 3) ^ fr) << 4) + (hi4 ? 8 : 0);
         kp1[rf] = ro * 64 + ((((c + 1) & 3) ^ fr) << 4);
     }
-    // R term, fragment rf: row 64 wr + 16 rf + rho, chunk g
-    int ra[4];
-#pragma unroll
-    for (int rf = 0; rf < 4; ++rf) ra[rf] = (64 * wr + 16 * rf + rho) * 64 + ((g ^ fr) << 4);
 
-    f32x4 acc[4][8];
+    f32x4 acc[2][8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = zero4();
 
-    // one iteration's MFMAs (t: the R term's r-block / the K term's key block u)
+    // one iteration's MFMAs: the R term of r-block t, the K term of key block u
     auto compute = [&](int t) {
-        const int u = t - 4 + 2 * wr;
-        const bool active = kterm ? (u >= 0 && u < nk) : (t < nk);
-        if (!active) return;
-        {
-            bf16x8 af[4];
-            if (kterm) {
+        const int u = t - 4 + w;
+        const bool rterm = t < nk, kterm = u >= 0 && u < nk;
+        const int sA = O_RING + (t % 3) * SLOT, sB = O_RING + ((t + 2) % 3) * SLOT;  // r-blocks t, t - 1
+        if (rterm) {
+            bf16x8 af[2];
 #pragma unroll
-                for (int rf = 0; rf < 4; ++rf) {
-                    const int blk0 = (t + kb_hi[rf]) & 3;
-                    const int blk1 = c1wrap[rf] ? ((t + kb_hi[rf] + 1) & 3) : blk0;
-                    const char* p0 = smem + O_RING + blk0 * SLOT + kp0[rf];
-                    const char* p1 = smem + O_RING + blk1 * SLOT + kp1[rf];
-                    const uint2 d0 = *(const uint2*)p0;
-                    const uint2 d1 = *(const uint2*)(hi4 ? p1 : p0 + 8);
-                    const uint2 d2 = *(const uint2*)(p1 + (hi4 ? 8 : 0));
-                    const uint32_t W[6] = {d0.x, d0.y, d1.x, d1.y, d2.x, d2.y};
-                    // (the dword select as a 64-bit shift by 0 / 32: written as a ternary
-                    // the compiler turned it into a dynamically indexed scratch array)
-                    uint32_t X[5];
-#pragma unroll
-                    for (int k = 0; k < 5; ++k) X[k] = (uint32_t)(((((uint64_t)W[k + 1]) << 32) | W[k]) >> s64);
-                    const u32x4 o = {__builtin_amdgcn_alignbit(X[1], X[0], sh), __builtin_amdgcn_alignbit(X[2], X[1], sh),
-                                     __builtin_amdgcn_alignbit(X[3], X[2], sh), __builtin_amdgcn_alignbit(X[4], X[3], sh)};
-                    af[rf] = __builtin_bit_cast(bf16x8, o);
-                }
-            } else {
-                const char* sq = smem + O_RING + (t & 3) * SLOT;
-#pragma unroll
-                for (int rf = 0; rf < 4; ++rf) af[rf] = *(const bf16x8*)(sq + ra[rf]);
-            }
-            const char* sb = kterm ? smem + O_K + (u & 3) * SLOT : smem + O_R + (t & 1) * SLOT;
+            for (int rf = 0; rf < 2; ++rf) af[rf] = *(const bf16x8*)(smem + sA + ra[rf]);
+            const char* sb = smem + O_R + (t & 1) * SLOT;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const bf16x8 bfr = frag_b(sb, 16 * j, lane);
 #pragma unroll
-                for (int rf = 0; rf < 4; ++rf) acc[rf][j] = mfma(bfr, af[rf], acc[rf][j]);
+                for (int rf = 0; rf < 2; ++rf) acc[rf][j] = mfma(bfr, af[rf], acc[rf][j]);
+            }
+        }
+        if (kterm) {
+            bf16x8 af[2];
+#pragma unroll
+            for (int rf = 0; rf < 2; ++rf) {
+                const char* p0 = smem + (km0[rf] ? sB : sA) + kp0[rf];
+                const char* p1 = smem + (km1[rf] ? sB : sA) + kp1[rf];
+                const uint2 d0 = *(const uint2*)p0;
+                const uint2 d1 = *(const uint2*)(hi4 ? p1 : p0 + 8);
+                const uint2 d2 = *(const uint2*)(p1 + (hi4 ? 8 : 0));
+                const uint32_t W[6] = {d0.x, d0.y, d1.x, d1.y, d2.x, d2.y};
+                uint32_t X[5];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) X[k] = (uint32_t)(((((uint64_t)W[k + 1]) << 32) | W[k]) >> s64);
+                const u32x4 o = {__builtin_amdgcn_alignbit(X[1], X[0], sh), __builtin_amdgcn_alignbit(X[2], X[1], sh),
+                                 __builtin_amdgcn_alignbit(X[3], X[2], sh), __builtin_amdgcn_alignbit(X[4], X[3], sh)};
+                af[rf] = __builtin_bit_cast(bf16x8, o);
+            }
+            const char* sb = smem + O_K + (u % NKS) * SLOT;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const bf16x8 bfr = frag_b(sb, 16 * j, lane);
+#pragma unroll
+                for (int rf = 0; rf < 2; ++rf) acc[rf][j] = mfma(bfr, af[rf], acc[rf][j]);
             }
         }
     };
-    // the LDS writes of iteration t: ring block t+1, key block t-1, R block t+1
+    // the LDS writes of iteration t: ring block t+1, key block t, R block t+1
 #define DQ_STORE(t, sq)                                                                                        \
     {                                                                                                          \
-        char* dq_ = smem + O_RING + (((t) + 1) & 3) * SLOT;                                                    \
-        char* dk_ = smem + O_K + (((t) - 1) & 3) * SLOT;                                                       \
+        char* dq_ = smem + O_RING + (((t) + 1) % 3) * SLOT;                                                    \
+        char* dk_ = smem + O_K + ((t) % NKS) * SLOT;                                                           \
         char* dr_ = smem + O_R + (((t) + 1) & 1) * SLOT;                                                       \
         _Pragma("unroll") for (int n = 0; n < 2; ++n) {                                                        \
             *(u32x4*)(dq_ + q_lds[n]) = sq[n];                                                                 \
@@ -215,11 +209,11 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
             *(u32x4*)(dr_ + kr_lds[n]) = sr[n];                                                                \
         }                                                                                                      \
     }
-    // iteration t: key block t-1 and R block t+1 (written at its end), ring
-    // block t+2 into the other ring set (written one iteration later; the sets
+    // iteration t: key block t and R block t+1 (written at its end), ring block
+    // t+2 into the other ring set (written one iteration later; the sets
     // alternate, so no register copy waits for a load in flight)
 #define DQ_ITER(t, QW, QL)                                                                                     \
-    DQ_LOAD_KR((t) - 1, (t) + 1);                                                                              \
+    DQ_LOAD_KR((t), (t) + 1);                                                                                  \
     DQ_LOAD_RING(QL, (t) + 2);                                                                                 \
     compute(t);                                                                                                \
     asm volatile("s_waitcnt vmcnt(2)" ::: "memory");                                                          \
@@ -229,7 +223,7 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
     // prologue: ring block 0 and R block 0 into LDS; ring block 1 into set 0
     // (written by iteration 0)
     DQ_LOAD_RING(sq1, 0);
-    DQ_LOAD_KR(-2, 0);
+    DQ_LOAD_KR(-1, 0);
     DQ_LOAD_RING(sq0, 1);
     asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
 #pragma unroll
@@ -246,30 +240,20 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
     if (t < T) {
         DQ_ITER(t, sq0, sq1)
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #undef DQ_ITER
 #undef DQ_STORE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #undef DQ_LOAD_RING
 #undef DQ_LOAD_KR
 
-    // the R-term waves hand their sums to the K-term wave of the same half
-    f32x4* scr = (f32x4*)smem;
-    if (!kterm) {
-#pragma unroll
-        for (int rf = 0; rf < 4; ++rf)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) scr[(wr * 32 + rf * 8 + j) * 64 + lane] = acc[rf][j];
-    }
-    bar();
-    if (!kterm) return;
     // lane holds dq[i = row][d .. d+3]
 #pragma unroll
-    for (int rf = 0; rf < 4; ++rf) {
-        const int m = i0 + 64 * wr + 16 * rf + rho;
+    for (int rf = 0; rf < 2; ++rf) {
+        const int m = i0 + 32 * w + 16 * rf + rho;
         if (m < 0 || m >= S) continue;
         bf16* p = dqkv + ((int64_t)b * S + m) * ldd + (int64_t)h * HS + 4 * g;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) store4(p + 16 * j, acc[rf][j] + scr[(wr * 32 + rf * 8 + j) * 64 + lane]);
+        for (int j = 0; j < 8; ++j) store4(p + 16 * j, acc[rf][j]);
     }
 }
 
