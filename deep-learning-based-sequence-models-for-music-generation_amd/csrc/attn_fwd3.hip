@@ -29,20 +29,7 @@ constexpr int O_D = O_M + 64 * 4;  // dropout keep words of the block's 256 quer
 constexpr int LDS_BYTES = O_D + 2 * QB * 4;
 constexpr uint32_t OOB = 0xFFFF0000u;
 // lazy-rescale threshold of the running row maximum, log2 units (P <= 2^RESCALE)
-#ifndef FWD3_RESCALE
-#define FWD3_RESCALE 8.f
-#endif
-constexpr float RESCALE = FWD3_RESCALE;
-// 1: the next K / V / R tile is staged through registers (loads after the
-// barrier, ds_write at the end of the tile) instead of in-loop LDS-DMA.
-// Measured 1-2 % slower at cfg 2 (0.908 vs 0.892 ms per launch, same box), so off.
-#ifndef FWD3_REGSTAGE
-#define FWD3_REGSTAGE 0
-#endif
-// ablation builds (tools/build_var.sh -DFWD3_LAB=n): the LAB mask of the launched kernel
-#ifndef FWD3_LAB
-#define FWD3_LAB 0
-#endif
+constexpr float RESCALE = 8.f;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
     const uint64_t a = (uint64_t)base;
@@ -78,13 +65,10 @@ __device__ __forceinline__ void bar() {
     asm volatile("" ::: "memory");
 }
 
-// LAB: ablation switches for tools/lab (0 in the library):
-// 1 no K.Q^T MFMA, 2 no QR MFMA, 4 no skew / softmax, 8 no PV MFMA, 16 no DMA in the loop,
-// 32 no skew scratch round trip, 64 no rescale, 128 no row max
 // DROP: attention-probability dropout (model_transformer.py:80): the keep word
 // of (query, key tile) is staged by LDS-DMA with the tile; P.V uses p * keep,
 // the softmax normaliser the undropped p, the output is scaled by 1/(1-p)
-template <int LAB = 0, bool DROP = false>
+template <bool DROP>
 __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __restrict__ out, int64_t ldo,
                                                            float* __restrict__ lse) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -182,46 +166,30 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
         dma32(rr, sR + c * KB * 256, offR, lrow, (uint32_t)(r0 * HS * 2), -r0, S - r0, w);
     }
 
-#if FWD3_REGSTAGE
-    // register staging of the next tile (T14: loads issued at the top of a
-    // tile, written to LDS at its end; an LDS-DMA wave-instruction costs
-    // 60-185 issue cycles, MI355X_MICROARCH 'LDS-DMA piece')
-    u32x4 gk, gv, gr;
-    uint32_t gm = 0u;
-#endif
-    for (int kt = 0; kt < nkt; ++kt) {
-        const int j0 = kt * KB, cur = kt & 1;
-        // one barrier per tile: it publishes tile kt (DMA'd in the prologue,
-        // or written by every wave at the end of tile kt-1) and releases tile
-        // kt-1's buffers
-#if FWD3_REGSTAGE
-        if (kt == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        bar();
-        if (kt + 1 < nkt && !(LAB & 16)) {
-            const int j1 = j0 + KB, c = kt + NCH - 1, r0 = rb0 + c * KB;
-            gk = __builtin_amdgcn_raw_buffer_load_b128(rq, lrow < S - j1 ? offK + (uint32_t)j1 * ldq2 : OOB, 0, 0);
-            gv = __builtin_amdgcn_raw_buffer_load_b128(rq, lrow < S - j1 ? offV + (uint32_t)j1 * ldq2 : OOB, 0, 0);
-            gr = __builtin_amdgcn_raw_buffer_load_b128(
-                rr, (lrow >= -r0 && lrow < S - r0) ? offR + (uint32_t)(r0 * HS * 2) : OOB, 0, 0);
-            if (DROP && w < 4) {
-                const int iq = i0 + 64 * w + lane;
-                gm = __builtin_amdgcn_raw_buffer_load_b32(
-                    rm, (iq >= 0 && iq < S) ? (uint32_t)(mask_word(mld, iq, 32 * (kt + 1)) * 4) : OOB, 0, 0);
-            }
-        }
-#else
+    // one barrier per tile: it publishes tile kt (DMA'd in the prologue, or
+    // one tile ahead) and releases tile kt-1's buffers
+    auto sync = [&](int kt) {
+        const int cur = kt & 1;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         bar();
-        if (kt + 1 < nkt && !(LAB & 16)) {
-            const int j1 = j0 + KB, c = kt + NCH - 1, r0 = rb0 + c * KB;
+        if (kt + 1 < nkt) {
+            const int j1 = (kt + 1) * KB, c = kt + NCH - 1, r0 = rb0 + c * KB;
             dma32(rq, smem + O_K + (cur ^ 1) * KB * 256, offK, lrow, (uint32_t)j1 * ldq2, 0, S - j1, w);
             dma32(rq, smem + O_V + (cur ^ 1) * KB * 256, offV, lrow, (uint32_t)j1 * ldq2, 0, S - j1, w);
             dma32(rr, sR + (c % NCH) * KB * 256, offR, lrow, (uint32_t)(r0 * HS * 2), -r0, S - r0, w);
             stage_m(kt + 1, cur ^ 1);
         }
-#endif
-        if (live) {
+    };
+    // tiles past the wave's last query are masked for all its queries (the
+    // metadata keys are in tile 0): the wave only meets their barriers and
+    // issues their DMA (a second loop, so the accumulators' registers stay
+    // put through the first)
+    const int nkw = live ? min(nkt, (iw + 31) / KB + 1) : 0;
+    int kt = 0;
+    for (; kt < nkw; ++kt) {
+        const int j0 = kt * KB, cur = kt & 1;
+        sync(kt);
+        {
             const char* cK = smem + O_K + cur * KB * 256;
             const char* cV = smem + O_V + cur * KB * 256;
             // S^T[key][query] = K . Q^T
@@ -232,12 +200,8 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
 #pragma unroll
                 for (int ks = 0; ks < 4; ++ks) {
                     const bf16x8 kfr = *(const bf16x8*)(cK + nt * 4096 + fro[ks]);
-                    if (LAB & 1) {
-                        asm volatile("" ::"v"(kfr));
-                    } else {
-                        sacc[0][nt] = mfma(kfr, qf[0][ks], sacc[0][nt]);
-                        sacc[1][nt] = mfma(kfr, qf[1][ks], sacc[1][nt]);
-                    }
+                    sacc[0][nt] = mfma(kfr, qf[0][ks], sacc[0][nt]);
+                    sacc[1][nt] = mfma(kfr, qf[1][ks], sacc[1][nt]);
                 }
             }
             // QR^T[window row][query]: the wave's 64-row union window starts at
@@ -254,12 +218,8 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
 #pragma unroll
                 for (int ks = 0; ks < 4; ++ks) {
                     const bf16x8 rfr = *(const bf16x8*)(sR + rowb * 256 + fro[ks]);
-                    if (LAB & 2) {
-                        asm volatile("" ::"v"(rfr));
-                    } else {
-                        if (t >= 1) qacc[0][t - 1] = mfma(rfr, qf[0][ks], qacc[0][t - 1]);
-                        if (t <= 2) qacc[1][t] = mfma(rfr, qf[1][ks], qacc[1][t]);
-                    }
+                    if (t >= 1) qacc[0][t - 1] = mfma(rfr, qf[0][ks], qacc[0][t - 1]);
+                    if (t <= 2) qacc[1][t] = mfma(rfr, qf[1][ks], qacc[1][t]);
                 }
             }
 
@@ -268,23 +228,14 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
             bf16x8 pf[2];
 #pragma unroll
             for (int q2 = 0; q2 < 2; ++q2) {
-                if (LAB & 4) {
-                    float x = sacc[q2][0][0] + sacc[q2][1][1] + qacc[q2][0][0] + qacc[q2][2][3];
-                    pf[q2] = (bf16x8){(bf16)x, (bf16)x, (bf16)x, (bf16)x, (bf16)x, (bf16)x, (bf16)x, (bf16)x};
-                    l_part[q2] += 1.f;
-                    m_run[q2] = 0.f;
-                    continue;
-                }
                 const int iq = iw + 16 * q2 + il;
                 // (a wave's LDS operations execute in issue order, so the skewed
                 // reads below see these writes, and the next group's writes
                 // follow this group's reads, without an lgkmcnt(0) between:
                 // the compiler waits only where a read's value is used)
-                if (!(LAB & 32)) {
 #pragma unroll
-                    for (int t = 0; t < 3; ++t) *(f32x4*)(scw + il * SCR + t * 16 + 4 * g) = qacc[q2][t];
-                    __builtin_amdgcn_wave_barrier();
-                }
+                for (int t = 0; t < 3; ++t) *(f32x4*)(scw + il * SCR + t * 16 + 4 * g) = qacc[q2][t];
+                __builtin_amdgcn_wave_barrier();
                 float sv[2][4];
                 float mx = -INFINITY;
                 // masking only where a key may follow a query of the group or
@@ -296,11 +247,22 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int jl = nt * 16 + 4 * g + r;
-                            const float x = sacc[q2][nt][r] + ((LAB & 32) ? qacc[q2][nt][r] : scw[il * SCR + jl - il + 15]);
+                            const float x = sacc[q2][nt][r] + scw[il * SCR + jl - il + 15];
                             sv[nt][r] = x;
                             mx = fmaxf(mx, x);
                         }
-                } else {
+                } else if (j0 >= nm) {  // the diagonal or the sequence end only
+#pragma unroll
+                    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int jl = nt * 16 + 4 * g + r;
+                            const int j = j0 + jl;
+                            const float x = sacc[q2][nt][r] + scw[il * SCR + jl - il + 15];
+                            sv[nt][r] = (j < S && j <= iq) ? x : -INFINITY;
+                            mx = fmaxf(mx, sv[nt][r]);
+                        }
+                } else {  // tile 0: the metadata keys every query sees
 #pragma unroll
                     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
@@ -315,14 +277,14 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
                             mx = fmaxf(mx, x);
                         }
                 }
-                if (!(LAB & 32)) __builtin_amdgcn_wave_barrier();  // (code motion only)
-                if (!(LAB & 128)) mx = max_rows(mx);
+                __builtin_amdgcn_wave_barrier();  // (code motion only)
+                mx = max_rows(mx);
                 // lazy rescale (T13): the running max moves only when some row's
                 // new maximum passes it by more than RESCALE (log2 units), so
                 // p = exp2(raw c2 - m) <= 2^RESCALE; l and O always see the same m
                 float m_new = m_run[q2];
-                if (!(LAB & 64) && __any(mx * c2 > m_run[q2] + RESCALE)) {
-                    m_new = (LAB & 128) ? 8.f : fmaxf(m_run[q2], mx * c2);
+                if (__any(mx * c2 > m_run[q2] + RESCALE)) {
+                    m_new = fmaxf(m_run[q2], mx * c2);
                     const float alpha = __builtin_amdgcn_exp2f(m_run[q2] - m_new);
                     l_part[q2] *= alpha;
 #pragma unroll
@@ -332,38 +294,39 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
                 float ps = 0.f;
                 uint32_t kw = 0;
                 if (DROP) kw = ((const uint32_t*)(smem + O_D + cur * QB * 4))[32 * w + 16 * q2 + il] >> (4 * g);
+                // p packed two keys per register; a dropped key's half is
+                // cleared by a mask of its sign-extended keep bit (v_bfe_i32,
+                // v_bfi_b32: 2.5 VALU per key instead of 4.5)
+                union { bf16x8 v; bf16x2 h[4]; uint32_t u[4]; } pk;
 #pragma unroll
                 for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float p = __builtin_amdgcn_exp2f(fmaf(sv[nt][r], c2, -m_new));
-                        ps += p;
-                        pf[q2][nt * 4 + r] = DROP ? ((kw >> (nt * 16 + r)) & 1u ? (bf16)p : (bf16)0.f) : (bf16)p;
+                    for (int r = 0; r < 4; r += 2) {
+                        const float p0 = __builtin_amdgcn_exp2f(fmaf(sv[nt][r], c2, -m_new));
+                        const float p1 = __builtin_amdgcn_exp2f(fmaf(sv[nt][r + 1], c2, -m_new));
+                        ps += p0;
+                        ps += p1;
+                        pk.h[nt * 2 + r / 2] = (bf16x2){(bf16)p0, (bf16)p1};
+                        if (DROP) {
+                            const int k = nt * 16 + r;
+                            const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)kw, k, 1);
+                            const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)kw, k + 1, 1);
+                            pk.u[nt * 2 + r / 2] &= (m0 & 0xFFFFu) | (m1 & 0xFFFF0000u);
+                        }
                     }
+                pf[q2] = pk.v;
                 l_part[q2] += ps;
             }
             // O^T[d][query] += V^T[d][key] . P^T[key][query]
 #pragma unroll
             for (int n = 0; n < 8; ++n) {
                 const bf16x8 vfr = cat8(tr_read(cV, vqo[n]), tr_read(cV, 4096 + vqo[n]));
-                if (LAB & 8) {
-                    asm volatile("" ::"v"(vfr), "v"(pf[0]), "v"(pf[1]));
-                } else {
-                    oacc[0][n] = mfma(vfr, pf[0], oacc[0][n]);
-                    oacc[1][n] = mfma(vfr, pf[1], oacc[1][n]);
-                }
+                oacc[0][n] = mfma(vfr, pf[0], oacc[0][n]);
+                oacc[1][n] = mfma(vfr, pf[1], oacc[1][n]);
             }
         }
-#if FWD3_REGSTAGE
-        if (kt + 1 < nkt && !(LAB & 16)) {
-            const int c = kt + NCH - 1;
-            *(u32x4*)(smem + O_K + (cur ^ 1) * KB * 256 + w * 1024 + lane * 16) = gk;
-            *(u32x4*)(smem + O_V + (cur ^ 1) * KB * 256 + w * 1024 + lane * 16) = gv;
-            *(u32x4*)(sR + (c % NCH) * KB * 256 + w * 1024 + lane * 16) = gr;
-            if (DROP && w < 4) *(uint32_t*)(smem + O_D + (cur ^ 1) * QB * 4 + w * 256 + lane * 4) = gm;
-        }
-#endif
     }
+    for (; kt < nkt; ++kt) sync(kt);
 
     if (!live) return;
 #pragma unroll
@@ -386,9 +349,9 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
 int flash_fwd3(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)flash_fwd3_kernel<FWD3_LAB, false>,
+        (void)hipFuncSetAttribute((const void*)flash_fwd3_kernel<false>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)flash_fwd3_kernel<FWD3_LAB, true>,
+        (void)hipFuncSetAttribute((const void*)flash_fwd3_kernel<true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
         attr = true;
     }
@@ -396,7 +359,7 @@ int flash_fwd3(const AttnArgs& a, bf16* out, int64_t ldo, float* lse, hipStream_
     if (a.S * a.ldq * 2 >= (int64_t)OOB || a.S * HS * 2 >= (int64_t)OOB || a.n_meta > 8) return -1;
     const dim3 grid((unsigned)((a.S + QB - 1) / QB), (unsigned)a.H, (unsigned)a.B);
     if (a.rowmask)
-        hipLaunchKernelGGL((flash_fwd3_kernel<FWD3_LAB, true>), grid, dim3(NT), LDS_BYTES, s, a, out, ldo, lse);
-    else hipLaunchKernelGGL((flash_fwd3_kernel<FWD3_LAB, false>), grid, dim3(NT), LDS_BYTES, s, a, out, ldo, lse);
+        hipLaunchKernelGGL((flash_fwd3_kernel<true>), grid, dim3(NT), LDS_BYTES, s, a, out, ldo, lse);
+    else hipLaunchKernelGGL((flash_fwd3_kernel<false>), grid, dim3(NT), LDS_BYTES, s, a, out, ldo, lse);
     return 0;
 }
