@@ -209,15 +209,16 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
             f32x4 qacc[2][3];
 #pragma unroll
             for (int t = 0; t < 3; ++t) qacc[0][t] = qacc[1][t] = zero4();
-            int wr0 = j0 + 224 - 32 * w;  // window row (from rb0) of union block 0
-            wr0 -= (wr0 / RING) * RING;
+            // window rows (from rb0) j0 + 224 - 32 w .. +63: ring chunks ca, cb
+            // (16-row blocks t = 0, 1 in ca, t = 2, 3 in cb: one lane address
+            // per chunk and k-step, the block an immediate offset)
+            const int ca = (kt + 7 - w) % NCH, cb = ca + 1 == NCH ? 0 : ca + 1;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                int rowb = wr0 + 16 * t;
-                rowb = rowb >= RING ? rowb - RING : rowb;
+                const char* rch = sR + (t < 2 ? ca : cb) * KB * 256 + (t & 1) * 16 * 256;
 #pragma unroll
                 for (int ks = 0; ks < 4; ++ks) {
-                    const bf16x8 rfr = *(const bf16x8*)(sR + rowb * 256 + fro[ks]);
+                    const bf16x8 rfr = *(const bf16x8*)(rch + fro[ks]);
                     if (t >= 1) qacc[0][t - 1] = mfma(rfr, qf[0][ks], qacc[0][t - 1]);
                     if (t <= 2) qacc[1][t] = mfma(rfr, qf[1][ks], qacc[1][t]);
                 }
@@ -259,7 +260,9 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
                             const int jl = nt * 16 + 4 * g + r;
                             const int j = j0 + jl;
                             const float x = sacc[q2][nt][r] + scw[il * SCR + jl - il + 15];
-                            sv[nt][r] = (j < S && j <= iq) ? x : -INFINITY;
+                            // (& not &&: a short-circuit test became a branch
+                            // around each scratch read, with a wait per read)
+                            sv[nt][r] = ((j < S) & (j <= iq)) ? x : -INFINITY;
                             mx = fmaxf(mx, sv[nt][r]);
                         }
                 } else {  // tile 0: the metadata keys every query sees
@@ -270,20 +273,24 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
                             const int jl = nt * 16 + 4 * g + r;
                             const int j = j0 + jl;
                             float x = sacc[q2][nt][r] + scw[il * SCR + jl - il + 15];
-                            const bool ok = (j < S) && (j <= iq || j < nm);
-                            if (j >= iq + 2 && j < nm && iq >= 0) x += mbd[iq * 8 + j];
+                            const bool ok = (j < S) & ((j <= iq) | (j < nm));
+                            const bool md = (j >= iq + 2) & (j < nm) & (iq >= 0);
+                            const float b = mbd[md ? iq * 8 + j : 0];  // (read unconditionally)
+                            x = md ? x + b : x;
                             x = ok ? x : -INFINITY;
                             sv[nt][r] = x;
                             mx = fmaxf(mx, x);
                         }
                 }
                 __builtin_amdgcn_wave_barrier();  // (code motion only)
-                mx = max_rows(mx);
                 // lazy rescale (T13): the running max moves only when some row's
                 // new maximum passes it by more than RESCALE (log2 units), so
-                // p = exp2(raw c2 - m) <= 2^RESCALE; l and O always see the same m
+                // p = exp2(raw c2 - m) <= 2^RESCALE; l and O always see the same m.
+                // A row passes iff one of its four lanes does, so the test runs on
+                // the lane maxima and the row maxima are formed only when it fires
                 float m_new = m_run[q2];
                 if (__any(mx * c2 > m_run[q2] + RESCALE)) {
+                    mx = max_rows(mx);
                     m_new = fmaxf(m_run[q2], mx * c2);
                     const float alpha = __builtin_amdgcn_exp2f(m_run[q2] - m_new);
                     l_part[q2] *= alpha;

@@ -34,6 +34,11 @@ struct MambaArgs {
 __device__ __forceinline__ float silu(float x) { return x / (1.f + expf(-x)); }
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 __device__ __forceinline__ float softplus(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+// e^x of a log-decay (cum / segment sums, x <= 0 wherever the value is used) as
+// one v_exp_f32 of x log2(e): the library expf's range reduction and
+// over/underflow selects cost ~14 VALU per value in the chunk-pair loops
+constexpr float LOG2E_F = 1.4426950408889634f;
+__device__ __forceinline__ float exp_decay(float x) { return __builtin_amdgcn_exp2f(x * LOG2E_F); }
 
 // ------------------------------------------------------------------ conv
 // out[b,t,c] = silu(bias[c] + sum_k w[c,k] * in[b, t-3+k, c]), in = zxbcdt[:, off + c]
@@ -1030,18 +1035,20 @@ struct Chunk {
 // hg > 1: one workgroup per group of hg heads (k.h = the group's first head)
 __device__ __forceinline__ Chunk chunk_of(const MambaArgs& a, int nch, int hg = 1) {
     Chunk k;
-    const int64_t ng = a.nheads / hg;
+    // 32-bit quotients (grid ids are 32-bit; the 64-bit forms expand to a
+    // long scalar division sequence per workgroup)
+    const uint32_t ng = (uint32_t)(a.nheads / hg), nc = (uint32_t)nch;
     if (a.xcd) {  // logical id (h fastest, then chunk, then b), contiguous per XCD
-        const int64_t id = __builtin_amdgcn_readfirstlane(xcd_remap((int)blockIdx.x, (int)gridDim.x));
-        k.h = id % ng * hg;
-        const int64_t r = id / ng;
-        k.c = r % nch;
-        k.b = r / nch;
+        const uint32_t id = __builtin_amdgcn_readfirstlane(xcd_remap((int)blockIdx.x, (int)gridDim.x));
+        k.h = (int64_t)(id % ng) * hg;
+        const uint32_t r = id / ng;
+        k.c = r % nc;
+        k.b = r / nc;
     } else {
-        const int64_t bh = blockIdx.x / nch;
-        k.c = blockIdx.x % nch;
+        const uint32_t bh = blockIdx.x / nc;
+        k.c = blockIdx.x % nc;
         k.b = bh / ng;
-        k.h = bh % ng * hg;
+        k.h = (int64_t)(bh % ng) * hg;
     }
     k.t0 = k.c * Q;
     k.nval = (int)min<int64_t>(Q, a.L - k.t0);
@@ -1199,6 +1206,12 @@ __global__ __launch_bounds__(512) void out_kernel(MambaArgs a, const bf16* __res
         f32x4 y2[2][1];
         y2[0][0] = y2[1][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
         mm<false, false, 1>(y2, sCB, 0, sXH, 1, rb, cb, lane);  // [t][p] = sum_n C[t][n] H[p][n]
+        // cum of this lane's rows t / columns s read once, log2 units (as grad_kernel)
+        float ct[2], cs[4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) ct[i] = scum[rb + 16 * i + il] * LOG2E_F;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs[r] = scum[cb + 4 * g + r] * LOG2E_F;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1208,7 +1221,8 @@ __global__ __launch_bounds__(512) void out_kernel(MambaArgs a, const bf16* __res
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int s = s0 + r;
-                    mv.e[r] = (bf16)(s <= t ? gm[i][j][r] * expf(scum[t] - scum[s]) : 0.f);
+                    const float e = __builtin_amdgcn_exp2f(ct[i] - cs[r]);
+                    mv.e[r] = (bf16)(s <= t ? gm[i][j][r] * e : 0.f);
                 }
                 *(uint64_t*)(sM + offd(t, s0 >> 3) + (s0 & 7) * 2) = mv.u;
             }
@@ -1220,7 +1234,7 @@ __global__ __launch_bounds__(512) void out_kernel(MambaArgs a, const bf16* __res
         for (int i = 0; i < 2; ++i) {
             const int t = rb + 16 * i + il;
             if (t >= k.nval) continue;
-            const float et = expf(scum[t]);
+            const float et = exp_decay(scum[t]);
             const int64_t row = k.b * a.L + k.t0 + t;
 #pragma unroll
             for (int j = 0; j < 1; ++j) {
@@ -1403,7 +1417,7 @@ __global__ __launch_bounds__(512) void scan_fwd_kernel(MambaArgs a, const bf16* 
         const float cl = scum[k.nval - 1];
         {
             const int row = tid >> 3;
-            const float f = row < k.nval ? sdt[row] * expf(cl - scum[row]) : 0.f;
+            const float f = row < k.nval ? sdt[row] * exp_decay(cl - scum[row]) : 0.f;
             float v[8];
             unpack8(xr[0], v);
 #pragma unroll
@@ -1415,7 +1429,7 @@ __global__ __launch_bounds__(512) void scan_fwd_kernel(MambaArgs a, const bf16* 
         f32x4 acc[2][1];
         acc[0][0] = acc[1][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
         mm<true, true, 1>(acc, sXB, 0, sXB, 1, rb, cb, lane);  // [p][n] = sum_s X[s][p] B[s][n]
-        const float ecl = expf(cl);
+        const float ecl = exp_decay(cl);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1489,7 +1503,7 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(MambaArgs a, const bf16* 
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
-            const float et = row < k.nval ? expf(scum[row]) : 0.f;
+            const float et = row < k.nval ? exp_decay(scum[row]) : 0.f;
             float v[8];
             unpack8(yr[u], v);
 #pragma unroll
@@ -1502,7 +1516,7 @@ __global__ __launch_bounds__(256) void scan_bwd_kernel(MambaArgs a, const bf16* 
         f32x4 acc[2][2];
         zero22(acc);
         mm<true, true>(acc, sYC, 0, sYC, 1, rb, cb, lane);  // [p][n] = sum_t Ys[t][p] C[t][n]
-        const float ecl = expf(cl);
+        const float ecl = exp_decay(cl);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1611,6 +1625,16 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
     float rowq[2] = {0.f, 0.f}, colq[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) colq[q] = 0.f;
+    // this lane's 2 rows t and 8 columns s of cum, read once (log2 units):
+    // L = 2^(ct - cs), computed for every pair and selected (no branch, no
+    // LDS round trip per pair)
+    float ct[2], cs[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ct[i] = scum[rb + 16 * i + il] * LOG2E_F;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs[j][r] = scum[cb + 16 * j + 4 * g + r] * LOG2E_F;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1620,7 +1644,8 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int s = s0 + r;
-                const float L_ = s <= t ? expf(scum[t] - scum[s]) : 0.f;
+                const float e = __builtin_amdgcn_exp2f(ct[i] - cs[j][r]);
+                const float L_ = s <= t ? e : 0.f;
                 const float m = mt[i][j][r] * L_;
                 const float d = s <= t ? dm[i][j][r] : 0.f;
                 const float q = d * m;
@@ -1658,7 +1683,7 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int s = rb + 16 * i + il;
-        const float ws = s < nv ? expf(cl - scum[s]) : 0.f;
+        const float ws = s < nv ? exp_decay(cl - scum[s]) : 0.f;
         float ddt_p = 0.f, dws = 0.f;
         const int64_t row = k.b * a.L + k.t0 + s;
 #pragma unroll
@@ -1699,7 +1724,7 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int t = rb + 16 * i + il;
-            const float et = expf(scum[t]);
+            const float et = exp_decay(scum[t]);
             float rs = 0.f;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
@@ -1726,7 +1751,7 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int s = rb + 16 * i + il;
-            const float ws = expf(cl - scum[s]);  // rows s >= nv are never stored
+            const float ws = exp_decay(cl - scum[s]);  // rows s >= nv are never stored
 #pragma unroll
             for (int j = 0; j < 2; ++j) dbs[i][j] += ws * tb[i][j];
         }
@@ -1739,7 +1764,7 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
         sred[4 + w] = gd;
     }
     __syncthreads();
-    if (tid == 0) sdcum[nv - 1] += expf(cl) * (sred[0] + sred[1] + sred[2] + sred[3]);
+    if (tid == 0) sdcum[nv - 1] += exp_decay(cl) * (sred[0] + sred[1] + sred[2] + sred[3]);
     __syncthreads();
     if (tid < 64) {
         // da_t = sum_{tau >= t} dcum_tau ; ddt = A da + sum_p dXS x ; d dt_raw = ddt sigmoid(raw)
