@@ -39,6 +39,41 @@ __device__ __forceinline__ float softplus(float x) { return x > 20.f ? x : log1p
 // over/underflow selects cost ~14 VALU per value in the chunk-pair loops
 constexpr float LOG2E_F = 1.4426950408889634f;
 __device__ __forceinline__ float exp_decay(float x) { return __builtin_amdgcn_exp2f(x * LOG2E_F); }
+// cross-lane sums and scans in VALU (DPP / permlane) instead of ds_bpermute
+// round trips (__shfl_xor / __shfl_up: an LDS-latency wait per step)
+template <int CTRL, int ROWS = 0xF, bool BOUND = true>
+__device__ __forceinline__ float dpp_f(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROWS, 0xF, BOUND));
+}
+// sum over the 16 lanes of a row, in every lane: quad xor 1, xor 2, half-row
+// mirror (quad q with its neighbour), row mirror (half with half)
+__device__ __forceinline__ float row16_sum(float v) {
+    v += dpp_f<0xB1>(v);
+    v += dpp_f<0x4E>(v);
+    v += dpp_f<0x141>(v);
+    v += dpp_f<0x140>(v);
+    return v;
+}
+// sum over the lanes l, l ^ 16, l ^ 32, l ^ 48
+__device__ __forceinline__ float cross4_sum(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) { return cross4_sum(row16_sum(v)); }
+// inclusive prefix sum over the 64 lanes: row_shr 1 / 2 / 4 / 8 within the
+// 16-lane rows (lanes without a source add 0), then row_bcast:15 (each row's
+// last lane into rows 1 and 3) and row_bcast:31 (lane 31 into rows 2 and 3)
+__device__ __forceinline__ float wave_scan_dpp(float v) {
+    v += dpp_f<0x111>(v);
+    v += dpp_f<0x112>(v);
+    v += dpp_f<0x114>(v);
+    v += dpp_f<0x118>(v);
+    v += dpp_f<0x142, 0xA, false>(v);
+    v += dpp_f<0x143, 0xC, false>(v);
+    return v;
+}
 
 // ------------------------------------------------------------------ conv
 // out[b,t,c] = silu(bias[c] + sum_k w[c,k] * in[b, t-3+k, c]), in = zxbcdt[:, off + c]
@@ -1061,13 +1096,7 @@ __device__ __forceinline__ void dt_cum(const MambaArgs& a, const Chunk& k, const
         float d = 0.f;
         if (tid < k.nval) d = softplus((float)zx[(k.b * a.L + t) * a.ldz + a.d_inner + a.conv_dim + k.h] + dt_bias[k.h]);
         sdt[tid] = d;
-        float v = d * A;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const float u = __shfl_up(v, o, 64);
-            if (tid >= o) v += u;
-        }
-        scum[tid] = v;
+        scum[tid] = wave_scan_dpp(d * A);
     }
 }
 // 16-B chunk e (row e >> 3, chunk e & 7) of a 64-column bf16 tile starting at column col0 of xc rows
@@ -1354,13 +1383,7 @@ __device__ __forceinline__ void dt_cum_raw(const Chunk& k, unsigned raw, float b
     if (tid < 64) {
         const float d = tid < k.nval ? softplus(__uint_as_float(raw << 16) + bias) : 0.f;
         sdt[tid] = d;
-        float v = d * A;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const float u = __shfl_up(v, o, 64);
-            if (tid >= o) v += u;
-        }
-        scum[tid] = v;
+        scum[tid] = wave_scan_dpp(d * A);  // (the same scan as dt_cum: identical cum values)
     }
 }
 
@@ -1602,7 +1625,7 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
     }
     dt_cum(a, k, zx, dt_bias, A, sdt, scum, tid);
     if (tid < 64) sdcum[tid] = sddt[tid] = 0.f;
-    hdh = wave_sum(hdh);
+    hdh = wave_sum_dpp(hdh);
     if (lane == 0) sred[w] = hdh;
     __syncthreads();
     const float cl = scum[nv - 1];
@@ -1660,16 +1683,12 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
     // dcum_t += sum_s dM M ; dcum_s -= sum_t dM M
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-        float v = rowq[i];
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
+        const float v = cross4_sum(rowq[i]);
         if (g == 0) atomicAdd(&sdcum[rb + 16 * i + il], v);
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-        float v = colq[q];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+        const float v = row16_sum(colq[q]);
         if (il == 0) atomicAdd(&sdcum[cb + 16 * (q >> 2) + 4 * g + (q & 3)], -v);
     }
     __syncthreads();  // M, dG images
@@ -1705,10 +1724,8 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
             }
             if (s < nv) *(f32x4*)(dxc + row * a.ldxc + k.h * P + pc) = o;
         }
-        ddt_p += __shfl_xor(ddt_p, 16, 64);
-        ddt_p += __shfl_xor(ddt_p, 32, 64);
-        dws += __shfl_xor(dws, 16, 64);
-        dws += __shfl_xor(dws, 32, 64);
+        ddt_p = cross4_sum(ddt_p);
+        dws = cross4_sum(dws);
         if (g == 0) {
             atomicAdd(&sddt[s], ddt_p);
             atomicAdd(&sdcum[s], -dws);
@@ -1737,8 +1754,7 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
                     dcs[i][j][r] += et * dyh[i][j][r];
                 }
             }
-            rs += __shfl_xor(rs, 16, 64);
-            rs += __shfl_xor(rs, 32, 64);
+            rs = cross4_sum(rs);
             if (g == 0) atomicAdd(&sdcum[t], rs);
         }
     }
@@ -1757,8 +1773,8 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
         }
     }
     // dcum_last += sum_s dws_s + e^{cum_last} sum dH o H
-    dws_tot = wave_sum(dws_tot) * 0.25f;  // each row sum was held by its 4 g-lanes
-    gd = wave_sum(gd);
+    dws_tot = wave_sum_dpp(dws_tot) * 0.25f;  // each row sum was held by its 4 g-lanes
+    gd = wave_sum_dpp(gd);
     if (lane == 0) {
         atomicAdd(&sdcum[nv - 1], dws_tot);
         sred[4 + w] = gd;
@@ -1784,8 +1800,8 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
             dzx[(k.b * a.L + t) * a.ldz + a.d_inner + a.conv_dim + k.h] = (TD)draw;
             gdb = draw;
         }
-        gA = wave_sum(gA);
-        gdb = wave_sum(gdb);
+        gA = wave_sum_dpp(gA);
+        gdb = wave_sum_dpp(gdb);
         if (tid == 0) {
             atomicAdd(gA_log + k.h, gA * A);  // A = -exp(A_log) -> dA/dA_log = A
             atomicAdd(gdt_bias + k.h, gdb);
