@@ -1784,12 +1784,11 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
     __syncthreads();
     if (tid < 64) {
         // da_t = sum_{tau >= t} dcum_tau ; ddt = A da + sum_p dXS x ; d dt_raw = ddt sigmoid(raw)
-        float v = tid < nv ? sdcum[tid] : 0.f;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const float u = __shfl_down(v, o, 64);
-            if (tid + o < 64) v += u;
-        }
+        // (suffix sum = prefix scan over the reversed lanes, back through the
+        // same LDS row: one wave, its LDS operations in issue order)
+        const float rv = 63 - tid < nv ? sdcum[63 - tid] : 0.f;
+        sdcum[63 - tid] = wave_scan_dpp(rv);
+        const float v = sdcum[tid];
         float gA = 0.f, gdb = 0.f;
         if (tid < nv) {
             const int64_t t = k.t0 + tid;
