@@ -227,16 +227,27 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
             // skew + online softmax per group (scores unscaled until the exp:
             // max commutes with the positive scale, p = exp2(raw * c2 - m))
             bf16x8 pf[2];
+            // skewed QR values of both groups: group 0's window written and read
+            // back, then group 1's into the same scratch rows, all issued before
+            // either is used (a wave's LDS operations execute in issue order, so
+            // each read sees its group's writes and group 1's writes follow group
+            // 0's reads without an lgkmcnt(0) between: one LDS round trip per
+            // tile instead of one per group)
+            float xs[2][2][4];
 #pragma unroll
             for (int q2 = 0; q2 < 2; ++q2) {
-                const int iq = iw + 16 * q2 + il;
-                // (a wave's LDS operations execute in issue order, so the skewed
-                // reads below see these writes, and the next group's writes
-                // follow this group's reads, without an lgkmcnt(0) between:
-                // the compiler waits only where a read's value is used)
 #pragma unroll
                 for (int t = 0; t < 3; ++t) *(f32x4*)(scw + il * SCR + t * 16 + 4 * g) = qacc[q2][t];
                 __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xs[q2][nt][r] = scw[il * SCR + nt * 16 + 4 * g + r - il + 15];
+                __builtin_amdgcn_wave_barrier();
+            }
+#pragma unroll
+            for (int q2 = 0; q2 < 2; ++q2) {
+                const int iq = iw + 16 * q2 + il;
                 float sv[2][4];
                 float mx = -INFINITY;
                 // masking only where a key may follow a query of the group or
@@ -248,7 +259,7 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int jl = nt * 16 + 4 * g + r;
-                            const float x = sacc[q2][nt][r] + scw[il * SCR + jl - il + 15];
+                            const float x = sacc[q2][nt][r] + xs[q2][nt][r];
                             sv[nt][r] = x;
                             mx = fmaxf(mx, x);
                         }
@@ -259,9 +270,8 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
                         for (int r = 0; r < 4; ++r) {
                             const int jl = nt * 16 + 4 * g + r;
                             const int j = j0 + jl;
-                            const float x = sacc[q2][nt][r] + scw[il * SCR + jl - il + 15];
-                            // (& not &&: a short-circuit test became a branch
-                            // around each scratch read, with a wait per read)
+                            const float x = sacc[q2][nt][r] + xs[q2][nt][r];
+                            // (& not &&: no branch per element)
                             sv[nt][r] = ((j < S) & (j <= iq)) ? x : -INFINITY;
                             mx = fmaxf(mx, sv[nt][r]);
                         }
@@ -272,7 +282,7 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
                         for (int r = 0; r < 4; ++r) {
                             const int jl = nt * 16 + 4 * g + r;
                             const int j = j0 + jl;
-                            float x = sacc[q2][nt][r] + scw[il * SCR + jl - il + 15];
+                            float x = sacc[q2][nt][r] + xs[q2][nt][r];
                             const bool ok = (j < S) & ((j <= iq) | (j < nm));
                             const bool md = (j >= iq + 2) & (j < nm) & (iq >= 0);
                             const float b = mbd[md ? iq * 8 + j : 0];  // (read unconditionally)
