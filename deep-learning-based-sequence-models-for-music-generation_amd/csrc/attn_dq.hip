@@ -23,9 +23,10 @@
 // against R rows [R0 + 32 t, +32); the K term of half wr contracts key block
 // u = t - 4 + 2 wr, whose skewed columns lie in r-blocks t-2 .. t for both
 // halves. LDS (80 KB): a ring of 4 r-blocks (128 x 32), 4 key blocks and 2 R
-// blocks (32 x 128). Every wave stages a quarter of each block, global ->
-// registers -> LDS: the key and R blocks one iteration ahead, the ring block
-// (the HBM stream) two.
+// blocks (32 x 128). Every wave stages a quarter of each block by LDS-DMA one
+// iteration ahead. (Round 6 measured register staging of all three streams
+// with the ring two iterations ahead, and a split with the ring through
+// registers: 539 / 537 us against 525 us for this form, same box.)
 #include "attn_tiles.h"
 
 namespace {
@@ -90,42 +91,38 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
     const int wr = w & 1;  // query half
     const int rho = lane & 15, g = lane >> 4;
 
-    // ---- staging: every wave moves a quarter of each block, global -> registers
-    // -> LDS. Iteration t loads key block t-1 and R block t+1 (written to LDS at
-    // its end) and ring block t+2 (written one iteration later: the dQR stream
-    // is the HBM one, so it gets two iterations of latency). Per lane: ring rows
-    // 32 w + 16 n + lane / 4, chunk lane % 4; key / R rows 8 w + 4 n + lane / 16,
-    // chunk kr_pos(row, lane % 16) (n = 0, 1).
+    // ---- staging: every wave moves a quarter of each block by LDS-DMA (lane-
+    // linear 1 KB pieces, the images' swizzles applied to the source addresses).
+    // Iteration t fills the slots the previous barrier released: ring block
+    // t+1, key block t-1, R block t+1, all read from iteration t+1 on. Per
+    // lane: ring rows 32 w + 16 n + lane / 4, source chunk (lane % 4) ^ f(row);
+    // key / R rows 8 w + 4 n + lane / 16, source chunk kr_pos(row, lane % 16)
+    // (n = 0, 1: the wave's two pieces per block)
     const __amdgpu_buffer_rsrc_t rQ =
         dq_rsrc(dqr + ((int64_t)h * a.B + b) * S * ldr, (uint32_t)((int64_t)S * ldr * 2));
     const __amdgpu_buffer_rsrc_t rK = dq_rsrc((const bf16*)a.qkv + (int64_t)b * S * ldq, (uint32_t)((int64_t)S * ldq * 2));
     const __amdgpu_buffer_rsrc_t rR = dq_rsrc((const bf16*)a.R + (int64_t)h * a.S_max * HS, (uint32_t)(S * HS * 2));
     uint32_t q_off[2], k_off[2], r_off[2];  // global byte offsets at block 0
-    int q_lds[2], kr_lds[2], q_lim[2];      // LDS offsets in a slot; ring block bi valid while 32 bi < q_lim
+    int q_lim[2];                           // ring block bi valid while 32 bi < q_lim
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
-        const int ro = 32 * w + 16 * n + (lane >> 2), k = lane & 3, i = i0 + ro;
+        const int ro = 32 * w + 16 * n + (lane >> 2), k = (lane & 3) ^ ring_f(ro), i = i0 + ro;
         const bool ok = i >= 0 && i < S;
         q_off[n] = (uint32_t)(((int64_t)(ok ? i : 0) * ldr + R0 + 8 * k) * 2);
-        q_lds[n] = ro * 64 + ((k ^ ring_f(ro)) << 4);
         q_lim[n] = ok ? S - (R0 + 8 * k) : 0;
         const int kr = 8 * w + 4 * n + (lane >> 4), ch = kr_pos(kr, lane & 15);
         k_off[n] = (uint32_t)(((int64_t)kr * ldq + (int64_t)(H + h) * HS + ch * 8) * 2);
         r_off[n] = (uint32_t)(((R0 + kr) * HS + ch * 8) * 2);
-        kr_lds[n] = kr * 256 + (lane & 15) * 16;
     }
-    // ring blocks in two register sets alternating between iterations (two
-    // iterations of latency for the HBM stream), key / R blocks in one
-    u32x4 sq0[2], sq1[2], sk[2], sr[2];
-#define DQ_LOAD_RING(dst, bi)                                                                                  \
-    _Pragma("unroll") for (int n = 0; n < 2; ++n) dst[n] = __builtin_amdgcn_raw_buffer_load_b128(             \
-        rQ, BK * (bi) < q_lim[n] ? q_off[n] + (uint32_t)(BK * (bi) * 2) : OOB, 0, 0)
-#define DQ_LOAD_KR(u, rt)                                                                                      \
+#define DQ_DMA(t)                                                                                              \
     _Pragma("unroll") for (int n = 0; n < 2; ++n) {                                                            \
-        sk[n] = __builtin_amdgcn_raw_buffer_load_b128(                                                         \
-            rK, (u) >= 0 && (u) < nk ? k_off[n] + (uint32_t)((int64_t)BK * (u) * ldq * 2) : OOB, 0, 0);        \
-        sr[n] = __builtin_amdgcn_raw_buffer_load_b128(rR, (rt) < nk ? r_off[n] + (uint32_t)(BK * (rt) * HS * 2) : OOB, \
-                                                      0, 0);                                                   \
+        const int bi_ = (t) + 1, u_ = (t) - 1, rt_ = (t) + 1;                                                  \
+        lds_dma16(rQ, smem + O_RING + (bi_ & 3) * SLOT + (2 * w + n) * 1024,                                   \
+                  BK * bi_ < q_lim[n] ? q_off[n] + (uint32_t)(BK * bi_ * 2) : OOB);                            \
+        lds_dma16(rK, smem + O_K + (u_ & 3) * SLOT + (2 * w + n) * 1024,                                       \
+                  u_ >= 0 && u_ < nk ? k_off[n] + (uint32_t)((int64_t)BK * u_ * ldq * 2) : OOB);               \
+        lds_dma16(rR, smem + O_R + (rt_ & 1) * SLOT + (2 * w + n) * 1024,                                      \
+                  rt_ < nk ? r_off[n] + (uint32_t)(BK * rt_ * HS * 2) : OOB);                                  \
     }
 
     // ---- fragment addressing (ring rows 64 wr + 16 rf + rho; f(row) depends on rho only)
@@ -203,54 +200,23 @@ __global__ __launch_bounds__(NT, 2) void flash_bwd_dq_kernel(AttnArgs a, const b
             }
         }
     };
-    // the LDS writes of iteration t: ring block t+1, key block t-1, R block t+1
-#define DQ_STORE(t, sq)                                                                                        \
-    {                                                                                                          \
-        char* dq_ = smem + O_RING + (((t) + 1) & 3) * SLOT;                                                    \
-        char* dk_ = smem + O_K + (((t) - 1) & 3) * SLOT;                                                       \
-        char* dr_ = smem + O_R + (((t) + 1) & 1) * SLOT;                                                       \
-        _Pragma("unroll") for (int n = 0; n < 2; ++n) {                                                        \
-            *(u32x4*)(dq_ + q_lds[n]) = sq[n];                                                                 \
-            *(u32x4*)(dk_ + kr_lds[n]) = sk[n];                                                                \
-            *(u32x4*)(dr_ + kr_lds[n]) = sr[n];                                                                \
-        }                                                                                                      \
-    }
-    // iteration t: key block t-1 and R block t+1 (written at its end), ring
-    // block t+2 into the other ring set (written one iteration later; the sets
-    // alternate, so no register copy waits for a load in flight)
-#define DQ_ITER(t, QW, QL)                                                                                     \
-    DQ_LOAD_KR((t) - 1, (t) + 1);                                                                              \
-    DQ_LOAD_RING(QL, (t) + 2);                                                                                 \
-    compute(t);                                                                                                \
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");                                                          \
-    DQ_STORE(t, QW);                                                                                           \
-    bar();
-
-    // prologue: ring block 0 and R block 0 into LDS; ring block 1 into set 0
-    // (written by iteration 0)
-    DQ_LOAD_RING(sq1, 0);
-    DQ_LOAD_KR(-2, 0);
-    DQ_LOAD_RING(sq0, 1);
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    // prologue: ring block 0 and R block 0 (key block -1 reads as zeros)
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
-        *(u32x4*)(smem + O_RING + q_lds[n]) = sq1[n];
-        *(u32x4*)(smem + O_R + kr_lds[n]) = sr[n];
+        lds_dma16(rQ, smem + O_RING + (2 * w + n) * 1024, 0 < q_lim[n] ? q_off[n] : OOB);
+        lds_dma16(rR, smem + O_R + (2 * w + n) * 1024, 0 < nk ? r_off[n] : OOB);
     }
-    bar();
-    int t = 0;
-    for (; t + 1 < T; t += 2) {
-        DQ_ITER(t, sq0, sq1)
-        DQ_ITER(t + 1, sq1, sq0)
-    }
-    if (t < T) {
-        DQ_ITER(t, sq0, sq1)
-    }
-#undef DQ_ITER
-#undef DQ_STORE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#undef DQ_LOAD_RING
-#undef DQ_LOAD_KR
+    bar();
+    for (int t = 0; t < T; ++t) {
+        DQ_DMA(t);
+        compute(t);
+        // this wave's pieces landed; the barrier orders every wave's for the
+        // reads of iteration t+1 and releases iteration t's slots
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+    }
+#undef DQ_DMA
 
     // the R-term waves hand their sums to the K-term wave of the same half
     f32x4* scr = (f32x4*)smem;
