@@ -115,12 +115,12 @@ CLASSIFY = {
 }
 
 
-PMC_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r5")
+PMC_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r6")
 
 
 def pmc_traffic(cls, name="pmc_traffic.json"):
     """HBM bytes per launch of a kernel class from the committed PMC passes
-    (tools/pmc_traffic.py, profiles/r5/<name>), or None."""
+    (tools/pmc_traffic.py, profiles/r6/<name>), or None."""
     try:
         with open(os.path.join(PMC_DIR, name)) as f:
             c = json.load(f)["classes"].get(cls)
@@ -458,7 +458,7 @@ def mamba_leg(dev, rank, world, timer, steps=3, B=8, T=4096, overlap=True, class
                            "bound": "hbm", "achieved": r["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
                            "frac": r["frac"], "traffic": pmc_traffic("ssd_fwd", "pmc_mamba_traffic.json"),
                            "avg_launch_ms": r["avg_launch_ms"], "algorithmic_bytes": int(r["work_per_launch"]),
-                           "traffic_source": "profiles/r5/pmc_mamba_traffic.json (FETCH_SIZE x2 + WRITE_SIZE passes "
+                           "traffic_source": "profiles/r6/pmc_mamba_traffic.json (FETCH_SIZE x2 + WRITE_SIZE passes "
                                              "of bench.py --only mamba)"}
     return out
 
@@ -617,7 +617,7 @@ def main():
                          "bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"],
                          "frac": r["frac"], "traffic": pmc_traffic(dom), "avg_launch_ms": r["avg_launch_ms"],
                          "algorithmic_work_per_launch": r["work_per_launch"],
-                         "traffic_source": "profiles/r5/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
+                         "traffic_source": "profiles/r6/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
                                            "passes of this step, bytes per class launch)"},
             "classes": classes,
             "classes_source": class_src,
