@@ -14,6 +14,7 @@
 //
 // fp32 exact path: plain LDS-tiled FMA kernel, fp32 end to end (parity mode).
 #include "gemm.h"
+#include "lds_dma.h"
 
 extern "C" size_t msq_colsum_workspace(int64_t rows, int64_t cols);
 extern "C" int msq_colsum(float* out, int accumulate, const void* x, int dtype, int64_t rows, int64_t cols,
@@ -423,12 +424,28 @@ namespace {
 // that traffic (1.05 GB per cfg-2 launch with 128 rows); the A operand and the
 // per-segment K ranges are as in gemm_bf16_kernel. fp32 split-K partials only
 // (ACCUM with ws), reduced by splitk_reduce.
-constexpr int TBM = 256, TNT = 512;
+// The product streams 2 GB of dQR per launch at one workgroup per CU, so the
+// k-steps are staged by LDS-DMA three deep (48 KB stages, two in flight while
+// the third is multiplied; each wave moves 6 lane-linear 1 KB pieces per stage,
+// the image swizzle applied to the source address): with one register-staged
+// step ahead the kernel sustained 4.9 TB/s (440 us), latency-bound.
+constexpr int TBM = 256, TNT = 512, TNST = 3;
+constexpr uint32_t TRI_OOB = 0xFFFF0000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tri_rsrc(const void* base, uint64_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void* p = (void*)(((uint64_t)hi << 32) | lo);
+    // (an integer select: min<uint64_t> went through f64 and a VGPR)
+    const uint32_t n = bytes < (uint64_t)(TRI_OOB - 1) ? (uint32_t)bytes : TRI_OOB - 1;
+    return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(n), 0x00020000);
+}
 __global__ __launch_bounds__(TNT, 1) void gemm_tri2_256_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tiles = g.tiles_m * g.tiles_n;
-    int bid = xcd_remap(blockIdx.x, gridDim.x);
+    int bid = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x));
     const int kslice = bid % g.ksplit;
     bid /= g.ksplit;
     const int bz = bid / tiles;
@@ -437,6 +454,9 @@ __global__ __launch_bounds__(TNT, 1) void gemm_tri2_256_kernel(GemmArgs g) {
     const int m0 = tm * TBM, n0 = tn * BN;
     const bf16* A = (const bf16*)g.A + bz * g.sA;
     const bf16* B = (const bf16*)g.B + bz * g.sB;
+    // 32-bit source offsets (checked at launch); rows past K and columns past
+    // the row pitch read as zeros (columns >= M / N inside the pitch feed only
+    // output rows / columns that are not stored)
     constexpr int SA = TBM * BK * 2, SB = BN * BK * 2, STG = SA + SB;
     const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
     f32x4 acc[4][4];
@@ -454,40 +474,40 @@ __global__ __launch_bounds__(TNT, 1) void gemm_tri2_256_kernel(GemmArgs g) {
             if (cs < sg_hi) ck = cs * g.seg + imin, cke = (cs + 1) * g.seg;
         }
     };
-    struct Regs { u32x4 a[4], b[2]; };
-    auto load = [&](Regs& x, int64_t k0, int64_t kend) {
+    // per-lane part of the pieces: A piece P = wid + 8 i (half P / 16, rows
+    // 4 (P % 16) ..), B piece Q = wid + 8 i (rows 4 Q ..); lane row +lane / 16,
+    // image position lane % 16 holds chunk swz_mn(row, lane % 16)
+    int arow[4], acol[4], brow[2], bcol[2];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {  // A [K][M]: 64 k rows x 32 chunks (two 128-column halves)
-            const int c = tid + TNT * i, kr = (c & 1023) >> 4, ch = c & 15, half = c >> 10;
-            const int64_t gk = k0 + kr, gm = m0 + half * 128 + ch * 8;
-            // columns m >= M only feed output rows that are not stored: a chunk
-            // inside the row pitch is read whole (no element-wise edge path)
-            const int valid = (gk < kend) ? (gm + 8 <= g.lda ? 8 : (int)min<int64_t>(8, g.M - gm)) : 0;
-            x.a[i] = load_chunk(A + gk * g.lda + gm, valid);
-        }
+    for (int i = 0; i < 4; ++i) {
+        const int P = wid + 8 * i, row = ((P & 15) << 2) + (lane >> 4);
+        arow[i] = row;
+        acol[i] = m0 + (P >> 4) * 128 + swz_mn(row, lane & 15) * 8;
+    }
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {  // B [K][N]: 64 k rows x 16 chunks
-            const int c = tid + TNT * i, kr = c >> 4, ch = c & 15;
-            const int64_t gk = k0 + kr, gn = n0 + ch * 8;
-            const int valid = (gk < kend) ? (int)min<int64_t>(8, g.N - gn) : 0;
-            x.b[i] = load_chunk(B + gk * g.ldb + gn, valid);
-        }
-    };
-    auto store = [&](const Regs& x, char* st) {
+    for (int i = 0; i < 2; ++i) {
+        const int Q = wid + 8 * i, row = (Q << 2) + (lane >> 4);
+        brow[i] = row;
+        bcol[i] = n0 + swz_mn(row, lane & 15) * 8;
+    }
+    auto issue = [&](char* st) -> bool {
+        if (cs >= sg_hi) return false;
+        const __amdgpu_buffer_rsrc_t rA = tri_rsrc(A, (uint64_t)g.K * g.lda * 2);
+        const __amdgpu_buffer_rsrc_t rB = tri_rsrc(B, (uint64_t)g.K * g.ldb * 2);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int c = tid + TNT * i, kr = (c & 1023) >> 4, ch = c & 15, half = c >> 10;
-            *(u32x4*)(st + half * (SA / 2) + kr * 256 + swz_mn(kr, ch) * 16) = x.a[i];
+            const int P = wid + 8 * i;
+            const int64_t gk = ck + arow[i];
+            const uint32_t off = gk < cke ? (uint32_t)((gk * g.lda + acol[i]) * 2) : TRI_OOB;
+            lds_dma16(rA, st + (P >> 4) * (SA / 2) + (P & 15) * 1024, off);
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const int c = tid + TNT * i, kr = c >> 4, ch = c & 15;
-            *(u32x4*)(st + SA + kr * 256 + swz_mn(kr, ch) * 16) = x.b[i];
+            const int Q = wid + 8 * i;
+            const int64_t gk = ck + brow[i];
+            const uint32_t off = gk < cke ? (uint32_t)((gk * g.ldb + bcol[i]) * 2) : TRI_OOB;
+            lds_dma16(rB, st + SA + Q * 1024, off);
         }
-    };
-    auto fetch = [&](Regs& x) {
-        if (cs >= sg_hi) return false;
-        load(x, ck, cke);
         ck += BK;
         skip_empty();
         return true;
@@ -508,26 +528,30 @@ __global__ __launch_bounds__(TNT, 1) void gemm_tri2_256_kernel(GemmArgs g) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         }
     };
-    char* s0 = smem;
-    char* s1 = smem + STG;
-    Regs r0, r1;
+    // stages rotate through the three slots: pc is multiplied while pn and pa
+    // land; a wave's 6 pieces of a stage retire by its counted vmcnt, the
+    // barrier after it orders every wave's for the reads and releases the slot
+    // read in the previous step
+    char* pc = smem;
+    char* pn = smem + STG;
+    char* pa = smem + 2 * STG;
     skip_empty();
-    bool v0 = fetch(r0);
-    if (v0) store(r0, s0);
-    bool v1 = fetch(r1);
-    __syncthreads();
-    while (v0) {
-        const bool v2 = fetch(r0);
-        mma(s0);
-        if (v1) store(r1, s1);
-        __syncthreads();
-        if (!v1) break;
-        const bool v3 = fetch(r1);
-        mma(s1);
-        if (v2) store(r0, s0);
-        __syncthreads();
-        v0 = v2;
-        v1 = v3;
+    bool vc = issue(pc);
+    bool vn = vc && issue(pn);
+    while (vc) {
+        if (vn) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const bool va = vn && issue(pa);
+        mma(pc);
+        char* t = pc;
+        pc = pn;
+        pn = pa;
+        pa = t;
+        vc = vn;
+        vn = va;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -575,7 +599,8 @@ int gemm_bf16_tri(int tri, int64_t seg, int ta, int tb, int64_t M, int64_t N, in
         g.ws = ws;
     // the dR product (fp32 C += dQR^T q): 256-row M tiles when the split-K
     // workspace holds their partials (else the 128 tile below)
-    if (tri == 2 && ta == 1 && tb == 1 && epi == MSQ_EPI_ACCUM && c_dtype == MSQ_F32 && ws && N % 4 == 0) {
+    if (tri == 2 && ta == 1 && tb == 1 && epi == MSQ_EPI_ACCUM && c_dtype == MSQ_F32 && ws && N % 4 == 0 &&
+        K * lda * 2 < (int64_t)TRI_OOB && K * ldb * 2 < (int64_t)TRI_OOB) {  // 32-bit DMA source offsets
         GemmArgs h = g;
         h.tiles_m = (int)((M + TBM - 1) / TBM);
         const int64_t nseg = K / seg, nb = (int64_t)h.tiles_m * h.tiles_n * batch;
@@ -585,7 +610,7 @@ int gemm_bf16_tri(int tri, int64_t seg, int ta, int tb, int64_t M, int64_t N, in
         h.ksplit = (int)((nseg + spb - 1) / spb);
         if (ws_bytes >= splitk_ws_bytes(M, N, batch, h.ksplit) && splitk_ws_bytes(M, N, batch, h.ksplit)) {
             h.ws = ws;
-            constexpr int lds = 2 * (TBM * BK * 2 + BN * BK * 2);
+            constexpr int lds = TNST * (TBM * BK * 2 + BN * BK * 2);
             static bool attr = false;
             if (!attr) {
                 (void)hipFuncSetAttribute((const void*)gemm_tri2_256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
