@@ -37,7 +37,10 @@ struct SkinnyConv {
     const float* b;  // [cd]
     int64_t c0, cd;
 };
-__device__ __forceinline__ float conv_silu(float x) { return x / (1.f + expf(-x)); }
+// as mamba.hip's silu (v_exp_f32 + v_rcp_f32), so the decode step matches the forward
+__device__ __forceinline__ float conv_silu(float x) {
+    return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-x * 1.4426950408889634f));
+}
 __device__ __forceinline__ void conv_apply(const SkinnyConv& cv, int64_t m, int64_t n, f32x4 v) {
     const int64_t c = n - cv.c0;
     if (c < 0 || c >= cv.cd) return;  // c0, cd % 4 == 0: the 4 columns are wholly in or out

@@ -31,8 +31,13 @@ struct MambaArgs {
     int xcd;
 };
 
-__device__ __forceinline__ float silu(float x) { return x / (1.f + expf(-x)); }
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+// sigmoid by one v_exp_f32 and one v_rcp_f32 (~1 ulp each; the library expf
+// and the IEEE division cost ~25 VALU per element); mamba_step.hip's silu is
+// the same expression, so the cached decode step matches the forward
+__device__ __forceinline__ float sigm(float x) {
+    return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-x * 1.4426950408889634f));
+}
+__device__ __forceinline__ float silu(float x) { return x * sigm(x); }
 __device__ __forceinline__ float softplus(float x) { return x > 20.f ? x : log1pf(expf(x)); }
 // e^x of a log-decay (cum / segment sums, x <= 0 wherever the value is used) as
 // one v_exp_f32 of x log2(e): the library expf's range reduction and
@@ -872,7 +877,7 @@ __global__ __launch_bounds__(256, (NK >= 8 ? 2 : 1)) void gnorm_bwd_kernel(
 // buffered by iteration, one barrier per row pair); every wave runs the same
 // number of iterations (rows past the end skip their loads and stores).
 template <typename TD, int NKH>
-__global__ __launch_bounds__(256, 4) void gnorm_bwd2_kernel(
+__global__ __launch_bounds__(256, 3) void gnorm_bwd2_kernel(
     const bf16* __restrict__ y, int64_t ldy, const bf16* __restrict__ z, int64_t ldz, const float* __restrict__ w,
     const float* __restrict__ rstd, const float* __restrict__ dout, int64_t ldd, bf16* __restrict__ dy,
     TD* __restrict__ dz, float* __restrict__ dw, int64_t rows, int dn) {
@@ -882,47 +887,74 @@ __global__ __launch_bounds__(256, 4) void gnorm_bwd2_kernel(
     };
     const int lane = threadIdx.x & 63, ws = threadIdx.x >> 6, q = ws >> 1, h = ws & 1;
     __shared__ f32x4 red[4][64 * NKH];
+    __shared__ f32x4 sw[2 * 64 * NKH];  // w, read from LDS in the loop (a global load there
+                                        // would wait, in order, for the prefetched rows)
     __shared__ float sred[2][2][2];  // [iteration parity][pair][half]
 #pragma unroll
     for (int k = 0; k < NKH; ++k) red[ws][lane + 64 * k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int e = threadIdx.x; e < 2 * 64 * NKH; e += 256)
+        sw[e] = 4 * e < dn ? *(const f32x4*)(w + 4 * e) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    // the next row pair's y / z / dout / rstd are loaded while this pair is
+    // reduced and written (one pair at a time it waited on every load: the
+    // LayerNorm backward's fix, round 6)
+    uint2 nyv[NKH], nzv[NKH];
+    f32x4 ndv[NKH];
+    float nr = 0.f;
+    // (unconditional loads from a clamped row / column: exec-masked loads made
+    // the compiler wait vmcnt(0) for the prefetch at every use; rows past the
+    // end are skipped below, columns past dn are never stored)
+    auto fetch = [&](int64_t row) {
+        const int64_t rr = row < rows ? row : rows - 1;
+        nr = rstd[rr];
+#pragma unroll
+        for (int k = 0; k < NKH; ++k) {
+            const int c = min(lane * 4 + 256 * (h * NKH + k), dn - 4);
+            nyv[k] = *(const uint2*)(y + rr * ldy + c);
+            ndv[k] = *(const f32x4*)(dout + rr * ldd + c);
+            nzv[k] = *(const uint2*)(z + rr * ldz + c);
+        }
+    };
+    const int64_t stride = (int64_t)gridDim.x * 2;
     int it = 0;
-    for (int64_t base = blockIdx.x * 2LL; base < rows; base += (int64_t)gridDim.x * 2, ++it) {
+    fetch(blockIdx.x * 2LL + q);
+    for (int64_t base = blockIdx.x * 2LL; base < rows; base += stride, ++it) {
         const int64_t row = base + q;
         const bool ok = row < rows;
-        const float r = ok ? rstd[row] : 0.f;
+        const float r = nr;
         uint2 yv[NKH], zv[NKH];
         f32x4 dv[NKH];
+#pragma unroll
+        for (int k = 0; k < NKH; ++k) {
+            yv[k] = nyv[k];
+            zv[k] = nzv[k];
+            dv[k] = ndv[k];
+        }
+        fetch(row + stride);
         float s = 0.f;
 #pragma unroll
         for (int k = 0; k < NKH; ++k) {
             const int c = lane * 4 + 256 * (h * NKH + k);
-            yv[k] = zv[k] = uint2{};
-            dv[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
-            if (ok && c < dn) {
-                yv[k] = *(const uint2*)(y + row * ldy + c);
-                dv[k] = *(const f32x4*)(dout + row * ldd + c);
-                zv[k] = *(const uint2*)(z + row * ldz + c);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < NKH; ++k) {
-            const int c = lane * 4 + 256 * (h * NKH + k);
             if (c >= dn) continue;
-            const f32x4 wv = *(const f32x4*)(w + c);
+            const f32x4 wv = sw[c / 4];
             const f32x4 zk = widen(zv[k]), yk = widen(yv[k]);
 #pragma unroll
             for (int t = 0; t < 4; ++t) s += dv[k][t] * wv[t] * yk[t] * silu(zk[t]) * r;
         }
         s = wave_sum(s);
         if (lane == 0) sred[it & 1][q][h] = s;
-        __syncthreads();
+        // (a raw barrier: the fence of __syncthreads would wait for the next
+        // pair's loads, vmcnt(0))
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
         const float mdn = (sred[it & 1][q][0] + sred[it & 1][q][1]) / dn;
         if (!ok) continue;
 #pragma unroll
         for (int k = 0; k < NKH; ++k) {
             const int c = lane * 4 + 256 * (h * NKH + k);
             if (c >= dn) continue;
-            const f32x4 wv = *(const f32x4*)(w + c);
+            const f32x4 wv = sw[c / 4];
             const f32x4 zk = widen(zv[k]), yk = widen(yv[k]);
             f32x4 o, zo, pw = red[ws][lane + 64 * k];
 #pragma unroll
@@ -1951,8 +1983,9 @@ extern "C" int msq_mamba_gnorm_bwd(void* dy, void* dzxbcdt, const void* y, int64
     // reduces its dw partials in LDS first
     const dim3 grid(768);
     if (dtype == MSQ_BF16 && d_inner > 1024 && d_inner <= 2048) {
-        // the row over a wave pair (4 waves per SIMD: 4 workgroups per CU)
-        hipLaunchKernelGGL((gnorm_bwd2_kernel<bf16, 4>), dim3(1024), dim3(256), 0, s, (const bf16*)y, ldy,
+        // the row over a wave pair, the next pair's loads in flight (3 waves per
+        // SIMD: 3 workgroups per CU)
+        hipLaunchKernelGGL((gnorm_bwd2_kernel<bf16, 4>), dim3(768), dim3(256), 0, s, (const bf16*)y, ldy,
                            (const bf16*)zxbcdt, ldz, w, rstd, dout, ldd, (bf16*)dy, (bf16*)dzxbcdt, dw, rows,
                            (int)d_inner);
         MSQ_LAUNCH_CHECK();

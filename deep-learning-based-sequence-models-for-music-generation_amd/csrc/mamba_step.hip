@@ -22,7 +22,10 @@ namespace {
 
 constexpr int P = 64, N = 64, KW = 4;
 
-__device__ __forceinline__ float silu(float x) { return x / (1.f + expf(-x)); }
+// as mamba.hip's silu (v_exp_f32 + v_rcp_f32), so the step matches the forward
+__device__ __forceinline__ float silu(float x) {
+    return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-x * 1.4426950408889634f));
+}
 __device__ __forceinline__ float softplus(float x) { return x > 20.f ? x : log1pf(expf(x)); }
 
 // one thread per (b, channel c) of xBC
