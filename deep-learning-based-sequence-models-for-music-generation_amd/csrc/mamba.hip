@@ -1627,20 +1627,38 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
     f32x4 dcs[2][2], dbs[2][2];
     zero22(dcs);
     zero22(dbs);
+    // a head's x / H / dH / dY chunks are loaded during the previous head's
+    // products (each head waited on its own loads: 68 % of wave cycles in
+    // SQ_WAIT_ANY at two waves per SIMD); unconditional loads from clamped rows
+    // (rows past nval are zeroed where they are used or written)
+    u32x4 pxr[2], phb[2], pdb[2], pdy[2];
+    auto prefetch = [&](int h2) {
+        const int64_t hd = kg.h + h2;
+        const int64_t slot2 = ((kg.b * a.nheads + hd) * nch + kg.c) * (int64_t)(P * N);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = tid + 256 * u, row = e >> 3, ch = e & 7, rr = min(row, nv - 1);
+            const int64_t grow = kg.b * a.L + kg.t0 + rr;
+            pxr[u] = *(const u32x4*)(xc + grow * a.ldxc + hd * P + ch * 8);
+            phb[u] = ld_state<SB>(states, slot2 + row * N + ch * 8);
+            pdb[u] = ld_state<SB>(dHx, slot2 + row * N + ch * 8);
+            pdy[u] = *(const u32x4*)(dY + grow * ldy + hd * P + ch * 8);
+        }
+    };
+    prefetch(0);
     for (int hh = 0; hh < hg; ++hh) {
     if (hh) __syncthreads();  // the previous head's last LDS reads are done
     Chunk k = kg;
     k.h = kg.h + hh;
     const float A = -expf(A_log[k.h]), Dh = Dp[k.h];
-    const int64_t slot = ((k.b * a.nheads + k.h) * nch + k.c) * (int64_t)(P * N);
     u32x4 xr[2];
     float hdh = 0.f;  // sum dH o H (the cum_last term)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         const int e = tid + 256 * u, row = e >> 3, ch = e & 7;
-        xr[u] = ld_chunk(a, k, xc, k.h * P, e);
+        xr[u] = row < k.nval ? pxr[u] : (u32x4){0u, 0u, 0u, 0u};
         // H / dH as bf16 (the MFMA operands); the cum_last term from the same values
-        const u32x4 hb = ld_state<SB>(states, slot + row * N + ch * 8), db = ld_state<SB>(dHx, slot + row * N + ch * 8);
+        const u32x4 hb = phb[u], db = pdb[u];
         {
             float hv[8], dv[8];
             unpack8(hb, hv);
@@ -1651,9 +1669,7 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
         *(u32x4*)(sHD + offd(row, ch)) = hb;
         *(u32x4*)(sHD + offd(row, 8 + ch)) = db;
         // dY rows are bf16 already: copied into the image as they are (zero past nval)
-        *(u32x4*)(sXY + offd(row, 8 + ch)) =
-            row < k.nval ? *(const u32x4*)(dY + (k.b * a.L + k.t0 + row) * ldy + k.h * P + ch * 8)
-                         : (u32x4){0u, 0u, 0u, 0u};
+        *(u32x4*)(sXY + offd(row, 8 + ch)) = row < k.nval ? pdy[u] : (u32x4){0u, 0u, 0u, 0u};
     }
     dt_cum(a, k, zx, dt_bias, A, sdt, scum, tid);
     if (tid < 64) sdcum[tid] = sddt[tid] = 0.f;
@@ -1670,6 +1686,7 @@ __global__ __launch_bounds__(256, 2) void grad_kernel(MambaArgs a, const bf16* _
         for (int q = 0; q < 8; ++q) v[q] *= sdt[row];
         *(u32x4*)(sXY + offd(row, e & 7)) = pack8(v);
     }
+    if (hh + 1 < hg) prefetch(hh + 1);
     // M = (C B^T) o L ; dM = dY XS^T (s <= t)
     f32x4 mt[2][2], dm[2][2];
     zero22(mt);
