@@ -467,6 +467,29 @@ def test_transpose_bf16(rows, cols, lds, ldd):
     assert bool((dst[:, rows:] == 7.0).all())  # nothing written past the rows
 
 
+def test_gemm_resid_ln_unfused_rejects_row_pitch():
+    """The unfused path of msq_gemm_resid_ln (fp32 operands) normalises C with
+    msq_layernorm_fwd, which reads C densely: a padded ldc (or ldy) is
+    rejected before anything is written."""
+    M, N, K = 8, 256, 64
+    g = torch.Generator().manual_seed(5)
+    a = torch.randn(M, K, generator=g).to(dev)
+    w = torch.randn(N, K, generator=g).to(dev)
+    bias, gamma, beta = (torch.randn(N, generator=g).to(dev) for _ in range(3))
+    res = torch.randn(M, N, generator=g).to(dev)
+    big = torch.full((M, N + 64), 7.0, device=dev)
+    y = torch.full((M, N), 7.0, device=dev)
+    with pytest.raises(RuntimeError, match="ldc == N"):
+        ops.gemm_resid_ln(a, w, big[:, :N], bias, res, gamma, beta, y)
+    bigy = torch.full((M, N + 64), 7.0, device=dev)
+    c = torch.full((M, N), 7.0, device=dev)
+    with pytest.raises(RuntimeError, match="ldy == N"):
+        ops.gemm_resid_ln(a, w, c, bias, res, gamma, beta, bigy[:, :N])
+    torch.cuda.synchronize()
+    assert bool((big == 7.0).all()) and bool((y == 7.0).all())
+    assert bool((bigy == 7.0).all()) and bool((c == 7.0).all())
+
+
 @pytest.mark.parametrize("M", [1, 7, 33, 64])
 @pytest.mark.parametrize("N,K", [(1024, 1024), (1024, 4096), (1000, 520), (256, 1024)])
 def test_gemm_resid_ln_matches_unfused(M, N, K):
