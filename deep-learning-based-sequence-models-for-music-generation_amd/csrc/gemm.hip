@@ -366,12 +366,15 @@ int dispatch_epi(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hipS
         case MSQ_EPI_NONE: return D(MSQ_EPI_NONE, float);
         case MSQ_EPI_BIAS: return D(MSQ_EPI_BIAS, float);
         case MSQ_EPI_BIAS_RELU: return D(MSQ_EPI_BIAS_RELU, float);
-        case MSQ_EPI_BIAS_RESID: return D(MSQ_EPI_BIAS_RESID, float);
+        // the aux operand is read as aux_dtype (bf16 residual streams included)
+        case MSQ_EPI_BIAS_RESID:
+            return aux_dtype == MSQ_BF16 ? D(MSQ_EPI_BIAS_RESID, bf16) : D(MSQ_EPI_BIAS_RESID, float);
         case MSQ_EPI_RELU_MASK:
             if (aux_dtype == MSQ_MASK1) return BF ? dispatch_bf16_t<MSQ_EPI_RELU_MASK, TC, mask1_t>(g, ta, tb, s) : 1;
             return aux_dtype == MSQ_BF16 ? D(MSQ_EPI_RELU_MASK, bf16) : D(MSQ_EPI_RELU_MASK, float);
         case MSQ_EPI_ACCUM: return D(MSQ_EPI_ACCUM, float);
-        case MSQ_EPI_BIAS_DROP_RESID: return D(MSQ_EPI_BIAS_DROP_RESID, float);
+        case MSQ_EPI_BIAS_DROP_RESID:
+            return aux_dtype == MSQ_BF16 ? D(MSQ_EPI_BIAS_DROP_RESID, bf16) : D(MSQ_EPI_BIAS_DROP_RESID, float);
     }
 #undef D
     return -1;
@@ -688,8 +691,14 @@ void tail_epi_launch(const GemmArgs& t, const float* tmp, int epi, int aux_dtype
         case MSQ_EPI_NONE: hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_NONE, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp); break;
         case MSQ_EPI_BIAS: hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_BIAS, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp); break;
         case MSQ_EPI_BIAS_RELU: hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_BIAS_RELU, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp); break;
-        case MSQ_EPI_BIAS_RESID: hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_BIAS_RESID, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp); break;
-        case MSQ_EPI_BIAS_DROP_RESID: hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_BIAS_DROP_RESID, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp); break;
+        case MSQ_EPI_BIAS_RESID:
+            if (aux_dtype == MSQ_BF16) hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_BIAS_RESID, TC, bf16>), dim3(nb), dim3(256), 0, s, t, tmp);
+            else hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_BIAS_RESID, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp);
+            break;
+        case MSQ_EPI_BIAS_DROP_RESID:
+            if (aux_dtype == MSQ_BF16) hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_BIAS_DROP_RESID, TC, bf16>), dim3(nb), dim3(256), 0, s, t, tmp);
+            else hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_BIAS_DROP_RESID, TC, float>), dim3(nb), dim3(256), 0, s, t, tmp);
+            break;
         case MSQ_EPI_RELU_MASK:
             if (aux_dtype == MSQ_MASK1) hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_RELU_MASK, TC, mask1_t>), dim3(nb), dim3(256), 0, s, t, tmp);
             else if (aux_dtype == MSQ_BF16) hipLaunchKernelGGL((tail_epi_kernel<MSQ_EPI_RELU_MASK, TC, bf16>), dim3(nb), dim3(256), 0, s, t, tmp);
@@ -758,6 +767,8 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
     MSQ_CHECK_ARG(epilogue >= MSQ_EPI_NONE && epilogue <= MSQ_EPI_BIAS_DROP_RESID, "msq_gemm: bad epilogue");
     MSQ_CHECK_ARG(p >= 0.f && p < 1.f, "msq_gemm_dropout: p must be in [0, 1)");
     MSQ_CHECK_ARG(aux || epilogue != MSQ_EPI_BIAS_DROP_RESID, "msq_gemm: epilogue needs aux");
+    MSQ_CHECK_ARG(aux_dtype == MSQ_F32 || aux_dtype == MSQ_BF16 || aux_dtype == MSQ_MASK1, "msq_gemm: bad aux_dtype %d",
+                  aux_dtype);
     MSQ_CHECK_ARG(!(epilogue == MSQ_EPI_ACCUM && c_dtype != MSQ_F32), "msq_gemm: ACCUM needs fp32 C");
     MSQ_CHECK_ARG(bias || (epilogue != MSQ_EPI_BIAS && epilogue != MSQ_EPI_BIAS_RELU),
                   "msq_gemm: epilogue needs bias (BIAS_RESID accepts NULL)");

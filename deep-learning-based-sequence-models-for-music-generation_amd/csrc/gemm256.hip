@@ -308,14 +308,21 @@ void dispatch_epi(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hip
         case MSQ_EPI_NONE: dispatch_t<MSQ_EPI_NONE, TC, float>(g, ta, tb, s); break;
         case MSQ_EPI_BIAS: dispatch_t<MSQ_EPI_BIAS, TC, float>(g, ta, tb, s); break;
         case MSQ_EPI_BIAS_RELU: dispatch_t<MSQ_EPI_BIAS_RELU, TC, float>(g, ta, tb, s); break;
-        case MSQ_EPI_BIAS_RESID: dispatch_t<MSQ_EPI_BIAS_RESID, TC, float>(g, ta, tb, s); break;
+        // the aux operand is read as aux_dtype (bf16 residual streams included)
+        case MSQ_EPI_BIAS_RESID:
+            if (aux_dtype == MSQ_BF16) dispatch_t<MSQ_EPI_BIAS_RESID, TC, bf16>(g, ta, tb, s);
+            else dispatch_t<MSQ_EPI_BIAS_RESID, TC, float>(g, ta, tb, s);
+            break;
         case MSQ_EPI_RELU_MASK:
             if (aux_dtype == MSQ_MASK1) dispatch_t<MSQ_EPI_RELU_MASK, TC, mask1_t>(g, ta, tb, s);
             else if (aux_dtype == MSQ_BF16) dispatch_t<MSQ_EPI_RELU_MASK, TC, bf16>(g, ta, tb, s);
             else dispatch_t<MSQ_EPI_RELU_MASK, TC, float>(g, ta, tb, s);
             break;
         case MSQ_EPI_ACCUM: dispatch_t<MSQ_EPI_ACCUM, TC, float>(g, ta, tb, s); break;
-        case MSQ_EPI_BIAS_DROP_RESID: dispatch_t<MSQ_EPI_BIAS_DROP_RESID, TC, float>(g, ta, tb, s); break;
+        case MSQ_EPI_BIAS_DROP_RESID:
+            if (aux_dtype == MSQ_BF16) dispatch_t<MSQ_EPI_BIAS_DROP_RESID, TC, bf16>(g, ta, tb, s);
+            else dispatch_t<MSQ_EPI_BIAS_DROP_RESID, TC, float>(g, ta, tb, s);
+            break;
     }
 }
 

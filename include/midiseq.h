@@ -114,8 +114,10 @@ int msq_layernorm_bwd_bias(float* dx_acc, void* dx_copy, int copy_dtype, float* 
  *   tb = 0: B stored [N,K] (K contiguous)     tb = 1: B stored [K,N]
  * dtype = MSQ_BF16: bf16 operands, fp32 accumulation on MFMA (fast path);
  * dtype = MSQ_F32 : fp32 operands and accumulation (exact/parity path).
- * c_dtype: output type (ACCUM requires fp32). aux is fp32 for BIAS_RESID,
- * aux_dtype-typed for RELU_MASK. Leading dims must be multiples of 8.        */
+ * c_dtype: output type (ACCUM requires fp32). aux (the residual of
+ * BIAS_RESID / BIAS_DROP_RESID, the mask source of RELU_MASK) is read as
+ * aux_dtype: MSQ_F32 or MSQ_BF16 (MSQ_MASK1 bits for RELU_MASK / BIAS_RELU).
+ * Leading dims must be multiples of 8.                                      */
 int msq_gemm(int dtype, int ta, int tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
              int64_t strideA, const void* B, int64_t ldb, int64_t strideB, void* C, int c_dtype, int64_t ldc,
              int64_t strideC, int64_t batch, int epilogue, const float* bias, const void* aux, int aux_dtype,

@@ -423,6 +423,33 @@ def test_adam_matches_torch():
     assert torch.equal(sh.cpu(), P.cpu().bfloat16())
 
 
+@pytest.mark.parametrize("route", list(ROUTES))
+def test_gemm_resid_epilogues_bf16_aux(route):
+    """BIAS_RESID / BIAS_DROP_RESID with a bf16 residual (aux_dtype MSQ_BF16)
+    on every kernel family, M with a tail (3000 = 11 x 256 + 184): the aux is
+    read as bf16 everywhere (it was read as fp32 outside the skinny kernel:
+    wrong columns, and past the end of the buffer on the last rows)."""
+    from oracle import dropout as odrop
+    g = torch.Generator().manual_seed(31)
+    M, N, K = 3000, 1024, 512
+    a = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * 0.05).bfloat16()
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g).bfloat16()
+    base = a.float() @ w.float().t() + bias
+    A, W, bi, R = a.to(dev), w.to(dev), bias.to(dev), res.to(dev)
+    with ops.gemm_route(ROUTES[route]):
+        o = ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_BIAS_RESID, bias=bi, aux=R)
+        assert _rel(o, base + res.float()) < 2e-3
+        ob = ops.gemm(A, W, out_dtype=torch.bfloat16, epilogue=L.EPI_BIAS_RESID, bias=bi, aux=R)
+        assert _rel(ob.float(), base + res.float()) < 1e-2
+        seed, site, p = 5, 9, 0.2
+        o = ops.gemm(A, W, out_dtype=torch.float32, epilogue=L.EPI_BIAS_RESID, bias=bi, aux=R, drop=(seed, site, p))
+        keep = torch.from_numpy(odrop.keep(seed, site, M, N, p))
+        ref = res.float() + torch.where(keep, base * odrop.scale(p), torch.zeros(()))
+        assert _rel(o, ref) < 2e-3
+
+
 @pytest.mark.parametrize("epi", ["drop", "relu_mask", "none"])
 def test_gemm256_tail_rows_split(epi):
     """M = 64*256 + 100 rows, N = 1024: the 256 tile runs rows [0, 16384) and
