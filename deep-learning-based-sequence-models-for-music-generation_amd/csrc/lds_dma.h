@@ -9,7 +9,8 @@
 // helpers counts its own DMA with explicit `s_waitcnt vmcnt(N)` before a
 // barrier, so that wait was never needed for correctness.
 // M0 carries the wave's LDS destination base; it is declared clobbered (the
-// compiler loads M0 itself before each of its own M0 users).
+// compiler loads M0 itself before each of its own M0 users). One wait state
+// between the M0 write and the LDS-DMA that reads it (s_nop 0).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -20,17 +21,17 @@
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rs, const void* dst, uint32_t voff) {
     const uint32_t m =
         __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)dst);
-    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(rs) : "m0");
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(rs) : "m0");
 }
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rs, const __attribute__((address_space(3))) char* dst,
                                           uint32_t voff) {
     const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
-    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(rs) : "m0");
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(rs) : "m0");
 }
 // 4 B per lane: lane l's word lands at dst + 4 l
 __device__ __forceinline__ void lds_dma4(__amdgpu_buffer_rsrc_t rs, const void* dst, uint32_t voff) {
     const uint32_t m =
         __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)dst);
-    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(rs) : "m0");
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(rs) : "m0");
 }
 #pragma clang diagnostic pop
