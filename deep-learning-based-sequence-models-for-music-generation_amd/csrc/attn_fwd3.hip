@@ -77,7 +77,7 @@ __global__ __launch_bounds__(NT, 1) void flash_fwd3_kernel(AttnArgs a, bf16* __r
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int S = (int)a.S, H = (int)a.H;
     const int64_t ldq = a.ldq;
-    const Blk3 blk = xcd_blk3(a.xcd);
+    const Blk3 blk = xcd_blk3_heavy_first(a.xcd);
     const int qb = blk.x;  // 0 = last (heaviest) 256 queries
     const int h = blk.y, b = blk.z;
     const int qhi = S - QB * qb, i0 = qhi - QB;  // queries [max(i0, 0), qhi)

@@ -91,6 +91,30 @@ __device__ __forceinline__ Blk3 xcd_blk3(bool remap) {
     return r;
 }
 
+// the same with the x blocks outermost inside each XCD's contiguous range of
+// logical ids (when the range holds whole (y, z) pairs): for grids whose x
+// block 0 is the heaviest (the attention forward's last query block), every
+// XCD runs its pairs' heavy blocks first and the light ones last, so its CUs
+// finish together (longest first). The key/value pass keeps xcd_blk3: its
+// blocks of one (b, h) share the query rows they stream, which the
+// interleaved order keeps in L2 together (heavy-first measured slower there
+// in the step)
+__device__ __forceinline__ Blk3 xcd_blk3_heavy_first(bool remap) {
+    if (!remap) return xcd_blk3(false);
+    const int nx = gridDim.x, ny = gridDim.y, n = nx * ny * (int)gridDim.z;
+    const int lin = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+    int L = __builtin_amdgcn_readfirstlane(xcd_remap(lin, n));
+    if (n % 8 == 0 && (n / 8) % nx == 0) {
+        const int q = n / 8, start = L / q * q, j = L - start, P = q / nx;
+        L = start + (j % P) * nx + j / P;
+    }
+    Blk3 r;
+    r.x = L % nx;
+    r.y = (L / nx) % ny;
+    r.z = L / (nx * ny);
+    return r;
+}
+
 // ---- dropout (nn.Dropout, model_transformer.py:51,80,101) ----
 // Counter-based keep mask: element (row, col) of dropout site `site` under the
 // step seed `seed` is kept iff drop_bits(drop_row(drop_base(seed, site), row),

@@ -32,6 +32,12 @@ struct GemmArgs {
     // column sums of the written C (msq_gemm_colsum): per-(M-tile, wave-row)
     // partials [tiles_m * 2][N], reduced in a fixed order afterwards
     float* cs_ws;
+    // bytes at ws (msq_gemm_ex's workspace) for the persistent tile's K-split
+    // tail: its last tail_tiles tiles run as tail_s K slices of tail_kst
+    // k-steps into fp32 partials at ws, summed with the epilogue afterwards
+    // (gemm256p.hip; 0 = off)
+    int64_t ws_bytes;
+    int tail_tiles, tail_s, tail_kst;
 };
 
 // bytes of the split-K partial workspace an ACCUM product with this split needs
@@ -135,6 +141,8 @@ bool gemm256_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dt
 bool gemm256p_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype, hipStream_t s);
 // whether gemm256p_launch would take this product
 bool gemm256p_applies(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_dtype);
+// workspace bytes of the persistent tile's K-split tail for this product (0: none)
+size_t gemm256p_tail_ws_bytes(int64_t M, int64_t N, int64_t K, int epi, int aux_dtype);
 // persistent tile with the column-sum partials of gemm256_colsum_launch (g.cs_ws set,
 // reduced by the caller); false when it does not apply
 bool gemm256p_colsum_launch(GemmArgs g, int ta, int tb, int epi, int aux_dtype, hipStream_t s);

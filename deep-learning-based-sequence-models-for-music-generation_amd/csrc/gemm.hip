@@ -734,9 +734,13 @@ extern "C" int64_t msq_gemm_workspace_size(int dtype, int ta, int tb, int64_t M,
     if (dtype != MSQ_BF16 || M <= 0 || N <= 0 || K <= 0 || batch <= 0) return 0;
     if (epilogue != MSQ_EPI_ACCUM) {  // the split-K tail of a wave-quantisation split
         if (M <= 64 && !ta && !tb && batch == 1) return (int64_t)skinny_ws_bytes(M, N, K);  // skinny split-K
-        if (batch != 1 || M % 256 == 0 || M <= 256 || M <= 64) return 0;
+        if (batch != 1 || M <= 64) return 0;
+        // the persistent tile's K-split tail (its aux type is not known here:
+        // sized as for an fp32 / bf16 aux, which is what it runs with)
+        const int64_t pt = (int64_t)gemm256p_tail_ws_bytes(M, N, K, epilogue, MSQ_F32);
+        if (M % 256 == 0 || M <= 256) return pt;
         const TailPlan tp = plan_tail(M % 256, N, K);
-        return tp.ksplit > 1 ? (int64_t)(tp.tmp_bytes + tp.part_bytes) : 0;
+        return std::max<int64_t>(pt, tp.ksplit > 1 ? (int64_t)(tp.tmp_bytes + tp.part_bytes) : 0);
     }
     GemmArgs g{};
     g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.batch = (int)batch;
@@ -812,6 +816,7 @@ extern "C" int msq_gemm_ex(int dtype, int ta, int tb, int64_t M, int64_t N, int6
     // partial tiles go to ws when it is large enough, else fp32 atomics into C
     plan128_ksplit(g, dtype, epilogue);
     g.ws = (float*)ws;
+    g.ws_bytes = ws ? ws_bytes : 0;
     hipStream_t s = (hipStream_t)stream;
     if (aux && aux_dtype == MSQ_MASK1 && epilogue == MSQ_EPI_BIAS_RELU) {
         // the persistent tile writes the mask in its epilogue; elsewhere the

@@ -257,6 +257,42 @@ __device__ __forceinline__ void p_epilogue(const GemmArgs& g, __amdgpu_buffer_rs
     }
 }
 
+// tile id -> (m0, n0): 8 row panels share each sweep over the columns
+__device__ __forceinline__ void p_tile_mn(const GemmArgs& g, int id, int64_t& m0, int64_t& n0) {
+    const int GROUP = 8;
+    const int per_group = GROUP * g.tiles_n;
+    const int grp = id / per_group, first_m = grp * GROUP;
+    const int gsz = min(g.tiles_m - first_m, GROUP);
+    m0 = (int64_t)(first_m + (id % per_group) % gsz) * 256;
+    n0 = (int64_t)((id % per_group) / gsz) * 256;
+}
+
+// Wave quantisation: M = B*S rows leave ntiles % G tiles (at cfg 2 the
+// 192-row last row panel: 4 tiles at N = 1 024) for a last round on a few
+// CUs. With a workspace those tail tiles run as K slices, one per idle CU:
+// work item id >= n_full is slice (id - n_full) % tail_s of tail tile
+// n_full + (id - n_full) / tail_s, stored as an fp32 partial 256 x 256 tile
+// at ws + (id - n_full) * 64 K floats; p_tail_fixup_kernel sums each tile's
+// slices in order and applies the epilogue. Every workgroup has at most one
+// slice and it is its last item (tail_tiles * tail_s <= G).
+template <int EPI, typename TC, typename TX>
+__global__ __launch_bounds__(256) void p_tail_fixup_kernel(GemmArgs g) {
+    const int n_full = g.tiles_m * g.tiles_n - g.tail_tiles;
+    constexpr int64_t QPT = 256 * 64;  // 4-column quads per tile
+    const int64_t total = (int64_t)g.tail_tiles * QPT;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+        const int tt = (int)(e / QPT), q = (int)(e % QPT), r = q >> 6, c = (q & 63) * 4;
+        int64_t m0, n0;
+        p_tile_mn(g, n_full + tt, m0, n0);
+        const int64_t m = m0 + r, n = n0 + c;
+        if (m >= g.M || n >= g.N) continue;
+        const float* P = g.ws + (int64_t)tt * g.tail_s * 65536 + r * 256 + c;
+        f32x4 v = load4(P);
+        for (int sl = 1; sl < g.tail_s; ++sl) v += load4(P + (int64_t)sl * 65536);
+        epi_apply<EPI, TC, TX>(g, (TC*)g.C, (const TX*)g.aux, m, n, v);
+    }
+}
+
 template <int TA, int TB, int EPI, typename TC, typename TX, int CSM = 0>
 __global__ __launch_bounds__(NT, 1) void gemm256p_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -267,18 +303,13 @@ __global__ __launch_bounds__(NT, 1) void gemm256p_kernel(GemmArgs g) {
     const int wr = w >> 2, wc = w & 3;
     const int ntiles = g.tiles_m * g.tiles_n;
     const int G = gridDim.x;
-    // tile id of round q for this workgroup: q * G + widx; blocks sharing an
-    // XCD take consecutive ids (T1), which the grouped order below turns into
-    // shared A / B panels in that XCD's L2
+    // item id of round q for this workgroup: q * G + widx; blocks sharing an
+    // XCD take consecutive ids (T1), which the grouped order turns into
+    // shared A / B panels in that XCD's L2. Items past n_full are the K
+    // slices of the tail tiles (p_tail_fixup_kernel)
     const int widx = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, G));
-    auto tile_mn = [&](int id, int64_t& m0, int64_t& n0) {
-        const int GROUP = 8;
-        const int per_group = GROUP * g.tiles_n;
-        const int grp = id / per_group, first_m = grp * GROUP;
-        const int gsz = min(g.tiles_m - first_m, GROUP);
-        m0 = (int64_t)(first_m + (id % per_group) % gsz) * 256;
-        n0 = (int64_t)((id % per_group) / gsz) * 256;
-    };
+    const int n_full = ntiles - g.tail_tiles;
+    const int n_items = n_full + g.tail_tiles * g.tail_s;
 
     const __amdgpu_buffer_rsrc_t ra = make_rsrc((const char*)g.A, g.a_ext);
     const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)g.B, g.b_ext);
@@ -318,36 +349,51 @@ __global__ __launch_bounds__(NT, 1) void gemm256p_kernel(GemmArgs g) {
         }
     }
 
-    const int nk = (int)((g.K + 63) / 64);
+    const int nkt = (int)((g.K + 63) / 64);
+    // item -> tile origin, first k-step, k-steps
+    auto item = [&](int id, int64_t& m0, int64_t& n0, int& kb, int& nkk) {
+        if (id < n_full) {
+            p_tile_mn(g, id, m0, n0);
+            kb = 0;
+            nkk = nkt;
+        } else {
+            const int u = id - n_full;
+            p_tile_mn(g, n_full + u / g.tail_s, m0, n0);
+            kb = (u % g.tail_s) * g.tail_kst;
+            nkk = min(g.tail_kst, nkt - kb);
+        }
+    };
     Stage<TA == 0> sa;
     Stage<TB == 0> sb;
     auto slot = [&](int b, int s) { return smem + (b * 4 + s) * HALF; };
-    auto issue = [&](int u, int h) {
-        const int64_t k0 = (int64_t)u * 64;
+    // k-step u of an item whose k-steps start at kb (slot parity by u)
+    auto issue = [&](int kb, int u, int h) {
+        const int64_t k0 = (int64_t)(kb + u) * 64;
         lds_t* dst = slot(u & 1, h);
         if (h == 0) sa.issue(ra, dst, 0, k0, g.K - k0, w);
         else if (h == 1) sb.issue(rb, dst, 0, k0, g.K - k0, w);
         else if (h == 2) sa.issue(ra, dst, 1, k0, g.K - k0, w);
         else sb.issue(rb, dst, 1, k0, g.K - k0, w);
     };
-    auto prologue = [&](int64_t m0, int64_t n0) {
+    auto prologue = [&](int64_t m0, int64_t n0, int kb, int nkk) {
         sa.init(m0, g.M, g.lda, w, lane);
         sb.init(n0, g.N, g.ldb, w, lane);
-        issue(0, 0);
-        issue(0, 1);
-        issue(0, 2);
-        issue(0, 3);
-        if (nk > 1) {
-            issue(1, 0);
-            issue(1, 1);
+        issue(kb, 0, 0);
+        issue(kb, 0, 1);
+        issue(kb, 0, 2);
+        issue(kb, 0, 3);
+        if (nkk > 1) {
+            issue(kb, 1, 0);
+            issue(kb, 1, 1);
         }
     };
 
     int id = widx;
-    if (id >= ntiles) return;
+    if (id >= n_items) return;
     int64_t m0, n0;
-    tile_mn(id, m0, n0);
-    prologue(m0, n0);
+    int kb, nk;
+    item(id, m0, n0, kb, nk);
+    prologue(m0, n0, kb, nk);
     order_fence();
     // the S stores a previous tile's epilogue would have left outstanding (to
     // distinct, non-adjacent dropped offsets: identical ones would be merged
@@ -376,7 +422,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256p_kernel(GemmArgs g) {
         }                                                                                               \
         const int su = (Q < 2) ? t + 1 : t + 2;                                                         \
         if (su < nk) {                                                                                  \
-            issue(su, (Q + 2) & 3);                                                                     \
+            issue(kb, su, (Q + 2) & 3);                                                                 \
             vm_wait<WAITN>();                                                                           \
         } else {                                                                                        \
             vm_wait0();                                                                                 \
@@ -431,19 +477,39 @@ __global__ __launch_bounds__(NT, 1) void gemm256p_kernel(GemmArgs g) {
         // every wave has read its last fragments: the next tile's prologue may
         // overwrite the LDS slots while this tile's epilogue runs
         const int nid = id + G;
-        const bool more = nid < ntiles;
+        const bool more = nid < n_items;
         int64_t m1 = 0, n1 = 0;
+        int kb1 = 0, nk1 = 0;
         if (more) {
-            tile_mn(nid, m1, n1);
-            prologue(m1, n1);
+            item(nid, m1, n1, kb1, nk1);
+            prologue(m1, n1, kb1, nk1);
         }
         order_fence();
-        p_epilogue<EPI, TC, TX, CSM>(g, rc, rx, rbias, rcs, m0, n0, wr, wc, lane, acc);
+        if (id < n_full) {
+            p_epilogue<EPI, TC, TX, CSM>(g, rc, rx, rbias, rcs, m0, n0, wr, wc, lane, acc);
+        } else {
+            // a tail slice (always the workgroup's last item): its fp32 partial
+            // tile, buffer stores from one lane offset (constant soffsets)
+            const __amdgpu_buffer_rsrc_t rw = make_rsrc((const char*)(g.ws + (int64_t)(id - n_full) * 65536), 65536u * 4);
+            const uint32_t lo = (uint32_t)(((wr * 64 + (lane & 15)) * 256 + wc * 32 + 4 * (lane >> 4)) * 4);
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a][b][i][j]), rw, lo,
+                                                                   ((a * 128 + i * 16) * 256 + b * 128 + j * 16) * 4, 0);
+        }
         order_fence();
         if (!more) break;
         id = nid;
         m0 = m1;
         n0 = n1;
+        kb = kb1;
+        nk = nk1;
     }
 #undef MSQ_PPHASE
 }
@@ -471,6 +537,13 @@ void launch_p(const GemmArgs& g, hipStream_t s) {
     }
     const int ntiles = g.tiles_m * g.tiles_n;
     hipLaunchKernelGGL(k, dim3(std::min(ntiles, num_cus())), dim3(NT), 8 * HALF, s, g);
+    if constexpr (CSM == 0) {
+        if (g.tail_tiles > 0) {
+            const int64_t total = (int64_t)g.tail_tiles * 256 * 64;
+            hipLaunchKernelGGL((p_tail_fixup_kernel<EPI, TC, TX>), dim3((unsigned)std::min<int64_t>((total + 255) / 256, 2048)),
+                               dim3(256), 0, s, g);
+        }
+    }
 }
 
 template <int EPI, typename TC, typename TX>
@@ -508,6 +581,34 @@ void dispatch_p(const GemmArgs& g, int ta, int tb, int epi, int aux_dtype, hipSt
 }
 }  // namespace
 
+// the K-split tail of a persistent launch (p_tail_fixup_kernel): on when the
+// last round holds at most a quarter of the grid's workgroups, the epilogue
+// is one p_tail_fixup_kernel applies (no mask-bit writes, no column sums),
+// and K spans >= 8 k-steps; tail_s slices of >= 4 k-steps, tail_tiles *
+// tail_s <= G. Returns the partials' bytes (0: off)
+struct PTail {
+    int tiles, s, kst;
+};
+static size_t p_tail_plan(int64_t M, int64_t N, int64_t K, int epi, int aux_dtype, PTail& t) {
+    t = PTail{0, 0, 0};
+    if (aux_dtype == MSQ_MASK1 || epi == MSQ_EPI_ACCUM) return 0;
+    const int64_t ntiles = ((M + 255) / 256) * ((N + 255) / 256);
+    const int64_t G = std::min<int64_t>(ntiles, num_cus());
+    const int64_t rem = ntiles % G, nk = (K + 63) / 64;
+    if (rem == 0 || rem * 4 > G || nk < 8) return 0;
+    int64_t S = std::min<int64_t>(std::min<int64_t>(G / rem, nk / 4), 32);
+    if (S < 2) return 0;
+    const int64_t kst = (nk + S - 1) / S;
+    S = (nk + kst - 1) / kst;
+    t = PTail{(int)rem, (int)S, (int)kst};
+    return (size_t)rem * S * 65536 * 4;
+}
+
+size_t gemm256p_tail_ws_bytes(int64_t M, int64_t N, int64_t K, int epi, int aux_dtype) {
+    PTail t;
+    return p_tail_plan(M, N, K, epi, aux_dtype, t);
+}
+
 // C / aux / bias preconditions of the persistent tile and its descriptor extents
 static bool p_prepare(GemmArgs& g, int ta, int tb, int epi, int c_dtype, int aux_dtype) {
     if (epi == MSQ_EPI_ACCUM || g.batch != 1) return false;
@@ -528,6 +629,15 @@ static bool p_prepare(GemmArgs& g, int ta, int tb, int epi, int c_dtype, int aux
     if (!gemm256_plan(g, ta, tb, epi) || g.ksplit != 1) return false;
     g.c_ext = (uint32_t)cext;
     g.x_ext = (uint32_t)xext;
+    PTail t;
+    const size_t tb_bytes = p_tail_plan(g.M, g.N, g.K, epi, aux_dtype, t);
+    if (tb_bytes && g.ws && g.ws_bytes >= (int64_t)tb_bytes && ((uintptr_t)g.ws % 16) == 0) {
+        g.tail_tiles = t.tiles;
+        g.tail_s = t.s;
+        g.tail_kst = t.kst;
+    } else {
+        g.tail_tiles = g.tail_s = g.tail_kst = 0;
+    }
     return true;
 }
 
@@ -547,6 +657,7 @@ bool gemm256p_launch(GemmArgs g, int ta, int tb, int epi, int c_dtype, int aux_d
 bool gemm256p_colsum_launch(GemmArgs g, int ta, int tb, int epi, int aux_dtype, hipStream_t s) {
     if (ta != 0 || (epi != MSQ_EPI_NONE && epi != MSQ_EPI_RELU_MASK)) return false;
     if (!p_prepare(g, ta, tb, epi, MSQ_BF16, aux_dtype)) return false;
+    g.tail_tiles = g.tail_s = g.tail_kst = 0;  // (the column sums need every tile's epilogue)
     if ((int64_t)g.tiles_m * 2 * g.N * 4 >= (int64_t)OOB) return false;
     const bool bx = aux_dtype == MSQ_BF16, b1 = aux_dtype == MSQ_MASK1;
     if (tb == 0) {

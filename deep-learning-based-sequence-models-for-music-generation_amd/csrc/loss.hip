@@ -450,37 +450,23 @@ __global__ __launch_bounds__(256) void rowlse_kernel(LossArgs a, const float* __
     const float* cl = clp + b * Vp;
     const float* w = wtp + (int64_t)bk * Vp;
     float m = -INFINITY, s = 0.f;
-    // four chunks per lane in flight (the loads of a chunk past the range
-    // re-read the range's last chunk and are masked out): the same update
-    // order per lane as one chunk at a time
-    constexpr int U = 4;
-    const int vlast = (hi - 1) & ~(N - 1);
-    for (int v0 = (lo & ~(N - 1)) + lane * N; v0 < hi; v0 += U * 64 * N) {
-        float x[U][N], c[U][N], ww[U][N];
+    for (int v = (lo & ~(N - 1)) + lane * N; v < hi; v += 64 * N) {
+        float x[N], c[N], ww[N], z[N];
+        ldv<T, N>(o + v, x);
+        ldf<N>(cl + v, c);
+        ldf<N>(w + v, ww);
+        float mm = m;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int vc = min(v0 + u * 64 * N, vlast);
-            ldv<T, N>(o + vc, x[u]);
-            ldf<N>(cl + vc, c[u]);
-            ldf<N>(w + vc, ww[u]);
+        for (int i = 0; i < N; ++i) {
+            z[i] = (v + i >= lo && v + i < hi) ? (c[i] - x[i]) * ww[i] * L2E : -INFINITY;
+            mm = fmaxf(mm, z[i]);
         }
+        if (mm != -INFINITY) {
+            float e = m == -INFINITY ? 0.f : s * __builtin_amdgcn_exp2f(m - mm);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int v = v0 + u * 64 * N;
-            float z[N];
-            float mm = m;
-#pragma unroll
-            for (int i = 0; i < N; ++i) {
-                z[i] = (v + i >= lo && v + i < hi) ? (c[u][i] - x[u][i]) * ww[u][i] * L2E : -INFINITY;
-                mm = fmaxf(mm, z[i]);
-            }
-            if (mm != -INFINITY) {
-                float e = m == -INFINITY ? 0.f : s * __builtin_amdgcn_exp2f(m - mm);
-#pragma unroll
-                for (int i = 0; i < N; ++i) e += __builtin_amdgcn_exp2f(z[i] - mm);
-                s = e;
-                m = mm;
-            }
+            for (int i = 0; i < N; ++i) e += __builtin_amdgcn_exp2f(z[i] - mm);
+            s = e;
+            m = mm;
         }
     }
 #pragma unroll

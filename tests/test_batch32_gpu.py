@@ -13,7 +13,13 @@ synthetic batch against 32 TrainSteps of the same model on each row alone:
 * the flat gradient equals the mean of the 32 per-row gradients (norm-relative
   < 1e-2, cosine > 0.9999: the per-row products are the same kernels, the
   weight gradients sum the rows in another order);
-* the logits rows of b = 0 and b = 31 equal their B = 1 forwards (1e-3 of max).
+* the logits rows of b = 0 and b = 31 equal their B = 1 forwards (1e-3 of max),
+  except the last (B*S) % 256 window positions of b = 31: those rows of the
+  layer products fall in the persistent GEMM's partial last round, which sums
+  them over K slices (csrc/gemm256p.hip), in another order than the B = 1
+  run's whole tiles, so they (and the logits they feed) agree to bf16
+  rounding through 8 layers (2e-2 of max); causal attention keeps every
+  earlier position's logits within 1e-3.
 Then the attention keep words of b = 31 (dropout p = 0.01, S = 2054) against
 oracle/dropout.py bit for bit."""
 import numpy as np
@@ -22,6 +28,7 @@ import torch
 
 from oracle import dropout as odrop
 from midiseq import ops
+from midiseq.config import N_META
 from midiseq.transformer import Transformer, TransformerConfig, DROP_ATTN
 from midiseq.train_parallel import TrainStep, SyntheticMIDI
 
@@ -38,6 +45,8 @@ def test_b32_step_equals_mean_of_rows():
     g32 = st.grads.clone()
     logits32 = m.engine.acts(B, T).logits.view(B, T, -1)[:, :, :m.cfg.vocab_size]
     rows = {b: logits32[b].float().clone() for b in (0, B - 1)}
+    S = T + N_META
+    t_cut = T - (B * S) % 256  # the partial-round rows of b = B-1 start at this token position
     gsum = torch.zeros_like(g32)
     losses = []
     lerr = {}
@@ -46,7 +55,10 @@ def test_b32_step_equals_mean_of_rows():
         gsum += st.grads
         if b in rows:
             l1 = m.engine.acts(1, T).logits.view(1, T, -1)[0, :, :m.cfg.vocab_size].float()
-            lerr[b] = ((l1 - rows[b]).abs().max() / rows[b].abs().max()).item()
+            scale = rows[b].abs().max()
+            lerr[b] = ((l1[:t_cut] - rows[b][:t_cut]).abs().max() / scale).item()
+            if b == B - 1:
+                lerr["tail"] = ((l1[t_cut:] - rows[b][t_cut:]).abs().max() / scale).item()
     torch.cuda.synchronize()
     gmean = gsum / B
     d = (g32.double() - gmean.double())
@@ -57,7 +69,7 @@ def test_b32_step_equals_mean_of_rows():
           f"logit rows err {lerr}")
     assert abs(loss - lm) <= 1e-4 * abs(lm)
     assert nr < 1e-2 and cos > 0.9999, (nr, cos)
-    assert all(v <= 1e-3 for v in lerr.values()), lerr
+    assert lerr[0] <= 1e-3 and lerr[B - 1] <= 1e-3 and lerr["tail"] <= 2e-2, lerr
 
 
 def test_attn_keep_words_at_b31():

@@ -16,6 +16,6 @@ for r in 1 2; do
     env $ev timeout -k 10 300 python -u bench.py --steps 10 --no-cpu-baseline --no-extra > gpurun_out/$tag/$v$r.json 2> gpurun_out/$tag/$v$r.err || { echo "bench $v failed"; tail -5 gpurun_out/$tag/$v$r.err; exit 1; }
     python -c "
 import json; d=json.load(open('gpurun_out/$tag/$v$r.json'))
-print('$v$r', d['ms_per_step'], {k: v['ms_per_step'] for k, v in d['classes'].items() if v['ms_per_step'] > 1.0})"
+print('$v$r' + (' (twin)' if '$v' == 'A' else ' (tree)'), d['ms_per_step'], {k: v['ms_per_step'] for k, v in d['classes'].items() if v['ms_per_step'] > 1.0})"
   done
 done
